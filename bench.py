@@ -1,0 +1,256 @@
+#!/usr/bin/env python3
+"""bench.py — BASELINE.json metric: geodesic-steps·pixels/s at 3840x2160 with a
+2048-step budget (config 3 on one GPU; config 4 = the same frame row-sharded
+over N GPUs with an RCCL gather to rank 0).
+
+One "step" = one frame: every rank renders its interleaved row bands of the
+4K frame with the HIP kernel (geo_render_bands), then (N > 1) rank 0 gathers
+the bands over RCCL and reassembles the frame for present.  Gathers run on
+RCCL's stream, double-buffered, so frame n's gather overlaps frame n+1's
+compute.  value = executed RK4 main-loop steps of all ranks / max-over-ranks
+wall time of the K timed frames (inputs resident in HBM, sky uploaded once).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+  torchrun --nproc-per-node N bench.py --gpus N ...
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+PEAK_FP32_TFLOPS = 157.3  # MI355X FP32 vector peak (MI355X_MICROARCH.md, spec)
+FLOPS_PER_EVAL = 40  # one RK4 evaluation of u'' = -u + 1.5 rs u^2
+NEWTON_EVALS = 3  # per sphere crossing (sphere_ray_tracer.rs:129)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--config", default="cfg3_4k")
+    p.add_argument("--band-rows", type=int, default=16)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-threads", type=int, default=16)
+    p.add_argument("--cpu-row-step", type=int, default=4)
+    p.add_argument("--mode", default="direct", choices=["direct", "fan"])
+    return p.parse_args()
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    import schwarzschild_raytracer_wgpu_amd as g
+    from schwarzschild_raytracer_wgpu_amd.scenes import CONFIGS, make_sky
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    cfg = CONFIGS[args.config]
+    W, H = cfg.width, cfg.height
+    obs = g.Observer(cfg.rs, cfg.fov, W, H)
+    obs.set_position(*cfg.position)
+    obs.set_camera(*cfg.camera)
+    obs.set_energy(cfg.energy)
+    frame = obs.calc_transformation_pipeline()
+    mode = g.GEO_MODE_FAN if args.mode == "fan" else g.GEO_MODE_DIRECT
+    scene = g.make_scene(cfg.rs, cfg.sphere_r, obs.get_radial_position(), cfg.step, cfg.max_steps, mode)
+    sky = make_sky(cfg.sky, cfg.sky_size)
+    ctx = g.Context(local)
+    ctx.set_sky(sky)
+    if mode == g.GEO_MODE_FAN:
+        ctx.solve_ray_fan(cfg.sphere_r, cfg.rs, cfg.max_steps, cfg.step, 400, obs.get_radial_position())
+
+    # interleaved row bands: rank g owns bands g, g+N, ... (balances the centre-heavy frame)
+    B = args.band_rows
+    nb_total = (H + B - 1) // B
+    nb_max = (nb_total + world - 1) // world
+    nb_mine = len(range(rank, nb_total, world))
+    band_bytes = B * W * 4
+    bufs = [torch.empty(nb_max * band_bytes, dtype=torch.uint8, device=dev) for _ in range(2)]
+    steps_ctr = torch.zeros(1, dtype=torch.int64, device=dev)
+
+    def render(buf, **kw):
+        ctx.render_bands(frame, scene, W, H, B, rank, world, nb_mine, buf, **kw)
+
+    # untimed diagnostic pass: per-pixel steps + mask give the RK4 evaluations
+    # per launch (main-loop steps + 3 Newton evaluations per sphere crossing)
+    diag_mask = torch.zeros(nb_max * B * W, dtype=torch.uint8, device=dev)
+    diag_steps = torch.zeros(nb_max * B * W, dtype=torch.int32, device=dev)
+    diag_ctr = torch.zeros(1, dtype=torch.int64, device=dev)
+    render(bufs[0], out_mask=diag_mask, out_steps=diag_steps, steps_total=diag_ctr)
+    torch.cuda.synchronize()
+    n_valid = nb_mine * B * W
+    st = diag_steps[: n_valid].to(torch.int64)
+    hits = int(((diag_mask[: n_valid] == 0) & (st > 0)).sum().item())
+    # clipped rows of the last band are not written: count rows that exist
+    rows_mine = sum(min(B, H - b * B) for b in range(rank, nb_total, world))
+    steps_diag = int(diag_ctr.item())
+    evals_per_launch = steps_diag + NEWTON_EVALS * hits
+
+    full = None
+    recv = None
+    if world > 1 and rank == 0:
+        full = torch.empty(nb_total * band_bytes, dtype=torch.uint8, device=dev)
+        recv = [[torch.empty(nb_max * band_bytes, dtype=torch.uint8, device=dev) for _ in range(world)]
+                for _ in range(2)]
+    works = [None, None]
+
+    def one_frame(i, ev=None):
+        slot = i % 2
+        if works[slot] is not None:
+            works[slot].wait()
+            works[slot] = None
+            if rank == 0:
+                assemble(slot)
+        if ev is not None:
+            ev[0].record()
+        render(bufs[slot], steps_total=steps_ctr)
+        if ev is not None:
+            ev[1].record()
+        if world > 1:
+            works[slot] = dist.gather(bufs[slot], gather_list=recv[slot] if rank == 0 else None, dst=0,
+                                      async_op=True)
+
+    def assemble(slot):
+        fv = full.view(nb_total, band_bytes)
+        for r in range(world):
+            n = len(range(r, nb_total, world))
+            fv[r::world] = recv[slot][r].view(nb_max, band_bytes)[:n]
+
+    def drain():
+        for s in (0, 1):
+            if works[s] is not None:
+                works[s].wait()
+                works[s] = None
+                if rank == 0:
+                    assemble(s)
+
+    for i in range(args.warmup):
+        one_frame(i)
+    drain()
+    torch.cuda.synchronize()
+    steps_ctr.zero_()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        one_frame(i, evs[i])
+    drain()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    kernel_ms = sorted(a.elapsed_time(b) for a, b in evs)
+    kernel_ms_avg = sum(kernel_ms) / len(kernel_ms)
+
+    steps_done = int(steps_ctr.item())
+    if steps_done != steps_diag * args.steps:
+        raise SystemExit(f"step counter mismatch: {steps_done} vs {steps_diag} x {args.steps}")
+    stats = torch.tensor([elapsed, kernel_ms_avg], dtype=torch.float64, device=dev)
+    tot = torch.tensor([steps_done, rows_mine * W * args.steps, evals_per_launch], dtype=torch.int64, device=dev)
+    if world > 1:
+        dist.all_reduce(stats, op=dist.ReduceOp.MAX)
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+    elapsed_max, kernel_ms_max = float(stats[0]), float(stats[1])
+    total_steps, total_pixels, evals_all = (int(x) for x in tot.tolist())
+
+    if rank != 0:
+        dist.destroy_process_group()
+        return
+
+    value = total_steps / elapsed_max
+    # roofline for the dominant kernel, on this rank: algorithmic flops per launch / avg launch time
+    achieved_tflops = FLOPS_PER_EVAL * evals_per_launch / (kernel_ms_avg * 1e-3) / 1e12
+    out = {
+        "metric": "geodesic-steps·pixels/sec at 3840x2160, 2048 max steps (whole job; /GPU = value/n_gpus)",
+        "value": value,
+        "unit": "geodesic-steps·pixels/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed_max / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "strong",  # one fixed 4K frame per step, split over the ranks
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (reference default scene scaled to rs=1; 4096x2048 equirect checkerboard+xorshift sky)",
+        "config": {
+            "workload": f"{cfg.name}: {W}x{H}, rs={cfg.rs}, sphere_r={cfg.sphere_r}, observer {cfg.position} "
+                        f"FrozenFall E={cfg.energy}, camera {tuple(round(c, 4) for c in cfg.camera)}, fov pi/2, "
+                        f"step pi/100, {cfg.max_steps} max RK4 steps, mode {args.mode}",
+            "width": W, "height": H, "max_steps": cfg.max_steps,
+            "parallelism": f"rowbands{world}" if world > 1 else "single",
+            "band_rows": B,
+        },
+        "per_gpu": value / world,
+        "pixels_per_s": total_pixels / elapsed_max,
+        "frames_per_s": args.steps / elapsed_max,
+        "steps_per_frame": total_steps // args.steps,
+        "mean_steps_per_pixel": total_steps / total_pixels,
+        "kernel_ms": {"avg": kernel_ms_avg, "median": kernel_ms[len(kernel_ms) // 2], "min": kernel_ms[0],
+                      "max_over_ranks_avg": kernel_ms_max},
+        "roofline": {
+            "bound": "valu",
+            "achieved": achieved_tflops,
+            "peak": PEAK_FP32_TFLOPS,
+            "unit": "TFLOP/s",
+            "frac": achieved_tflops / PEAK_FP32_TFLOPS,
+            "traffic": None,
+            "kernel": "geo_render_kernel<0>",
+            "algorithmic_flops_per_launch": FLOPS_PER_EVAL * evals_per_launch,
+            "evals_per_launch": evals_per_launch,
+        },
+    }
+    if world == 1 and not args.no_cpu_baseline and mode == g.GEO_MODE_DIRECT:
+        out["cpu_baseline"] = cpu_baseline(frame, scene, sky, W, H, args)
+    print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(frame, scene, sky, W, H, args):
+    """The oracle's scalar f32 restatement of the same per-pixel integrator
+    (oracle/geo_oracle.c), pthreads over rows, on every k-th row of the frame."""
+    import oracle as O
+
+    threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+    k = args.cpu_row_step
+    nrows = (H + k - 1) // k
+    t0 = time.perf_counter()
+    r = O.render_f32(frame, scene, sky, W, H, row0=0, nrows=nrows, row_step=k, threads=threads,
+                     want_uv=False, want_steps=False)
+    dt = time.perf_counter() - t0
+    return {
+        "value": r["steps_total"] / dt,
+        "unit": "geodesic-steps·pixels/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"every {k}th row of the same {W}x{H} frame ({nrows} rows, {nrows * W} pixels, "
+                  f"{r['steps_total']} RK4 steps) in {dt:.2f} s on {threads} threads",
+        "seconds": dt,
+    }
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,176 @@
+/*
+ * geo.h — C-ABI of libgeo.so, the MI355X-native per-pixel Schwarzschild
+ * geodesic renderer (drop-in for the sky-sphere hot path of
+ * FirePrincess01/schwarzschild_raytracer_wgpu).
+ *
+ * Plain C, plain pointers and sizes: no HIP, no torch types.  A HIP stream is
+ * passed as `void*` (a hipStream_t; NULL = the legacy default stream).
+ *
+ * Reference interfaces replaced (paths relative to the reference repo,
+ * `SR/` = schwarzschild_raytracer/src/):
+ *
+ *   geo_frame                  TransformationPipeline            SR/simulation/observer.rs:21-28
+ *                              (WGSL twin ObserverTransformations SR/schwarzschild_sphere_shader/shader.wgsl:26-33)
+ *   geo_observer_*             Observer::{new, calc_transformation_pipeline,
+ *                              update_screen_format, move_camera, start_*}
+ *                                                                SR/simulation/observer.rs:68-296
+ *   geo_set_sky                Texture::new_with_mipmaps (group 2, LOD 0)
+ *                                                                SR/schwarzschild_sphere_shader/sphere_buffer/basic_sphere_buffer.rs:29-36
+ *   geo_solve_ray_fan          SphereRayTracer::solve_ray_fan + BasicSphereBuffer::update_ray_fan
+ *                                                                SR/simulation/sphere_ray_tracer.rs:35-56,
+ *                                                                .../basic_sphere_buffer.rs:85-88
+ *   geo_set_fan                RayFanTexture::update             SR/schwarzschild_sphere_shader/ray_fan_texture.rs:65-90
+ *   geo_render_rows            SchwarzschildSphereShaderDraw::draw + fs_main
+ *                                                                SR/schwarzschild_sphere_shader/schwarzschild_sphere_shader_draw.rs:3-6,
+ *                                                                .../basic_sphere_buffer.rs:92-100,
+ *                                                                SR/schwarzschild_sphere_shader/shader.wgsl:57-106
+ *
+ * Conventions: every int-returning entry point returns GEO_OK (0) or a
+ * negative geo_status.  All output buffers are caller-owned.  A geo_ctx is
+ * bound to one device and is not thread-safe; calls that take a stream are
+ * asynchronous on it unless documented otherwise.
+ */
+#ifndef GEO_GEO_H
+#define GEO_GEO_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GEO_ABI_VERSION 1
+
+typedef enum geo_status {
+    GEO_OK = 0,
+    GEO_EINVAL = -1,  /* bad argument (null pointer, zero size, out-of-range rows) */
+    GEO_EHIP = -2,    /* a HIP runtime call failed */
+    GEO_ENOMEM = -3,  /* device or host allocation failed */
+    GEO_ENODEV = -4,  /* no such HIP device */
+    GEO_ESTATE = -5   /* call out of order (e.g. render before geo_set_sky) */
+} geo_status;
+
+/* Render modes (geo_scene.mode). */
+#define GEO_MODE_DIRECT 0u /* per-pixel RK4 of the null geodesic at the pixel's own angle */
+#define GEO_MODE_FAN 1u    /* reference-exact: lerp into the ray fan (shader.wgsl:77-84) */
+
+/* Observer motion states, ObserverState (SR/simulation/observer.rs:12-16). */
+#define GEO_OBSERVER_UNMOVING 0
+#define GEO_OBSERVER_FROZEN_FALL 1
+#define GEO_OBSERVER_ORBITING 2
+
+/* Sentinel for a ray that never reaches the sphere, SphereRayTracer::NO_VALUE
+ * (sphere_ray_tracer.rs:22).  Fan / traveled-angle space. */
+#define GEO_NO_VALUE 15.0
+
+/* Byte-for-byte TransformationPipeline (observer.rs:21-28): three column-major
+ * 4x4 f32 matrices and [sqrt((psi-1)/psi), x, y, z].  208 bytes. */
+typedef struct geo_frame {
+    float display_to_movement[16]; /* camera rotation; column 3 = FOV scale (observer.rs:253-254) */
+    float movement_to_central[16];
+    float central_to_uv[16];
+    float psi_factor_and_position[4];
+} geo_frame;
+
+/* Per-draw scene constants.  The reference fixes these per sphere
+ * (basic_sphere_buffer.rs:42-51, lib.rs:72, renderer.rs:83). */
+typedef struct geo_scene {
+    float rs;           /* Schwarzschild radius */
+    float sphere_r;     /* radius of the textured sky sphere */
+    float r_obs;        /* observer radial position |pos| (lib.rs:292) */
+    float step;         /* RK4 step in traveled angle (PI/100 in the reference) */
+    uint32_t max_steps; /* RK4 budget per ray (1000 in the reference) */
+    uint32_t mode;      /* GEO_MODE_* */
+    uint32_t flags;     /* reserved, must be 0 */
+    uint32_t reserved;  /* must be 0 */
+} geo_scene;
+
+typedef struct geo_ctx geo_ctx;
+typedef struct geo_observer geo_observer;
+
+/* ---- library ---------------------------------------------------------- */
+int geo_abi_version(void);
+const char* geo_status_str(int status);
+
+/* ---- device context --------------------------------------------------- */
+/* Creates a context on HIP device `device`.  Fails with GEO_ENODEV when the
+ * device does not exist (there is no CPU fallback). */
+int geo_ctx_create(int device, geo_ctx** out);
+void geo_ctx_destroy(geo_ctx* ctx);
+
+/* Uploads an equirect RGBA8 sky (row-major, w*h*4 bytes, host memory; the
+ * bytes are copied, synchronously).  U wraps, V clamps, LOD-0 bilinear. */
+int geo_set_sky(geo_ctx* ctx, const uint8_t* rgba8, uint32_t w, uint32_t h);
+
+/* Uploads a ray fan of n >= 2 nodes (host memory, copied synchronously):
+ * node i is PI/2 - traveled angle of the ray at theta_i = PI/2 - PI*i/(n-1). */
+int geo_set_fan(geo_ctx* ctx, const float* fan, uint32_t n);
+
+/* Computes the ray fan on the GPU in f64 (SphereRayTracer::solve_ray_fan,
+ * sphere_ray_tracer.rs:35-193) for nr_nodes nodes at observer radius r and
+ * makes it the context's fan.  When fan_out (host) is non-NULL the call
+ * synchronises `stream` and copies the nr_nodes f32 values there. */
+int geo_solve_ray_fan(geo_ctx* ctx, double sphere_r, double schwarz_r, uint32_t max_iter,
+                      double step, uint32_t nr_nodes, double r, float* fan_out, void* stream);
+
+/* Renders rows [row0, row0+nrows) of a width x height frame (fs_main,
+ * shader.wgsl:57-106, composited onto the clear colour (0,0,0,1) with the
+ * reference's alpha blend, pipeline.rs:49 / renderer.rs:233-238).
+ * Outputs are DEVICE pointers laid out row-major relative to row0:
+ *   out_rgba8    nrows*width*4 bytes (required)
+ *   out_mask     nrows*width bytes, 1 = black hole / discard (optional)
+ *   out_uv       nrows*width*2 floats, sky-sphere (U,V) (optional)
+ *   out_steps    nrows*width u32, executed RK4 main-loop steps (optional)
+ *   steps_total  one u64 that the executed steps of this call are ADDED to (optional)
+ * Asynchronous on `stream`. */
+int geo_render_rows(geo_ctx* ctx, const geo_frame* frame, const geo_scene* scene,
+                    uint32_t width, uint32_t height, uint32_t row0, uint32_t nrows,
+                    uint8_t* out_rgba8, uint8_t* out_mask, float* out_uv,
+                    uint32_t* out_steps, unsigned long long* steps_total, void* stream);
+
+/* Renders an interleaved set of row bands (balanced multi-GPU sharding): bands
+ * band0, band0+band_step, ..., nbands of them, each band_rows tall; band b
+ * covers rows [b*band_rows, (b+1)*band_rows) clipped to height.  Outputs are
+ * packed band after band (nbands*band_rows rows; clipped rows are not
+ * written).  geo_render_rows(row0, nrows) is the single-band case. */
+int geo_render_bands(geo_ctx* ctx, const geo_frame* frame, const geo_scene* scene,
+                     uint32_t width, uint32_t height, uint32_t band_rows, uint32_t band0,
+                     uint32_t band_step, uint32_t nbands, uint8_t* out_rgba8, uint8_t* out_mask,
+                     float* out_uv, uint32_t* out_steps, unsigned long long* steps_total,
+                     void* stream);
+
+/* Sets the persistent-grid size used by geo_render_rows (0 = automatic). */
+int geo_set_launch_blocks(geo_ctx* ctx, uint32_t blocks);
+
+/* ---- observer (host, f64; SR/simulation/observer.rs) ----------------- */
+/* Observer::new (observer.rs:68-87): pos (25,0,1), camera (PI,0), FrozenFall,
+ * energy 1, fov scale (tan(fov/2), tan(fov/2)*w/h, 1, 1). */
+int geo_observer_create(double schwarz_r, double fov, double width, double height,
+                        geo_observer** out);
+void geo_observer_destroy(geo_observer* obs);
+int geo_observer_set_position(geo_observer* obs, double x, double y, double z);
+int geo_observer_get_position(const geo_observer* obs, double* xyz3);
+int geo_observer_set_camera(geo_observer* obs, double phi, double theta);
+int geo_observer_set_energy(geo_observer* obs, double energy);
+/* GEO_OBSERVER_UNMOVING / GEO_OBSERVER_FROZEN_FALL (start_unmoving / start_frozen_fall,
+ * observer.rs:173-181). */
+int geo_observer_set_state(geo_observer* obs, int state);
+/* Observer::start_orbit (observer.rs:162-169); returns GEO_ESTATE when no orbit
+ * can start there (inside the horizon, orbit.rs:33-35). */
+int geo_observer_start_orbit(geo_observer* obs, double rotation);
+int geo_observer_get_state(const geo_observer* obs);
+double geo_observer_radial_position(const geo_observer* obs);
+/* Observer::update_position (observer.rs:105-125); dir = (forward, left, up). */
+int geo_observer_update_position(geo_observer* obs, double fwd, double left, double up, double dt);
+int geo_observer_move_camera(geo_observer* obs, double dx_pixels, double dy_pixels);
+int geo_observer_update_screen_format(geo_observer* obs, double width, double height);
+int geo_observer_is_singular(const geo_observer* obs);
+/* Observer::calc_transformation_pipeline (observer.rs:197-262). */
+int geo_observer_calc_transformation_pipeline(geo_observer* obs, geo_frame* out);
+
+#ifdef __cplusplus
+} /* extern "C" */
+#endif
+
+#endif /* GEO_GEO_H */

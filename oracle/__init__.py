@@ -1,0 +1,192 @@
+"""ORACLE loader — test infrastructure only.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may
+import this package, and only as the checker / the timed CPU baseline; the
+product (schwarzschild_raytracer_wgpu_amd, libgeo.so) never does.
+
+PARITY UNPINNED against reference outputs: the Rust/WGSL reference cannot be
+built or run here, and its only hot-path test asserts nothing
+(SR/simulation/tests.rs:8-13).  Pinned by analytic KATs and committed goldens
+(tests/golden/).  See geo_oracle.h.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "liboracle.so")
+
+
+class GeoFrameC(ctypes.Structure):
+    _fields_ = [
+        ("display_to_movement", ctypes.c_float * 16),
+        ("movement_to_central", ctypes.c_float * 16),
+        ("central_to_uv", ctypes.c_float * 16),
+        ("psi_factor_and_position", ctypes.c_float * 4),
+    ]
+
+
+class GeoSceneC(ctypes.Structure):
+    _fields_ = [
+        ("rs", ctypes.c_float),
+        ("sphere_r", ctypes.c_float),
+        ("r_obs", ctypes.c_float),
+        ("step", ctypes.c_float),
+        ("max_steps", ctypes.c_uint32),
+        ("mode", ctypes.c_uint32),
+        ("flags", ctypes.c_uint32),
+        ("reserved", ctypes.c_uint32),
+    ]
+
+
+class OraclePx(ctypes.Structure):
+    _fields_ = [
+        ("lam", ctypes.c_double),
+        ("u", ctypes.c_double),
+        ("v", ctypes.c_double),
+        ("theta", ctypes.c_double),
+        ("steps", ctypes.c_uint32),
+        ("bh", ctypes.c_int),
+    ]
+
+
+def build() -> str:
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return LIB_PATH
+
+
+def _load() -> ctypes.CDLL:
+    if not os.path.exists(LIB_PATH):
+        build()
+    lib = ctypes.CDLL(LIB_PATH)
+    vp, u32, f64, i = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_double, ctypes.c_int
+    sig = {
+        "geo_oracle_solve_geodesic_f64": (f64, [f64, f64, u32, f64, f64, f64, f64, i, vp]),
+        "geo_oracle_solve_ray_fan_f64": (None, [f64, f64, u32, f64, u32, f64, vp]),
+        "geo_oracle_geodesic_at_theta_f64": (f64, [f64, f64, u32, f64, f64, f64, vp]),
+        "geo_oracle_pixel_f64": (None, [vp, vp, vp, u32, u32, u32, u32, u32, vp]),
+        "geo_oracle_render_f64": (i, [vp, vp, vp, u32, u32, u32, u32, u32, i, vp, vp, vp, vp]),
+        "geo_oracle_render_f32": (i, [vp, vp, vp, u32, vp, u32, u32, u32, u32, u32, u32, u32, i, vp, vp, vp,
+                                      vp, vp]),
+        "geo_oracle_observer_frame": (None, [f64, f64, f64, f64, vp, f64, f64, i, f64, vp]),
+        "geo_oracle_asinf": (ctypes.c_float, [ctypes.c_float]),
+        "geo_oracle_atan2f": (ctypes.c_float, [ctypes.c_float, ctypes.c_float]),
+        "geo_oracle_sincosf": (None, [ctypes.c_float, vp, vp]),
+    }
+    for n, (r, a) in sig.items():
+        fn = getattr(lib, n)
+        fn.restype = r
+        fn.argtypes = a
+    return lib
+
+
+lib = _load()
+
+
+def _addr(x):
+    return None if x is None else ctypes.cast(ctypes.byref(x), ctypes.c_void_p)
+
+
+def _np(a):
+    return None if a is None else a.ctypes.data
+
+
+def as_frame(frame) -> GeoFrameC:
+    """Copy any 208-byte TransformationPipeline-like ctypes struct."""
+    out = GeoFrameC()
+    ctypes.memmove(ctypes.byref(out), ctypes.byref(frame), ctypes.sizeof(GeoFrameC))
+    return out
+
+
+def as_scene(scene) -> GeoSceneC:
+    out = GeoSceneC()
+    ctypes.memmove(ctypes.byref(out), ctypes.byref(scene), ctypes.sizeof(GeoSceneC))
+    return out
+
+
+def solve_geodesic(sphere_r, schwarz_r, max_iter, step, r, energy, rotation, r_falling):
+    steps = ctypes.c_uint32()
+    a = lib.geo_oracle_solve_geodesic_f64(sphere_r, schwarz_r, max_iter, step, r, energy, rotation,
+                                          int(bool(r_falling)), ctypes.byref(steps))
+    return a, steps.value
+
+
+def geodesic_at_theta(sphere_r, schwarz_r, max_iter, step, r, theta):
+    steps = ctypes.c_uint32()
+    a = lib.geo_oracle_geodesic_at_theta_f64(sphere_r, schwarz_r, max_iter, step, r, theta, ctypes.byref(steps))
+    return a, steps.value
+
+
+def solve_ray_fan(sphere_r, schwarz_r, max_iter, step, nr_nodes, r) -> np.ndarray:
+    out = np.empty(nr_nodes, dtype=np.float32)
+    lib.geo_oracle_solve_ray_fan_f64(sphere_r, schwarz_r, max_iter, step, nr_nodes, r, out.ctypes.data)
+    return out
+
+
+def observer_frame(schwarz_r, fov, width, height, pos, cam_phi, cam_theta, state=1, energy=1.0) -> GeoFrameC:
+    f = GeoFrameC()
+    p = (ctypes.c_double * 3)(*pos)
+    lib.geo_oracle_observer_frame(schwarz_r, fov, width, height, ctypes.cast(p, ctypes.c_void_p), cam_phi,
+                                  cam_theta, state, energy, _addr(f))
+    return f
+
+
+def pixel_f64(frame, scene, width, height, px, py, fan=None) -> OraclePx:
+    fr, sc = as_frame(frame), as_scene(scene)
+    fan_a = None if fan is None else np.ascontiguousarray(fan, dtype=np.float32)
+    out = OraclePx()
+    lib.geo_oracle_pixel_f64(_addr(fr), _addr(sc), _np(fan_a), 0 if fan_a is None else fan_a.size, width, height,
+                             px, py, _addr(out))
+    return out
+
+
+def render_f64(frame, scene, width, height, row0=0, nrows=None, fan=None, threads=8):
+    nrows = height - row0 if nrows is None else nrows
+    fr, sc = as_frame(frame), as_scene(scene)
+    fan_a = None if fan is None else np.ascontiguousarray(fan, dtype=np.float32)
+    mask = np.empty((nrows, width), np.uint8)
+    uv = np.empty((nrows, width, 2), np.float32)
+    steps = np.empty((nrows, width), np.uint32)
+    lam = np.empty((nrows, width), np.float64)
+    rc = lib.geo_oracle_render_f64(_addr(fr), _addr(sc), _np(fan_a), 0 if fan_a is None else fan_a.size, width,
+                                   height, row0, nrows, threads, _np(mask), _np(uv), _np(steps), _np(lam))
+    if rc != 0:
+        raise ValueError(f"geo_oracle_render_f64: {rc}")
+    return dict(mask=mask, uv=uv, steps=steps, lam=lam)
+
+
+def render_f32(frame, scene, sky, width, height, row0=0, nrows=None, row_step=1, fan=None, threads=8,
+               want_uv=True, want_steps=True):
+    nrows = height - row0 if nrows is None else nrows
+    fr, sc = as_frame(frame), as_scene(scene)
+    sky_a = np.ascontiguousarray(sky, dtype=np.uint8)
+    fan_a = None if fan is None else np.ascontiguousarray(fan, dtype=np.float32)
+    rgba = np.empty((nrows, width, 4), np.uint8)
+    mask = np.empty((nrows, width), np.uint8)
+    uv = np.empty((nrows, width, 2), np.float32) if want_uv else None
+    steps = np.empty((nrows, width), np.uint32) if want_steps else None
+    total = ctypes.c_uint64()
+    rc = lib.geo_oracle_render_f32(_addr(fr), _addr(sc), _np(fan_a), 0 if fan_a is None else fan_a.size,
+                                   _np(sky_a), sky_a.shape[1], sky_a.shape[0], width, height, row0, nrows, row_step,
+                                   threads, _np(rgba), _np(mask), _np(uv), _np(steps), _addr(total))
+    if rc != 0:
+        raise ValueError(f"geo_oracle_render_f32: {rc}")
+    return dict(rgba=rgba, mask=mask, uv=uv, steps=steps, steps_total=total.value)
+
+
+def asinf(x: float) -> float:
+    return lib.geo_oracle_asinf(x)
+
+
+def atan2f(y: float, x: float) -> float:
+    return lib.geo_oracle_atan2f(y, x)
+
+
+def sincosf(x: float):
+    s, c = ctypes.c_float(), ctypes.c_float()
+    lib.geo_oracle_sincosf(x, _addr(s), _addr(c))
+    return s.value, c.value

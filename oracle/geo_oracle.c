@@ -1,0 +1,759 @@
+/*
+ * geo_oracle.c — ORACLE (test infrastructure only).  See geo_oracle.h for the
+ * contract and the "parity unpinned" statement.
+ *
+ * Two independent restatements of the reference hot path:
+ *   (1) f64, literal: every arithmetic expression of
+ *       SR/simulation/sphere_ray_tracer.rs:35-193 and
+ *       SR/schwarzschild_sphere_shader/shader.wgsl:57-106 in its source order,
+ *       with libm transcendentals;
+ *   (2) f32, the kernel's documented evaluation order (geo_pixel.h), written
+ *       here from the specification in DESIGN.md §3, not shared with the
+ *       product sources: tests require the HIP output to equal it bit for bit.
+ *
+ * Build: make -C oracle   (gcc, -ffp-contract=off so no implicit FMA).
+ */
+#include "geo_oracle.h"
+
+#include <math.h>
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define O_PI 3.14159265358979323846
+#define O_FRAC_PI_2 1.57079632679489661923
+#define O_NO_VALUE 15.0
+
+/* ------------------------------------------------------------------ */
+/* (1) f64 literal restatement                                          */
+/* ------------------------------------------------------------------ */
+
+/* sphere_ray_tracer.rs:60-193 */
+double geo_oracle_solve_geodesic_f64(double sphere_r, double schwarz_r, uint32_t max_iter,
+                                     double default_step, double r, double energy,
+                                     double rotation, int r_falling, uint32_t* steps) {
+    uint32_t dummy;
+    if (!steps) steps = &dummy;
+    *steps = 0;
+    double b = rotation / energy;
+    int outside = r > schwarz_r;
+    int sphere_outside = sphere_r > schwarz_r;
+    int inside_sphere = r < sphere_r;
+
+    if (rotation < 1e-10) { /* :67-104 */
+        if (inside_sphere) {
+            if (outside) {
+                if (r_falling) {
+                    if (schwarz_r == 0.) return O_PI;
+                    return O_NO_VALUE;
+                }
+                return 0.;
+            } else {
+                if (sphere_outside) {
+                    if (energy > 0.) return 0.;
+                    return O_NO_VALUE;
+                }
+                return 0.;
+            }
+        } else {
+            if (sphere_outside && r_falling) return 0.;
+            return O_NO_VALUE;
+        }
+    }
+    /* :107-119 */
+    int barrier_3r_2 = (schwarz_r > 0.) && 1. / (b * b) < 4. / (27. * schwarz_r * schwarz_r);
+    double r3_2 = 3. * schwarz_r / 2.;
+    int different_sides_3r_2 = ((r < r3_2) ^ (sphere_r < r3_2)) && fabs(r - r3_2) > 1e-10;
+    if ((inside_sphere && !sphere_outside) || (!outside && sphere_outside && energy < 0.) ||
+        (barrier_3r_2 && different_sides_3r_2) || (r < r3_2 && inside_sphere && r_falling) ||
+        (r > r3_2 && !inside_sphere && !r_falling)) {
+        return O_NO_VALUE;
+    }
+    /* :122-132 */
+    double u_k = 1. / r;
+    double u_bar_k = (r_falling ? 1. : -1.) * sqrt(1. / (b * b) - (1. - schwarz_r / r) / (r * r));
+    double angle = 0.;
+    uint32_t iteration = 0;
+    double bound = 0.9 * fmin(u_k, 1. / fmax(sphere_r, r3_2));
+    double step = default_step;
+    double step_half = step / 2.;
+    double sphere_u = 1. / sphere_r;
+    double schwarz_u = 1. / schwarz_r;
+    /* :134-191 */
+    while (!(schwarz_r != 0. && u_k > schwarz_u && u_bar_k > 0.) && iteration < max_iter && u_k > 0.) {
+        double a_u = u_k + step_half * u_bar_k;
+        double a_u_bar = u_bar_k + step_half * (-u_k + r3_2 * u_k * u_k);
+        double b_u = u_k + step_half * a_u_bar;
+        double b_u_bar = u_bar_k + step_half * (-a_u + r3_2 * a_u * a_u);
+        double c_u = u_k + step * b_u_bar;
+        double c_u_bar = u_bar_k + step * (-b_u + r3_2 * b_u * b_u);
+        double next_u = u_k + step * (u_bar_k + 2. * a_u_bar + 2. * b_u_bar + c_u_bar) / 6.;
+        double next_u_bar = u_bar_k + step * ((-u_k + r3_2 * u_k * u_k) + 2. * (-a_u + r3_2 * a_u * a_u) +
+                                              2. * (-b_u + r3_2 * b_u * b_u) + (-c_u + r3_2 * c_u * c_u)) / 6.;
+        *steps = iteration + 1;
+        if ((next_u > sphere_u) ^ (u_k > sphere_u)) {
+            double newton_u, newton_u_bar, newton_step;
+            if (fabs(u_bar_k) > fabs(next_u_bar)) {
+                newton_step = 0.;
+                newton_u = u_k;
+                newton_u_bar = u_bar_k;
+            } else {
+                newton_step = step;
+                newton_u = next_u;
+                newton_u_bar = next_u_bar;
+            }
+            for (int n = 0; n < 3; ++n) {
+                newton_step -= (newton_u - sphere_u) / newton_u_bar;
+                double newton_step_half = newton_step / 2.;
+                a_u = u_k + newton_step_half * u_bar_k;
+                a_u_bar = u_bar_k + newton_step_half * (-u_k + r3_2 * u_k * u_k);
+                b_u = u_k + newton_step_half * a_u_bar;
+                b_u_bar = u_bar_k + newton_step_half * (-a_u + r3_2 * a_u * a_u);
+                c_u = u_k + newton_step * b_u_bar;
+                c_u_bar = u_bar_k + newton_step * (-b_u + r3_2 * b_u * b_u);
+                newton_u = u_k + newton_step * (u_bar_k + 2. * a_u_bar + 2. * b_u_bar + c_u_bar) / 6.;
+                newton_u_bar = u_bar_k + newton_step * ((-u_k + r3_2 * u_k * u_k) + 2. * (-a_u + r3_2 * a_u * a_u) +
+                                                        2. * (-b_u + r3_2 * b_u * b_u) + (-c_u + r3_2 * c_u * c_u)) / 6.;
+            }
+            return angle + newton_step;
+        }
+        if (next_u < bound) return O_NO_VALUE;
+        u_k = next_u;
+        u_bar_k = next_u_bar;
+        iteration += 1;
+        angle += step;
+    }
+    return O_NO_VALUE;
+}
+
+/* sphere_ray_tracer.rs:38-52 for one theta */
+double geo_oracle_geodesic_at_theta_f64(double sphere_r, double schwarz_r, uint32_t max_iter,
+                                        double step, double r, double theta, uint32_t* steps) {
+    double rotation = r * cos(theta);
+    int r_falling;
+    double energy;
+    if (r < schwarz_r) {
+        r_falling = 0;
+        energy = sin(-theta) * sqrt(-1. + schwarz_r / r);
+    } else {
+        r_falling = theta > 0.;
+        energy = sqrt(1. - schwarz_r / r);
+    }
+    return geo_oracle_solve_geodesic_f64(sphere_r, schwarz_r, max_iter, step, r, energy, rotation,
+                                         r_falling, steps);
+}
+
+/* sphere_ray_tracer.rs:35-56 */
+void geo_oracle_solve_ray_fan_f64(double sphere_r, double schwarz_r, uint32_t max_iter,
+                                  double step, uint32_t nr_nodes, double r, float* fan_out) {
+    for (uint32_t i = 0; i < nr_nodes; ++i) {
+        double theta = O_FRAC_PI_2 - O_PI * (double)i / ((double)nr_nodes - 1.);
+        fan_out[i] = (float)(O_FRAC_PI_2 -
+                             geo_oracle_geodesic_at_theta_f64(sphere_r, schwarz_r, max_iter, step, r, theta, NULL));
+    }
+}
+
+/* mat4x4<f32> * vec4 (w = 0), column-major, evaluated in f64 */
+static void m3v_d(const float* m, const double* v, double* o) {
+    for (int i = 0; i < 3; ++i) o[i] = (double)m[i] * v[0] + (double)m[4 + i] * v[1] + (double)m[8 + i] * v[2];
+}
+
+/* shader.wgsl:47-55 */
+static void to_cart_d(double phi, double lam, double* c) {
+    c[0] = cos(phi) * cos(lam);
+    c[1] = sin(phi) * cos(lam);
+    c[2] = sin(lam);
+}
+
+/* shader.wgsl:57-106 in f64; the fan lookup (:77-84) in fan mode, else the
+ * per-pixel geodesic at theta = lambda. */
+void geo_oracle_pixel_f64(const geo_frame* f, const geo_scene* s, const float* fan, uint32_t n_fan,
+                          uint32_t width, uint32_t height, uint32_t px, uint32_t py,
+                          geo_oracle_px* out) {
+    /* full-screen quad position at the pixel centre (basic_sphere_buffer.rs:63-83) */
+    double ndc_x = ((double)px + 0.5) / (double)width * 2. - 1.;
+    double ndc_y = 1. - ((double)py + 0.5) / (double)height * 2.;
+    const float* m0 = f->display_to_movement;
+    double c[3] = {-ndc_y * (double)m0[12], -ndc_x * (double)m0[13], 1. * (double)m0[14]};
+    double d[3];
+    m3v_d(m0, c, d);
+    double len = sqrt(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]);
+    d[0] /= len;
+    d[1] /= len;
+    d[2] /= len;
+    double phi = atan2(d[1], d[0]);
+    double lam = asin(d[2]);
+    double k = (double)f->psi_factor_and_position[0];
+    double sin_result = sin(lam);
+    lam = asin((sin_result - k) / (1. - sin_result * k));
+    to_cart_d(phi, lam, c);
+    m3v_d(f->movement_to_central, c, d);
+    phi = atan2(d[1], d[0]);
+    lam = asin(d[2]);
+    out->theta = lam;
+    out->steps = 0;
+    double lam2;
+    if (s->mode == GEO_MODE_FAN) {
+        double t = (O_FRAC_PI_2 - lam) / (O_FRAC_PI_2 * 2.);
+        t = t < 0. ? 0. : (t > 1. ? 1. : t);
+        t = t * (double)(n_fan - 1u);
+        double fl = floor(t);
+        uint32_t i = (uint32_t)fl;
+        double w = t - fl;
+        uint32_t i1 = i + 1u < n_fan ? i + 1u : n_fan - 1u;
+        lam2 = (double)fan[i] * (1. - w) + (double)fan[i1] * w;
+    } else {
+        lam2 = O_FRAC_PI_2 - geo_oracle_geodesic_at_theta_f64((double)s->sphere_r, (double)s->rs, s->max_steps,
+                                                              (double)s->step, (double)s->r_obs, lam, &out->steps);
+    }
+    out->lam = lam2;
+    out->bh = lam2 < -7.;
+    to_cart_d(phi, lam2, c);
+    m3v_d(f->central_to_uv, c, d);
+    phi = atan2(d[1], d[0]);
+    lam = asin(d[2]);
+    double u = phi / (O_FRAC_PI_2 * 4.);
+    if (u < 0.) u += 1.;
+    out->u = u;
+    out->v = 0.5 - lam / (O_FRAC_PI_2 * 2.);
+}
+
+/* ------------------------------------------------------------------ */
+/* (2) f32 restatement of the kernel's evaluation order                 */
+/* ------------------------------------------------------------------ */
+
+#define F_PI 3.14159265358979323846f
+#define F_PI2 1.57079632679489661923f
+#define F_PI4 0.785398163397448309616f
+
+static inline float clampf(float x, float lo, float hi) { return x < lo ? lo : (x > hi ? hi : x); }
+static inline float maxz(float a, float b) { return a > b ? a : b; }
+
+void geo_oracle_sincosf(float x, float* so, float* co) {
+    float j = rintf(x * 0.636619772367581343076f);
+    float r = fmaf(-j, 1.5703125f, x);
+    r = fmaf(-j, 4.837512969970703125e-4f, r);
+    r = fmaf(-j, 7.54978995489188216e-8f, r);
+    float z = r * r;
+    float ps = fmaf(fmaf(-1.9515295891e-4f, z, 8.3321608736e-3f), z, -1.6666654611e-1f);
+    float sn = fmaf(ps * z, r, r);
+    float pc = fmaf(fmaf(2.443315711809948e-5f, z, -1.388731625493765e-3f), z, 4.166664568298827e-2f);
+    float cs = fmaf(pc * z, z, fmaf(-0.5f, z, 1.0f));
+    int q = ((int)j) & 3;
+    float sv, cv;
+    switch (q) {
+        case 0: sv = sn; cv = cs; break;
+        case 1: sv = cs; cv = -sn; break;
+        case 2: sv = -sn; cv = -cs; break;
+        default: sv = -cs; cv = sn; break;
+    }
+    *so = sv;
+    *co = cv;
+}
+
+float geo_oracle_asinf(float x) {
+    x = clampf(x, -1.0f, 1.0f);
+    float a = fabsf(x);
+    int big = a > 0.5f;
+    float z, sq;
+    if (big) {
+        z = 0.5f * (1.0f - a);
+        sq = sqrtf(z);
+    } else {
+        z = a * a;
+        sq = a;
+    }
+    float p = fmaf(fmaf(fmaf(fmaf(4.2163199048e-2f, z, 2.4181311049e-2f), z, 4.5470025998e-2f), z,
+                        7.4953002686e-2f), z, 1.6666752422e-1f);
+    float r = fmaf(p * z, sq, sq);
+    if (big) r = fmaf(-2.0f, r, F_PI2);
+    return copysignf(r, x);
+}
+
+float geo_oracle_atan2f(float y, float x) {
+    float ay = fabsf(y), ax = fabsf(x);
+    float num, den, y0;
+    if (ay > 2.414213562373095f * ax) {
+        num = -ax; den = ay; y0 = F_PI2;
+    } else if (ay > 0.4142135623730950f * ax) {
+        num = ay - ax; den = ay + ax; y0 = F_PI4;
+    } else {
+        num = ay; den = ax; y0 = 0.0f;
+    }
+    float t = den > 0.0f ? num / den : 0.0f;
+    float z = t * t;
+    float p = fmaf(fmaf(fmaf(8.05374449538e-2f, z, -1.38776856032e-1f), z, 1.99777106478e-1f), z,
+                   -3.33329491539e-1f);
+    float r = y0 + fmaf(p * z, t, t);
+    if (x < 0.0f) r = F_PI - r;
+    return copysignf(r, y);
+}
+
+typedef struct {
+    float rs, sphere_r, r, step;
+    uint32_t max_steps;
+    float hh, h6, r3_2, sphere_u, schwarz_u, u0, h_over_r2, bound, e_out, e_in, barrier;
+    int r_inside_h, outside, sphere_outside, inside_sphere, diff_sides, rs_nonzero;
+} fconsts;
+
+static fconsts make_fconsts(const geo_scene* s) {
+    fconsts k;
+    k.rs = s->rs;
+    k.sphere_r = s->sphere_r;
+    k.r = s->r_obs;
+    k.step = s->step;
+    k.max_steps = s->max_steps;
+    k.hh = k.step * 0.5f;
+    k.h6 = k.step / 6.0f;
+    k.r3_2 = 1.5f * k.rs;
+    k.sphere_u = 1.0f / k.sphere_r;
+    k.schwarz_u = 1.0f / k.rs;
+    k.u0 = 1.0f / k.r;
+    k.h_over_r2 = (1.0f - k.rs / k.r) / (k.r * k.r);
+    float mx = k.sphere_r > k.r3_2 ? k.sphere_r : k.r3_2;
+    float um = 1.0f / mx;
+    k.bound = 0.9f * (k.u0 < um ? k.u0 : um);
+    k.e_out = sqrtf(1.0f - k.rs / k.r);
+    k.e_in = sqrtf(-1.0f + k.rs / k.r);
+    k.barrier = 4.0f / (27.0f * k.rs * k.rs);
+    k.r_inside_h = k.r < k.rs;
+    k.outside = k.r > k.rs;
+    k.sphere_outside = k.sphere_r > k.rs;
+    k.inside_sphere = k.r < k.sphere_r;
+    k.diff_sides = ((k.r < k.r3_2) != (k.sphere_r < k.r3_2)) && (fabsf(k.r - k.r3_2) > 1e-10f);
+    k.rs_nonzero = k.rs != 0.0f;
+    return k;
+}
+
+/* the RK4 step of sphere_ray_tracer.rs:137-146 with f(x) = x*(c*x - 1) */
+static inline void rk4f(float u, float ub, float h, float hh, float h6, float c, float* nu, float* nub) {
+    float fu = fmaf(c, u, -1.0f) * u;
+    float au = fmaf(hh, ub, u);
+    float aub = fmaf(hh, fu, ub);
+    float fa = fmaf(c, au, -1.0f) * au;
+    float bu = fmaf(hh, aub, u);
+    float bub = fmaf(hh, fa, ub);
+    float fb = fmaf(c, bu, -1.0f) * bu;
+    float cu = fmaf(h, bub, u);
+    float cub = fmaf(h, fb, ub);
+    float fc = fmaf(c, cu, -1.0f) * cu;
+    float s1 = fmaf(2.0f, aub + bub, ub) + cub;
+    float s2 = fmaf(2.0f, fa + fb, fu) + fc;
+    *nu = fmaf(h6, s1, u);
+    *nub = fmaf(h6, s2, ub);
+}
+
+static float geodesic_f32(const fconsts* k, float st, uint32_t* steps) {
+    *steps = 0;
+    float ct = sqrtf(maxz(0.0f, (1.0f - st) * (1.0f + st)));
+    float rotation = k->r * ct;
+    int falling;
+    float energy;
+    if (k->r_inside_h) {
+        falling = 0;
+        energy = (-st) * k->e_in;
+    } else {
+        falling = st > 0.0f;
+        energy = k->e_out;
+    }
+    if (rotation < 1e-10f) {
+        if (k->inside_sphere) {
+            if (k->outside) {
+                if (falling) return k->rs_nonzero ? 15.0f : F_PI;
+                return 0.0f;
+            }
+            if (k->sphere_outside) return energy > 0.0f ? 0.0f : 15.0f;
+            return 0.0f;
+        }
+        return (k->sphere_outside && falling) ? 0.0f : 15.0f;
+    }
+    float b = rotation / energy;
+    float inv_b2 = 1.0f / (b * b);
+    int barrier = k->rs > 0.0f && inv_b2 < k->barrier;
+    if ((k->inside_sphere && !k->sphere_outside) || (!k->outside && k->sphere_outside && energy < 0.0f) ||
+        (barrier && k->diff_sides) || (k->r < k->r3_2 && k->inside_sphere && falling) ||
+        (k->r > k->r3_2 && !k->inside_sphere && !falling))
+        return 15.0f;
+    float u = k->u0;
+    float ub = sqrtf(maxz(0.0f, inv_b2 - k->h_over_r2));
+    if (!falling) ub = -ub;
+    float su = k->sphere_u, c = k->r3_2;
+    uint32_t it = 0;
+    while (!(k->rs_nonzero && u > k->schwarz_u && ub > 0.0f) && it < k->max_steps && u > 0.0f) {
+        float nu, nub;
+        rk4f(u, ub, k->step, k->hh, k->h6, c, &nu, &nub);
+        ++it;
+        if ((nu > su) != (u > su)) {
+            float ns, wu, wub;
+            if (fabsf(ub) > fabsf(nub)) {
+                ns = 0.0f; wu = u; wub = ub;
+            } else {
+                ns = k->step; wu = nu; wub = nub;
+            }
+            for (int n = 0; n < 3; ++n) {
+                ns = ns - (wu - su) / wub;
+                rk4f(u, ub, ns, ns * 0.5f, ns / 6.0f, c, &wu, &wub);
+            }
+            *steps = it;
+            return (float)(it - 1u) * k->step + ns;
+        }
+        if (nu < k->bound) {
+            *steps = it;
+            return 15.0f;
+        }
+        u = nu;
+        ub = nub;
+    }
+    *steps = it;
+    return 15.0f;
+}
+
+static inline void m3vf(const float* m, float x, float y, float z, float* o) {
+    o[0] = fmaf(m[8], z, fmaf(m[4], y, m[0] * x));
+    o[1] = fmaf(m[9], z, fmaf(m[5], y, m[1] * x));
+    o[2] = fmaf(m[10], z, fmaf(m[6], y, m[2] * x));
+}
+
+static inline float lerpf(float a, float b, float t) { return fmaf(t, b - a, a); }
+static inline uint32_t u8f(float v) { return (uint32_t)clampf(v + 0.5f, 0.0f, 255.0f); }
+
+static void pixel_f32(const geo_frame* f, const fconsts* k, int mode, const float* fan, uint32_t n_fan,
+                      const uint32_t* sky, uint32_t sw, uint32_t sh, uint32_t width, uint32_t height,
+                      uint32_t px, uint32_t py, uint32_t* rgba, uint8_t* bh_out, float* uv, uint32_t* steps) {
+    const float* m0 = f->display_to_movement;
+    float nx = ((float)(2u * px + 1u) - (float)width) / (float)width;
+    float ny = ((float)height - (float)(2u * py + 1u)) / (float)height;
+    float d[3];
+    m3vf(m0, -ny * m0[12], -nx * m0[13], m0[14], d);
+    float inv = 1.0f / sqrtf(fmaf(d[2], d[2], fmaf(d[1], d[1], d[0] * d[0])));
+    d[0] *= inv;
+    d[1] *= inv;
+    d[2] *= inv;
+    float kk = f->psi_factor_and_position[0];
+    float s = clampf(d[2], -1.0f, 1.0f);
+    float q = clampf((s - kk) / fmaf(-s, kk, 1.0f), -1.0f, 1.0f);
+    float cl = sqrtf(maxz(0.0f, (1.0f - q) * (1.0f + q)));
+    float rho = sqrtf(fmaf(d[1], d[1], d[0] * d[0]));
+    float cp = 1.0f, sp = 0.0f;
+    if (rho > 0.0f) {
+        cp = d[0] / rho;
+        sp = d[1] / rho;
+    }
+    float c2[3];
+    m3vf(f->movement_to_central, cp * cl, sp * cl, q, c2);
+    float st = clampf(c2[2], -1.0f, 1.0f);
+    float lam;
+    *steps = 0;
+    if (mode == (int)GEO_MODE_FAN) {
+        float theta = geo_oracle_asinf(st);
+        float t = clampf((F_PI2 - theta) / F_PI, 0.0f, 1.0f);
+        t = t * (float)(n_fan - 1u);
+        float fl = floorf(t);
+        uint32_t i = (uint32_t)fl;
+        float w = t - fl;
+        uint32_t i1 = (i + 1u < n_fan) ? i + 1u : n_fan - 1u;
+        lam = fan[i] * (1.0f - w) + fan[i1] * w;
+    } else {
+        lam = F_PI2 - geodesic_f32(k, st, steps);
+    }
+    int bh = lam < -7.0f;
+    /* sky_uv */
+    float rho2 = sqrtf(fmaf(c2[1], c2[1], c2[0] * c2[0]));
+    float cp2 = 1.0f, sp2 = 0.0f;
+    if (rho2 > 0.0f) {
+        cp2 = c2[0] / rho2;
+        sp2 = c2[1] / rho2;
+    }
+    float sl, cll;
+    geo_oracle_sincosf(lam, &sl, &cll);
+    float c3[3];
+    m3vf(f->central_to_uv, cp2 * cll, sp2 * cll, sl, c3);
+    float U = geo_oracle_atan2f(c3[1], c3[0]) * 0.159154943091895335769f;
+    if (U < 0.0f) U += 1.0f;
+    float V = 0.5f - geo_oracle_asinf(c3[2]) * 0.318309886183790671538f;
+    if (!(U == U)) U = 0.0f;
+    if (!(V == V)) V = 0.0f;
+    U = clampf(U, 0.0f, 1.0f);
+    V = clampf(V, 0.0f, 1.0f);
+    uv[0] = U;
+    uv[1] = V;
+    *bh_out = (uint8_t)bh;
+    if (bh) {
+        *rgba = 0xFF000000u;
+        return;
+    }
+    /* bilinear LOD-0, U wraps, V clamps; alpha blend over (0,0,0,1) */
+    float x = fmaf(U, (float)sw, -0.5f);
+    float y = fmaf(V, (float)sh, -0.5f);
+    float fx0 = floorf(x), fy0 = floorf(y);
+    float fx = x - fx0, fy = y - fy0;
+    int ix0 = (int)fx0, iy0 = (int)fy0;
+    int w = (int)sw, h = (int)sh;
+    if (ix0 < 0) ix0 += w;
+    if (ix0 >= w) ix0 -= w;
+    int ix1 = (ix0 + 1 == w) ? 0 : ix0 + 1;
+    int iy1 = iy0 + 1;
+    iy0 = iy0 < 0 ? 0 : (iy0 > h - 1 ? h - 1 : iy0);
+    iy1 = iy1 < 0 ? 0 : (iy1 > h - 1 ? h - 1 : iy1);
+    uint32_t t00 = sky[(uint32_t)iy0 * sw + (uint32_t)ix0];
+    uint32_t t10 = sky[(uint32_t)iy0 * sw + (uint32_t)ix1];
+    uint32_t t01 = sky[(uint32_t)iy1 * sw + (uint32_t)ix0];
+    uint32_t t11 = sky[(uint32_t)iy1 * sw + (uint32_t)ix1];
+    float cc[4];
+    for (int ch = 0; ch < 4; ++ch) {
+        float a = lerpf((float)((t00 >> (8 * ch)) & 255u), (float)((t10 >> (8 * ch)) & 255u), fx);
+        float b = lerpf((float)((t01 >> (8 * ch)) & 255u), (float)((t11 >> (8 * ch)) & 255u), fx);
+        cc[ch] = lerpf(a, b, fy);
+    }
+    float alpha = cc[3] * (1.0f / 255.0f);
+    *rgba = u8f(cc[0] * alpha) | (u8f(cc[1] * alpha) << 8) | (u8f(cc[2] * alpha) << 16) | (255u << 24);
+}
+
+typedef struct {
+    const geo_frame* f;
+    const geo_scene* s;
+    fconsts k;
+    const float* fan;
+    uint32_t n_fan;
+    const uint32_t* sky;
+    uint32_t sw, sh, width, height, row0, nrows, row_step;
+    int threads, tid;
+    uint8_t* rgba;
+    uint8_t* mask;
+    float* uv;
+    uint32_t* steps;
+    double* lam;
+    uint64_t total;
+} job_t;
+
+static void* job_f32(void* arg) {
+    job_t* j = (job_t*)arg;
+    uint64_t total = 0;
+    for (uint32_t r = (uint32_t)j->tid; r < j->nrows; r += (uint32_t)j->threads) {
+        uint32_t py = j->row0 + r * j->row_step;
+        for (uint32_t px = 0; px < j->width; ++px) {
+            size_t o = (size_t)r * j->width + px;
+            uint32_t rgba, st;
+            uint8_t bh;
+            float uv[2];
+            pixel_f32(j->f, &j->k, (int)j->s->mode, j->fan, j->n_fan, j->sky, j->sw, j->sh, j->width, j->height,
+                      px, py, &rgba, &bh, uv, &st);
+            memcpy(j->rgba + 4 * o, &rgba, 4);
+            if (j->mask) j->mask[o] = bh;
+            if (j->uv) {
+                j->uv[2 * o] = uv[0];
+                j->uv[2 * o + 1] = uv[1];
+            }
+            if (j->steps) j->steps[o] = st;
+            total += st;
+        }
+    }
+    j->total = total;
+    return NULL;
+}
+
+static void* job_f64(void* arg) {
+    job_t* j = (job_t*)arg;
+    for (uint32_t r = (uint32_t)j->tid; r < j->nrows; r += (uint32_t)j->threads) {
+        uint32_t py = j->row0 + r;
+        for (uint32_t px = 0; px < j->width; ++px) {
+            size_t o = (size_t)r * j->width + px;
+            geo_oracle_px p;
+            geo_oracle_pixel_f64(j->f, j->s, j->fan, j->n_fan, j->width, j->height, px, py, &p);
+            if (j->mask) j->mask[o] = (uint8_t)p.bh;
+            if (j->uv) {
+                j->uv[2 * o] = (float)p.u;
+                j->uv[2 * o + 1] = (float)p.v;
+            }
+            if (j->steps) j->steps[o] = p.steps;
+            if (j->lam) j->lam[o] = p.lam;
+        }
+    }
+    return NULL;
+}
+
+static int run_jobs(job_t* base, int threads, void* (*fn)(void*), uint64_t* total) {
+    if (threads < 1) threads = 1;
+    if (threads > 256) threads = 256;
+    job_t* jobs = (job_t*)calloc((size_t)threads, sizeof(job_t));
+    pthread_t* th = (pthread_t*)calloc((size_t)threads, sizeof(pthread_t));
+    if (!jobs || !th) {
+        free(jobs);
+        free(th);
+        return -3;
+    }
+    for (int t = 0; t < threads; ++t) {
+        jobs[t] = *base;
+        jobs[t].threads = threads;
+        jobs[t].tid = t;
+        if (t > 0 && pthread_create(&th[t], NULL, fn, &jobs[t]) != 0) {
+            jobs[t].tid = -1; /* run inline below */
+        }
+    }
+    fn(&jobs[0]);
+    for (int t = 1; t < threads; ++t) {
+        if (jobs[t].tid < 0) {
+            jobs[t].tid = t;
+            fn(&jobs[t]);
+        } else {
+            pthread_join(th[t], NULL);
+        }
+    }
+    uint64_t sum = 0;
+    for (int t = 0; t < threads; ++t) sum += jobs[t].total;
+    if (total) *total = sum;
+    free(jobs);
+    free(th);
+    return 0;
+}
+
+int geo_oracle_render_f32(const geo_frame* f, const geo_scene* s, const float* fan, uint32_t n_fan,
+                          const uint8_t* sky, uint32_t sky_w, uint32_t sky_h, uint32_t width,
+                          uint32_t height, uint32_t row0, uint32_t nrows, uint32_t row_step,
+                          int threads, uint8_t* rgba, uint8_t* mask, float* uv, uint32_t* steps,
+                          uint64_t* steps_total) {
+    if (!f || !s || !sky || !rgba || width == 0 || height == 0 || row_step == 0) return -1;
+    if ((uint64_t)row0 + (uint64_t)(nrows ? nrows - 1 : 0) * row_step >= height) return -1;
+    if (s->mode == GEO_MODE_FAN && (!fan || n_fan < 2)) return -1;
+    job_t j;
+    memset(&j, 0, sizeof(j));
+    j.f = f;
+    j.s = s;
+    j.k = make_fconsts(s);
+    j.fan = fan;
+    j.n_fan = n_fan;
+    j.sky = (const uint32_t*)sky;
+    j.sw = sky_w;
+    j.sh = sky_h;
+    j.width = width;
+    j.height = height;
+    j.row0 = row0;
+    j.nrows = nrows;
+    j.row_step = row_step;
+    j.rgba = rgba;
+    j.mask = mask;
+    j.uv = uv;
+    j.steps = steps;
+    return run_jobs(&j, threads, job_f32, steps_total);
+}
+
+int geo_oracle_render_f64(const geo_frame* f, const geo_scene* s, const float* fan, uint32_t n_fan,
+                          uint32_t width, uint32_t height, uint32_t row0, uint32_t nrows,
+                          int threads, uint8_t* mask, float* uv, uint32_t* steps, double* lam) {
+    if (!f || !s || width == 0 || height == 0 || (uint64_t)row0 + nrows > height) return -1;
+    if (s->mode == GEO_MODE_FAN && (!fan || n_fan < 2)) return -1;
+    job_t j;
+    memset(&j, 0, sizeof(j));
+    j.f = f;
+    j.s = s;
+    j.fan = fan;
+    j.n_fan = n_fan;
+    j.width = width;
+    j.height = height;
+    j.row0 = row0;
+    j.nrows = nrows;
+    j.mask = mask;
+    j.uv = uv;
+    j.steps = steps;
+    j.lam = lam;
+    return run_jobs(&j, threads, job_f64, NULL);
+}
+
+/* ------------------------------------------------------------------ */
+/* Observer (observer.rs:68-87, 141-160, 197-262; glam 0.25 semantics)  */
+/* ------------------------------------------------------------------ */
+
+typedef struct { double x, y, z; } ov3;
+typedef struct { ov3 c[3]; } om3; /* column-major */
+
+static double olen(ov3 a) { return sqrt(a.x * a.x + a.y * a.y + a.z * a.z); }
+static ov3 ocross(ov3 a, ov3 b) {
+    ov3 r = {a.y * b.z - b.y * a.z, a.z * b.x - b.z * a.x, a.x * b.y - b.x * a.y};
+    return r;
+}
+static ov3 omv(const om3* m, ov3 v) {
+    ov3 r;
+    r.x = m->c[0].x * v.x + m->c[1].x * v.y + m->c[2].x * v.z;
+    r.y = m->c[0].y * v.x + m->c[1].y * v.y + m->c[2].y * v.z;
+    r.z = m->c[0].z * v.x + m->c[1].z * v.y + m->c[2].z * v.z;
+    return r;
+}
+static om3 omm(const om3* a, const om3* b) {
+    om3 r;
+    for (int i = 0; i < 3; ++i) r.c[i] = omv(a, b->c[i]);
+    return r;
+}
+static om3 otr(const om3* m) {
+    om3 r;
+    r.c[0].x = m->c[0].x; r.c[0].y = m->c[1].x; r.c[0].z = m->c[2].x;
+    r.c[1].x = m->c[0].y; r.c[1].y = m->c[1].y; r.c[1].z = m->c[2].y;
+    r.c[2].x = m->c[0].z; r.c[2].y = m->c[1].z; r.c[2].z = m->c[2].z;
+    return r;
+}
+/* polar_transformations.rs:43-51 */
+static om3 olook(ov3 t) {
+    double inv = 1.0 / olen(t);
+    ov3 z = {t.x * inv, t.y * inv, t.z * inv};
+    double pr = olen(z), pphi = 0., plam = 0.;
+    if (pr != 0.) {
+        pphi = atan2(z.y, z.x);
+        plam = asin(z.z / pr);
+    }
+    plam -= O_FRAC_PI_2;
+    ov3 x = {pr * cos(pphi) * cos(plam), pr * sin(pphi) * cos(plam), pr * sin(plam)};
+    ov3 y = ocross(z, x);
+    om3 m = {{x, y, z}};
+    return m;
+}
+
+void geo_oracle_observer_frame(double rs, double fov, double width, double height, const double pos[3],
+                               double cam_phi, double cam_theta, int state, double energy, geo_frame* out) {
+    ov3 p = {pos[0], pos[1], pos[2]};
+    double r = olen(p);
+    double hr = 1. - rs / r;
+    double vx, vy;
+    /* unmoving_velocity / frozen_fall_velocity (observer.rs:141-160) */
+    int unmoving = (state == GEO_OBSERVER_UNMOVING) || (energy * energy < hr);
+    if (unmoving) {
+        if (r > rs) {
+            vx = 1. / sqrt(hr);
+            vy = 0.;
+        } else {
+            vx = 0.;
+            vy = -sqrt(-hr);
+        }
+    } else {
+        vx = energy / hr;
+        vy = sqrt(energy * energy - hr);
+    }
+    double psi = r > rs ? vx * vx * hr : -vy * vy / hr;
+    if (psi - 1. < 1e-10) psi = 1.;
+    ov3 np = {-p.x, -p.y, -p.z};
+    om3 l = olook(np);
+    om3 std_to_central = otr(&l);
+    om3 cu = olook(p);
+    om3 flip = {{{1, 0, 0}, {0, -1, 0}, {0, 0, 1}}};
+    om3 central_to_uv = omm(&cu, &flip);
+    ov3 camv = {cos(cam_phi) * cos(cam_theta), sin(cam_phi) * cos(cam_theta), sin(cam_theta)};
+    om3 cam_to_std = olook(camv);
+    om3 cam = omm(&std_to_central, &cam_to_std);
+    double t = tan(fov / 2.);
+    double fov_scaling[4] = {t, t * (width / height), 1., 1.};
+    memset(out, 0, sizeof(*out));
+    for (int c = 0; c < 3; ++c) {
+        out->display_to_movement[c * 4 + 0] = (float)cam.c[c].x;
+        out->display_to_movement[c * 4 + 1] = (float)cam.c[c].y;
+        out->display_to_movement[c * 4 + 2] = (float)cam.c[c].z;
+        out->central_to_uv[c * 4 + 0] = (float)central_to_uv.c[c].x;
+        out->central_to_uv[c * 4 + 1] = (float)central_to_uv.c[c].y;
+        out->central_to_uv[c * 4 + 2] = (float)central_to_uv.c[c].z;
+        out->movement_to_central[c * 4 + c] = 1.f;
+    }
+    for (int i = 0; i < 4; ++i) out->display_to_movement[12 + i] = (float)fov_scaling[i];
+    out->movement_to_central[15] = 1.f;
+    out->central_to_uv[15] = 1.f;
+    out->psi_factor_and_position[0] = (float)sqrt((psi - 1.) / psi);
+    out->psi_factor_and_position[1] = (float)p.x;
+    out->psi_factor_and_position[2] = (float)p.y;
+    out->psi_factor_and_position[3] = (float)p.z;
+}

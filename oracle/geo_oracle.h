@@ -1,0 +1,81 @@
+/*
+ * geo_oracle.h — ORACLE (test infrastructure only; never linked into, called
+ * by, or shipped with libgeo.so).  Only tests/, __graft_entry__.smoke() and
+ * bench.py's cpu_baseline leg may load it, and only as the checker.
+ *
+ * PARITY UNPINNED against the reference's own outputs: the reference
+ * (Rust + WGSL, wgpu 0.19) cannot be built here (no cargo/rustc; the
+ * wgpu_renderer submodule is empty) and its only hot-path test,
+ * sphere_geodesics_test (SR/simulation/tests.rs:8-13), asserts nothing.  The
+ * oracle is pinned instead by analytic known-answer tests (flat space,
+ * capture threshold, scale invariance, radial rays: tests/test_oracle_kat.py)
+ * and by committed golden vectors of its own output (tests/golden/).
+ *
+ * Contents:
+ *   f64 restatements, operation for operation, of the reference:
+ *     geo_oracle_solve_geodesic_f64   sphere_ray_tracer.rs:60-193
+ *     geo_oracle_solve_ray_fan_f64    sphere_ray_tracer.rs:35-56
+ *     geo_oracle_pixel_f64            shader.wgsl:57-106 (direct or fan mode)
+ *     geo_oracle_observer_frame       observer.rs:197-262 + polar_transformations.rs
+ *   f32 restatement of the kernel's fixed evaluation order (bit-exact checker):
+ *     geo_oracle_pixel_f32 / geo_oracle_render_f32
+ */
+#ifndef GEO_ORACLE_H
+#define GEO_ORACLE_H
+
+#include <stdint.h>
+
+#include "../include/geo/geo.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct geo_oracle_px {
+    double lam;     /* PI/2 - traveled angle (or fan lerp) */
+    double u, v;    /* sky-sphere UV */
+    double theta;   /* angle to the black hole (lambda after movement_to_central) */
+    uint32_t steps; /* executed main-loop RK4 steps */
+    int bh;         /* 1 = black hole / discard */
+} geo_oracle_px;
+
+double geo_oracle_solve_geodesic_f64(double sphere_r, double schwarz_r, uint32_t max_iter,
+                                     double step, double r, double energy, double rotation,
+                                     int r_falling, uint32_t* steps);
+void geo_oracle_solve_ray_fan_f64(double sphere_r, double schwarz_r, uint32_t max_iter,
+                                  double step, uint32_t nr_nodes, double r, float* fan_out);
+/* One node of solve_ray_fan at an arbitrary theta (sphere_ray_tracer.rs:38-52),
+ * returning the traveled angle. */
+double geo_oracle_geodesic_at_theta_f64(double sphere_r, double schwarz_r, uint32_t max_iter,
+                                        double step, double r, double theta, uint32_t* steps);
+
+void geo_oracle_pixel_f64(const geo_frame* f, const geo_scene* s, const float* fan, uint32_t n_fan,
+                          uint32_t width, uint32_t height, uint32_t px, uint32_t py,
+                          geo_oracle_px* out);
+int geo_oracle_render_f64(const geo_frame* f, const geo_scene* s, const float* fan, uint32_t n_fan,
+                          uint32_t width, uint32_t height, uint32_t row0, uint32_t nrows,
+                          int threads, uint8_t* mask, float* uv, uint32_t* steps, double* lam);
+
+/* f32 kernel mirror.  rgba/mask/uv/steps may be NULL (except rgba). */
+int geo_oracle_render_f32(const geo_frame* f, const geo_scene* s, const float* fan, uint32_t n_fan,
+                          const uint8_t* sky, uint32_t sky_w, uint32_t sky_h, uint32_t width,
+                          uint32_t height, uint32_t row0, uint32_t nrows, uint32_t row_step,
+                          int threads, uint8_t* rgba, uint8_t* mask, float* uv, uint32_t* steps,
+                          uint64_t* steps_total);
+
+/* Observer::calc_transformation_pipeline for a fixed pose (observer.rs:68-87,
+ * 141-160, 197-262); state = GEO_OBSERVER_UNMOVING or GEO_OBSERVER_FROZEN_FALL. */
+void geo_oracle_observer_frame(double schwarz_r, double fov, double width, double height,
+                               const double pos[3], double cam_phi, double cam_theta, int state,
+                               double energy, geo_frame* out);
+
+/* f32 math kernels, exported for accuracy tests */
+float geo_oracle_asinf(float x);
+float geo_oracle_atan2f(float y, float x);
+void geo_oracle_sincosf(float x, float* s, float* c);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif

@@ -1,0 +1,90 @@
+// geo_math.h — f32 transcendentals with a fixed, fully specified evaluation
+// order (explicit fmaf, no contraction), so that the gfx950 kernel and a
+// host build of the same sequence produce bit-identical results.
+//
+// Why: the per-pixel hit-classification mask must match the CPU path pixel
+// for pixel (BASELINE.json north_star).  ROCm OCML and glibc differ by a few
+// ULP in asinf/atan2f/sinf, enough to flip pixels on the photon-ring edge.
+// Only IEEE-exact operations are used: + - * / sqrt fma rint fabs copysign
+// min max and compares; compile with -ffp-contract=off and correctly rounded
+// f32 divide/sqrt (hipcc default, pinned by -fhip-fp32-correctly-rounded-divide-sqrt).
+//
+// Algorithms: Cody-Waite reduction by pi/2 plus Cephes-style minimax
+// polynomials (sin/cos on [-pi/4, pi/4], asin on [0, 1/2], atan on
+// [-(sqrt2-1), sqrt2-1]).  Accuracy is checked against libm in
+// tests/test_math.py (<= 3 ulp / 2e-7 abs on the ranges used).
+#pragma once
+
+#if defined(__HIPCC__) || defined(__HIP__)
+#define GEO_HD __host__ __device__ __forceinline__
+#else
+#define GEO_HD static inline
+#endif
+
+namespace geo {
+
+constexpr float kPi = 3.14159265358979323846f;
+constexpr float kPi2 = 1.57079632679489661923f;   // PI/2 (shader.wgsl:23 M_PI_2)
+constexpr float kPi4 = 0.785398163397448309616f;
+constexpr float kTwoOverPi = 0.636619772367581343076f;
+constexpr float kInvPi = 0.318309886183790671538f;
+constexpr float kInvTwoPi = 0.159154943091895335769f;
+
+GEO_HD float fmaf_(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
+GEO_HD float clampf_(float x, float lo, float hi) { return x < lo ? lo : (x > hi ? hi : x); }
+// max(a, b) with a NaN `a` mapped to b (used to clamp radicands at 0).
+GEO_HD float fmaxf_(float a, float b) { return a > b ? a : b; }
+
+// sin and cos of x, |x| < ~1e4.
+GEO_HD void sincosf_(float x, float* s, float* c) {
+    const float j = __builtin_rintf(x * kTwoOverPi);
+    float r = fmaf_(-j, 1.5703125f, x);
+    r = fmaf_(-j, 4.837512969970703125e-4f, r);
+    r = fmaf_(-j, 7.54978995489188216e-8f, r);
+    const float z = r * r;
+    const float ps = fmaf_(fmaf_(-1.9515295891e-4f, z, 8.3321608736e-3f), z, -1.6666654611e-1f);
+    const float sn = fmaf_(ps * z, r, r);
+    const float pc = fmaf_(fmaf_(2.443315711809948e-5f, z, -1.388731625493765e-3f), z,
+                           4.166664568298827e-2f);
+    const float cs = fmaf_(pc * z, z, fmaf_(-0.5f, z, 1.0f));
+    const int q = ((int)j) & 3;
+    const float sa = (q & 1) ? cs : sn;
+    const float ca = (q & 1) ? sn : cs;
+    *s = (q & 2) ? -sa : sa;
+    *c = ((q + 1) & 2) ? -ca : ca;
+}
+
+// asin(x) for x in [-1, 1] (clamped).
+GEO_HD float asinf_(float x) {
+    x = clampf_(x, -1.0f, 1.0f);
+    const float a = __builtin_fabsf(x);
+    const bool big = a > 0.5f;
+    const float z = big ? 0.5f * (1.0f - a) : a * a;
+    const float s = big ? __builtin_sqrtf(z) : a;
+    const float p = fmaf_(fmaf_(fmaf_(fmaf_(4.2163199048e-2f, z, 2.4181311049e-2f), z,
+                                      4.5470025998e-2f), z, 7.4953002686e-2f), z,
+                          1.6666752422e-1f);
+    float r = fmaf_(p * z, s, s);
+    r = big ? fmaf_(-2.0f, r, kPi2) : r;
+    return __builtin_copysignf(r, x);
+}
+
+// atan2(y, x); atan2(0, 0) = 0.
+GEO_HD float atan2f_(float y, float x) {
+    const float ay = __builtin_fabsf(y);
+    const float ax = __builtin_fabsf(x);
+    const bool big = ay > 2.414213562373095f * ax;
+    const bool mid = ay > 0.4142135623730950f * ax;
+    const float num = big ? -ax : (mid ? ay - ax : ay);
+    const float den = big ? ay : (mid ? ay + ax : ax);
+    const float y0 = big ? kPi2 : (mid ? kPi4 : 0.0f);
+    const float t = den > 0.0f ? num / den : 0.0f;
+    const float z = t * t;
+    const float p = fmaf_(fmaf_(fmaf_(8.05374449538e-2f, z, -1.38776856032e-1f), z,
+                                1.99777106478e-1f), z, -3.33329491539e-1f);
+    float r = y0 + fmaf_(p * z, t, t);
+    r = (x < 0.0f) ? kPi - r : r;
+    return __builtin_copysignf(r, y);
+}
+
+}  // namespace geo

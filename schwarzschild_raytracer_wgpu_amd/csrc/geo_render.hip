@@ -1,0 +1,453 @@
+// geo_render.hip — gfx950 kernels and the device half of the libgeo C-ABI.
+//
+//   geo_render_kernel<MODE>  per-pixel fs_main + solve_geodesic
+//                            (SR/schwarzschild_sphere_shader/shader.wgsl:57-106,
+//                             SR/simulation/sphere_ray_tracer.rs:35-193)
+//   geo_fan_kernel           SphereRayTracer::solve_ray_fan in f64, one lane per node
+//                            (sphere_ray_tracer.rs:35-193)
+//   geo_steps_finalize       folds the sharded step counters into the caller's u64
+//
+// Work decomposition: one 256-thread workgroup per 16x16 pixel tile, each
+// wave64 a 16x4 sub-tile (compact 2-D footprint = coherent step counts);
+// the frame uniform rides in the kernarg segment (SGPRs, wave-uniform), the
+// ray fan is staged in LDS; per-lane ray state lives in VGPRs.  The hot loop
+// is pure FP32 VALU — no MFMA, no LDS, no memory traffic.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <new>
+
+#include "../../include/geo/geo.h"
+#include "geo_pixel.h"
+
+namespace {
+
+constexpr int kTileW = 16;
+constexpr int kTileH = 16;
+constexpr int kBlock = kTileW * kTileH;  // 256 threads = 4 waves
+constexpr uint32_t kMaxFan = 4096;       // LDS fan capacity (16 KiB)
+constexpr int kStepSlots = 64;           // sharded step counters
+constexpr int kSlotStride = 16;          // u64 per slot = 128 B (own cache line)
+
+struct RenderArgs {
+    geo_frame frame;
+    geo::PixelConsts k;  // frame constants, evaluated once on the host (IEEE f32, same bits)
+    uint32_t width, height, row0, nrows;
+    uint32_t band_rows, band_stride;  // local row lr -> row0 + (lr/band_rows)*band_stride + lr%band_rows
+    uint32_t tiles_x;
+    const uint32_t* sky;
+    uint32_t sky_w, sky_h;
+    const float* fan;
+    uint32_t n_fan;
+    uint32_t* out_rgba;
+    uint8_t* out_mask;
+    float2* out_uv;
+    uint32_t* out_steps;
+    unsigned long long* step_slots;
+};
+
+template <int MODE>
+__global__ __launch_bounds__(kBlock) void geo_render_kernel(const RenderArgs a) {
+    __shared__ float s_fan[MODE == GEO_MODE_FAN ? kMaxFan : 1];
+    __shared__ unsigned long long s_red[kBlock / 64];
+    if constexpr (MODE == GEO_MODE_FAN) {
+        for (uint32_t i = threadIdx.x; i < a.n_fan; i += kBlock) s_fan[i] = a.fan[i];
+        __syncthreads();
+    }
+    const uint32_t tx = blockIdx.x % a.tiles_x;
+    const uint32_t ty = blockIdx.x / a.tiles_x;
+    const uint32_t px = tx * kTileW + (threadIdx.x % kTileW);
+    const uint32_t ly = ty * kTileH + (threadIdx.x / kTileW);
+    uint32_t steps = 0;
+    const uint32_t py = a.row0 + (ly / a.band_rows) * a.band_stride + (ly % a.band_rows);
+    if (px < a.width && ly < a.nrows && py < a.height) {
+        float c2x, c2y, c2z;
+        geo::pixel_central_dir(a.frame.display_to_movement, a.frame.movement_to_central,
+                               a.frame.psi_factor_and_position[0], a.width, a.height, px, py,
+                               &c2x, &c2y, &c2z);
+        const float st = geo::clampf_(c2z, -1.0f, 1.0f);
+        float lam;
+        if constexpr (MODE == GEO_MODE_FAN) {
+            lam = geo::fan_lerp(s_fan, a.n_fan, st);
+        } else {
+            lam = geo::kPi2 - geo::geodesic_angle(a.k, st, &steps);
+        }
+        const bool bh = lam < geo::kBlackHoleLambda;
+        float U, V;
+        geo::sky_uv(a.frame.central_to_uv, c2x, c2y, lam, &U, &V);
+        const uint32_t* sky = a.sky;
+        const uint32_t rgba = bh ? geo::kBlackRGBA
+                                 : geo::sample_sky([sky](uint32_t i) { return sky[i]; },
+                                                   a.sky_w, a.sky_h, U, V);
+        const size_t o = (size_t)ly * a.width + px;
+        a.out_rgba[o] = rgba;
+        if (a.out_mask) a.out_mask[o] = bh ? 1 : 0;
+        if (a.out_uv) a.out_uv[o] = make_float2(U, V);
+        if (a.out_steps) a.out_steps[o] = steps;
+    }
+    if constexpr (MODE == GEO_MODE_DIRECT) {
+        if (a.step_slots) {
+            unsigned long long s = steps;
+            for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+            if ((threadIdx.x & 63) == 0) s_red[threadIdx.x >> 6] = s;
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                const unsigned long long t = s_red[0] + s_red[1] + s_red[2] + s_red[3];
+                if (t) atomicAdd(&a.step_slots[(blockIdx.x % kStepSlots) * kSlotStride], t);
+            }
+        }
+    }
+}
+
+__global__ void geo_steps_finalize(unsigned long long* slots, unsigned long long* total) {
+    __shared__ unsigned long long s[kStepSlots];
+    const int i = threadIdx.x;
+    s[i] = slots[i * kSlotStride];
+    slots[i * kSlotStride] = 0;
+    __syncthreads();
+    if (i == 0) {
+        unsigned long long t = 0;
+        for (int j = 0; j < kStepSlots; ++j) t += s[j];
+        *total += t;
+    }
+}
+
+// f64 restatement of SphereRayTracer::solve_geodesic (sphere_ray_tracer.rs:60-193),
+// operation for operation (no contraction).
+__device__ double solve_geodesic_f64(double sphere_r, double schwarz_r, uint32_t max_iter,
+                                     double default_step, double r, double energy,
+                                     double rotation, bool r_falling) {
+    const double NO_VALUE = GEO_NO_VALUE;
+    const double PI = 3.14159265358979323846;
+    const double b = rotation / energy;
+    const bool outside = r > schwarz_r;
+    const bool sphere_outside = sphere_r > schwarz_r;
+    const bool inside_sphere = r < sphere_r;
+    if (rotation < 1e-10) {
+        if (inside_sphere) {
+            if (outside) {
+                if (r_falling) return schwarz_r == 0. ? PI : NO_VALUE;
+                return 0.;
+            }
+            if (sphere_outside) return energy > 0. ? 0. : NO_VALUE;
+            return 0.;
+        }
+        return (sphere_outside && r_falling) ? 0. : NO_VALUE;
+    }
+    const bool barrier_3r_2 = (schwarz_r > 0.) && 1. / (b * b) < 4. / (27. * schwarz_r * schwarz_r);
+    const double r3_2 = 3. * schwarz_r / 2.;
+    const bool different_sides_3r_2 = ((r < r3_2) != (sphere_r < r3_2)) && fabs(r - r3_2) > 1e-10;
+    if ((inside_sphere && !sphere_outside) || (!outside && sphere_outside && energy < 0.) ||
+        (barrier_3r_2 && different_sides_3r_2) || (r < r3_2 && inside_sphere && r_falling) ||
+        (r > r3_2 && !inside_sphere && !r_falling)) {
+        return NO_VALUE;
+    }
+    double u_k = 1. / r;
+    double u_bar_k = (r_falling ? 1. : -1.) * sqrt(1. / (b * b) - (1. - schwarz_r / r) / (r * r));
+    double angle = 0.;
+    uint32_t iteration = 0;
+    const double bound = 0.9 * fmin(u_k, 1. / fmax(sphere_r, r3_2));
+    const double step = default_step;
+    const double step_half = step / 2.;
+    const double sphere_u = 1. / sphere_r;
+    const double schwarz_u = 1. / schwarz_r;
+    while (!(schwarz_r != 0. && u_k > schwarz_u && u_bar_k > 0.) && iteration < max_iter &&
+           u_k > 0.) {
+        double a_u = u_k + step_half * u_bar_k;
+        double a_u_bar = u_bar_k + step_half * (-u_k + r3_2 * u_k * u_k);
+        double b_u = u_k + step_half * a_u_bar;
+        double b_u_bar = u_bar_k + step_half * (-a_u + r3_2 * a_u * a_u);
+        double c_u = u_k + step * b_u_bar;
+        double c_u_bar = u_bar_k + step * (-b_u + r3_2 * b_u * b_u);
+        const double next_u = u_k + step * (u_bar_k + 2. * a_u_bar + 2. * b_u_bar + c_u_bar) / 6.;
+        const double next_u_bar =
+            u_bar_k + step * ((-u_k + r3_2 * u_k * u_k) + 2. * (-a_u + r3_2 * a_u * a_u) +
+                              2. * (-b_u + r3_2 * b_u * b_u) + (-c_u + r3_2 * c_u * c_u)) / 6.;
+        if ((next_u > sphere_u) != (u_k > sphere_u)) {
+            double newton_u, newton_u_bar, newton_step;
+            if (fabs(u_bar_k) > fabs(next_u_bar)) {
+                newton_step = 0.;
+                newton_u = u_k;
+                newton_u_bar = u_bar_k;
+            } else {
+                newton_step = step;
+                newton_u = next_u;
+                newton_u_bar = next_u_bar;
+            }
+            for (int n = 0; n < 3; ++n) {
+                newton_step -= (newton_u - sphere_u) / newton_u_bar;
+                const double nsh = newton_step / 2.;
+                a_u = u_k + nsh * u_bar_k;
+                a_u_bar = u_bar_k + nsh * (-u_k + r3_2 * u_k * u_k);
+                b_u = u_k + nsh * a_u_bar;
+                b_u_bar = u_bar_k + nsh * (-a_u + r3_2 * a_u * a_u);
+                c_u = u_k + newton_step * b_u_bar;
+                c_u_bar = u_bar_k + newton_step * (-b_u + r3_2 * b_u * b_u);
+                newton_u = u_k + newton_step * (u_bar_k + 2. * a_u_bar + 2. * b_u_bar + c_u_bar) / 6.;
+                newton_u_bar = u_bar_k + newton_step *
+                                             ((-u_k + r3_2 * u_k * u_k) + 2. * (-a_u + r3_2 * a_u * a_u) +
+                                              2. * (-b_u + r3_2 * b_u * b_u) + (-c_u + r3_2 * c_u * c_u)) /
+                                             6.;
+            }
+            return angle + newton_step;
+        }
+        if (next_u < bound) return NO_VALUE;
+        u_k = next_u;
+        u_bar_k = next_u_bar;
+        iteration += 1;
+        angle += step;
+    }
+    return NO_VALUE;
+}
+
+__global__ void geo_fan_kernel(double sphere_r, double schwarz_r, uint32_t max_iter, double step,
+                               uint32_t n, double r, float* fan) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const double PI = 3.14159265358979323846;
+    const double FRAC_PI_2 = 1.57079632679489661923;
+    // solve_ray_fan (sphere_ray_tracer.rs:37-53)
+    const double theta = FRAC_PI_2 - PI * (double)i / ((double)n - 1.);
+    const double rotation = r * cos(theta);
+    bool r_falling;
+    double energy;
+    if (r < schwarz_r) {
+        r_falling = false;
+        energy = sin(-theta) * sqrt(-1. + schwarz_r / r);
+    } else {
+        r_falling = theta > 0.;
+        energy = sqrt(1. - schwarz_r / r);
+    }
+    fan[i] = (float)(FRAC_PI_2 -
+                     solve_geodesic_f64(sphere_r, schwarz_r, max_iter, step, r, energy, rotation, r_falling));
+}
+
+}  // namespace
+
+struct geo_ctx {
+    int device;
+    int num_cus;
+    uint32_t launch_blocks;
+    uint32_t* sky;
+    uint32_t sky_w, sky_h;
+    float* fan;
+    uint32_t fan_cap, n_fan;
+    unsigned long long* step_slots;
+};
+
+namespace {
+
+struct DeviceGuard {
+    int prev = -1;
+    bool ok = false;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        ok = hipSetDevice(dev) == hipSuccess;
+    }
+    ~DeviceGuard() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
+}  // namespace
+
+extern "C" {
+
+int geo_abi_version(void) { return GEO_ABI_VERSION; }
+
+const char* geo_status_str(int status) {
+    switch (status) {
+        case GEO_OK: return "ok";
+        case GEO_EINVAL: return "invalid argument";
+        case GEO_EHIP: return "HIP runtime error";
+        case GEO_ENOMEM: return "out of memory";
+        case GEO_ENODEV: return "no such HIP device";
+        case GEO_ESTATE: return "call out of order";
+        default: return "unknown status";
+    }
+}
+
+int geo_ctx_create(int device, geo_ctx** out) {
+    if (!out) return GEO_EINVAL;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return GEO_ENODEV;
+    DeviceGuard g(device);
+    if (!g.ok) return GEO_EHIP;
+    geo_ctx* c = new (std::nothrow) geo_ctx();
+    if (!c) return GEO_ENOMEM;
+    c->device = device;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) {
+        delete c;
+        return GEO_EHIP;
+    }
+    c->num_cus = prop.multiProcessorCount;
+    c->launch_blocks = 0;
+    if (hipMalloc(&c->step_slots, sizeof(unsigned long long) * kStepSlots * kSlotStride) != hipSuccess) {
+        delete c;
+        return GEO_ENOMEM;
+    }
+    if (hipMemset(c->step_slots, 0, sizeof(unsigned long long) * kStepSlots * kSlotStride) != hipSuccess) {
+        (void)hipFree(c->step_slots);
+        delete c;
+        return GEO_EHIP;
+    }
+    *out = c;
+    return GEO_OK;
+}
+
+void geo_ctx_destroy(geo_ctx* c) {
+    if (!c) return;
+    DeviceGuard g(c->device);
+    if (c->sky) (void)hipFree(c->sky);
+    if (c->fan) (void)hipFree(c->fan);
+    if (c->step_slots) (void)hipFree(c->step_slots);
+    delete c;
+}
+
+int geo_set_sky(geo_ctx* c, const uint8_t* rgba8, uint32_t w, uint32_t h) {
+    if (!c || !rgba8 || w == 0 || h == 0 || (uint64_t)w * h > (1ull << 31)) return GEO_EINVAL;
+    DeviceGuard g(c->device);
+    if (!g.ok) return GEO_EHIP;
+    const size_t bytes = (size_t)w * h * 4;
+    if (c->sky && (uint64_t)c->sky_w * c->sky_h != (uint64_t)w * h) {
+        (void)hipFree(c->sky);
+        c->sky = nullptr;
+    }
+    if (!c->sky && hipMalloc(&c->sky, bytes) != hipSuccess) {
+        c->sky = nullptr;
+        return GEO_ENOMEM;
+    }
+    if (hipMemcpy(c->sky, rgba8, bytes, hipMemcpyHostToDevice) != hipSuccess) return GEO_EHIP;
+    c->sky_w = w;
+    c->sky_h = h;
+    return GEO_OK;
+}
+
+static int ensure_fan(geo_ctx* c, uint32_t n) {
+    if (c->fan && c->fan_cap >= n) return GEO_OK;
+    if (c->fan) (void)hipFree(c->fan);
+    c->fan = nullptr;
+    c->fan_cap = 0;
+    if (hipMalloc(&c->fan, sizeof(float) * n) != hipSuccess) return GEO_ENOMEM;
+    c->fan_cap = n;
+    return GEO_OK;
+}
+
+int geo_set_fan(geo_ctx* c, const float* fan, uint32_t n) {
+    if (!c || !fan || n < 2 || n > kMaxFan) return GEO_EINVAL;
+    DeviceGuard g(c->device);
+    if (!g.ok) return GEO_EHIP;
+    int st = ensure_fan(c, n);
+    if (st) return st;
+    if (hipMemcpy(c->fan, fan, sizeof(float) * n, hipMemcpyHostToDevice) != hipSuccess) return GEO_EHIP;
+    c->n_fan = n;
+    return GEO_OK;
+}
+
+int geo_solve_ray_fan(geo_ctx* c, double sphere_r, double schwarz_r, uint32_t max_iter, double step,
+                      uint32_t nr_nodes, double r, float* fan_out, void* stream) {
+    if (!c || nr_nodes < 2 || nr_nodes > kMaxFan || !(step > 0.)) return GEO_EINVAL;
+    DeviceGuard g(c->device);
+    if (!g.ok) return GEO_EHIP;
+    int st = ensure_fan(c, nr_nodes);
+    if (st) return st;
+    hipStream_t s = (hipStream_t)stream;
+    hipLaunchKernelGGL(geo_fan_kernel, dim3((nr_nodes + 63) / 64), dim3(64), 0, s, sphere_r,
+                       schwarz_r, max_iter, step, nr_nodes, r, c->fan);
+    if (hipGetLastError() != hipSuccess) return GEO_EHIP;
+    c->n_fan = nr_nodes;
+    if (fan_out) {
+        if (hipMemcpyAsync(fan_out, c->fan, sizeof(float) * nr_nodes, hipMemcpyDeviceToHost, s) !=
+            hipSuccess)
+            return GEO_EHIP;
+        if (hipStreamSynchronize(s) != hipSuccess) return GEO_EHIP;
+    }
+    return GEO_OK;
+}
+
+int geo_set_launch_blocks(geo_ctx* c, uint32_t blocks) {
+    if (!c) return GEO_EINVAL;
+    c->launch_blocks = blocks;
+    return GEO_OK;
+}
+
+static int render_impl(geo_ctx* c, const geo_frame* frame, const geo_scene* scene, uint32_t width,
+                       uint32_t height, uint32_t row0, uint32_t nrows, uint32_t band_rows,
+                       uint32_t band_stride, uint8_t* out_rgba8, uint8_t* out_mask, float* out_uv,
+                       uint32_t* out_steps, unsigned long long* steps_total, void* stream) {
+    if (scene->mode != GEO_MODE_DIRECT && scene->mode != GEO_MODE_FAN) return GEO_EINVAL;
+    if (scene->flags != 0 || scene->reserved != 0) return GEO_EINVAL;
+    if (!c->sky) return GEO_ESTATE;
+    if (scene->mode == GEO_MODE_FAN && (!c->fan || c->n_fan < 2)) return GEO_ESTATE;
+    if (scene->mode == GEO_MODE_DIRECT && !(scene->step > 0.0f)) return GEO_EINVAL;
+    DeviceGuard g(c->device);
+    if (!g.ok) return GEO_EHIP;
+    RenderArgs a;
+    std::memcpy(&a.frame, frame, sizeof(geo_frame));
+    a.k = geo::make_consts(scene->rs, scene->sphere_r, scene->r_obs, scene->step, scene->max_steps);
+    a.width = width;
+    a.height = height;
+    a.row0 = row0;
+    a.nrows = nrows;
+    a.band_rows = band_rows;
+    a.band_stride = band_stride;
+    a.tiles_x = (width + kTileW - 1) / kTileW;
+    const uint32_t tiles_y = (nrows + kTileH - 1) / kTileH;
+    a.sky = c->sky;
+    a.sky_w = c->sky_w;
+    a.sky_h = c->sky_h;
+    a.fan = c->fan;
+    a.n_fan = c->n_fan;
+    a.out_rgba = reinterpret_cast<uint32_t*>(out_rgba8);
+    a.out_mask = out_mask;
+    a.out_uv = reinterpret_cast<float2*>(out_uv);
+    a.out_steps = out_steps;
+    a.step_slots = steps_total ? c->step_slots : nullptr;
+    hipStream_t s = (hipStream_t)stream;
+    const dim3 grid(a.tiles_x * tiles_y);
+    if (scene->mode == GEO_MODE_FAN)
+        hipLaunchKernelGGL(geo_render_kernel<GEO_MODE_FAN>, grid, dim3(kBlock), 0, s, a);
+    else
+        hipLaunchKernelGGL(geo_render_kernel<GEO_MODE_DIRECT>, grid, dim3(kBlock), 0, s, a);
+    if (hipGetLastError() != hipSuccess) return GEO_EHIP;
+    if (steps_total && scene->mode == GEO_MODE_DIRECT) {
+        hipLaunchKernelGGL(geo_steps_finalize, dim3(1), dim3(kStepSlots), 0, s, c->step_slots,
+                           steps_total);
+        if (hipGetLastError() != hipSuccess) return GEO_EHIP;
+    }
+    return GEO_OK;
+}
+
+int geo_render_rows(geo_ctx* c, const geo_frame* frame, const geo_scene* scene, uint32_t width,
+                    uint32_t height, uint32_t row0, uint32_t nrows, uint8_t* out_rgba8,
+                    uint8_t* out_mask, float* out_uv, uint32_t* out_steps,
+                    unsigned long long* steps_total, void* stream) {
+    if (!c || !frame || !scene || !out_rgba8 || width == 0 || height == 0 || nrows == 0)
+        return GEO_EINVAL;
+    if ((uint64_t)row0 + nrows > height || width > (1u << 20) || height > (1u << 20))
+        return GEO_EINVAL;
+    return render_impl(c, frame, scene, width, height, row0, nrows, nrows, nrows, out_rgba8, out_mask,
+                       out_uv, out_steps, steps_total, stream);
+}
+
+int geo_render_bands(geo_ctx* c, const geo_frame* frame, const geo_scene* scene, uint32_t width,
+                     uint32_t height, uint32_t band_rows, uint32_t band0, uint32_t band_step,
+                     uint32_t nbands, uint8_t* out_rgba8, uint8_t* out_mask, float* out_uv,
+                     uint32_t* out_steps, unsigned long long* steps_total, void* stream) {
+    if (!c || !frame || !scene || !out_rgba8 || width == 0 || height == 0 || band_rows == 0 ||
+        nbands == 0 || band_step == 0)
+        return GEO_EINVAL;
+    if (width > (1u << 20) || height > (1u << 20)) return GEO_EINVAL;
+    const uint64_t first = (uint64_t)band0 * band_rows;
+    const uint64_t last = first + (uint64_t)(nbands - 1) * band_step * band_rows;
+    const uint64_t nrows = (uint64_t)nbands * band_rows;
+    if (first >= height || last >= height || nrows > (1u << 20)) return GEO_EINVAL;
+    return render_impl(c, frame, scene, width, height, (uint32_t)first, (uint32_t)nrows, band_rows,
+                       band_step * band_rows, out_rgba8, out_mask, out_uv, out_steps, steps_total,
+                       stream);
+}
+
+}  // extern "C"

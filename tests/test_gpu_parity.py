@@ -1,0 +1,239 @@
+"""HIP kernel parity (through the C-ABI) against the CPU oracle.
+
+Bar (BASELINE.json north_star): hit-classification mask identical pixel for
+pixel, sky UV within 1e-4 relative.  The kernel and the oracle's f32 mirror
+evaluate the same fixed operation sequence, so we require MORE: mask, UV,
+steps and RGBA bit-identical.  UV_TOL is the stated tolerance, checked too.
+"""
+import ctypes
+import math
+import os
+
+import numpy as np
+import pytest
+
+import oracle as O
+from helpers import R_OBS, default_frame, default_scene, wrap_du
+
+pytestmark = pytest.mark.gpu
+
+UV_TOL = 1e-4  # relative, north_star
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+@pytest.fixture(scope="module")
+def torch_mod():
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    return torch
+
+
+@pytest.fixture(scope="module")
+def geo():
+    import schwarzschild_raytracer_wgpu_amd as g
+
+    return g
+
+
+def render(g, torch, ctx, frame, scene, w, h, row0=0, nrows=None):
+    nrows = h - row0 if nrows is None else nrows
+    dev = torch.device("cuda:0")
+    rgba = torch.empty(nrows * w * 4, dtype=torch.uint8, device=dev)
+    mask = torch.empty(nrows * w, dtype=torch.uint8, device=dev)
+    uv = torch.empty(nrows * w * 2, dtype=torch.float32, device=dev)
+    steps = torch.empty(nrows * w, dtype=torch.int32, device=dev)
+    total = torch.zeros(1, dtype=torch.int64, device=dev)
+    ctx.render_rows(frame, scene, w, h, row0, nrows, rgba, mask, uv, steps, total)
+    torch.cuda.synchronize()
+    return dict(rgba=rgba.cpu().numpy().reshape(nrows, w, 4), mask=mask.cpu().numpy().reshape(nrows, w),
+                uv=uv.cpu().numpy().reshape(nrows, w, 2),
+                steps=steps.cpu().numpy().view(np.uint32).reshape(nrows, w), total=int(total.item()))
+
+
+def assert_same(hip, ref, fields=("mask", "uv", "steps", "rgba")):
+    for f in fields:
+        a, b = hip[f], ref[f]
+        if f == "uv":
+            assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), (
+                f"uv differs at {np.argwhere(a.view(np.uint32) != b.view(np.uint32))[:5]}")
+        else:
+            bad = np.argwhere(a != b)
+            assert bad.size == 0, f"{f} differs at {len(bad)} places, first {bad[:5]}"
+    # the stated tolerance, for the record
+    d = wrap_du(hip["uv"], ref["uv"])
+    assert float(d.max()) <= UV_TOL
+
+
+def make_ctx(g, sky):
+    ctx = g.Context(0)
+    ctx.set_sky(sky)
+    return ctx
+
+
+def test_golden_fixture_bitexact(geo, torch_mod):
+    z = np.load(os.path.join(GOLD, "pixels_64x36.npz"))
+    frame = geo.GeoFrame.from_buffer_copy(z["frame"].tobytes())
+    ctx = make_ctx(geo, z["sky"])
+    hip = render(geo, torch_mod, ctx, frame, default_scene(2048), 64, 36)
+    assert_same(hip, dict(rgba=z["f32_rgba"], mask=z["f32_mask"], uv=z["f32_uv"], steps=z["f32_steps"]))
+    assert hip["total"] == int(z["f32_steps"].sum())
+    # against the f64 literal restatement: mask identical on this frame, UV close
+    assert np.array_equal(hip["mask"], z["f64_mask"])
+    nb = z["f64_mask"] == 0
+    assert wrap_du(hip["uv"], z["f64_uv"])[nb].max() < 2e-4
+
+
+SCENES = [
+    # name, w, h, frame kwargs, scene kwargs, sky
+    ("cfg1_256_flat", 256, 256, {}, dict(max_steps=128), "flat"),
+    ("odd_333x187", 333, 187, {}, dict(max_steps=512), "equirect"),
+    ("unmoving", 160, 90, dict(state=0), dict(max_steps=512), "equirect"),
+    ("offaxis_inside_photon_sphere", 192, 108, dict(pos=(1.3 * math.cos(0.2), 1.3 * math.sin(0.2), 0.05),
+                                                      camera=(math.pi + 0.6, 0.3)),
+     dict(max_steps=2048, r_obs=math.sqrt(1.3 ** 2 + 0.05 ** 2)), "equirect"),
+    ("inside_horizon", 128, 128, dict(pos=(0.8, 0.0, 0.05)), dict(max_steps=512, r_obs=math.sqrt(0.64 + 0.0025)),
+     "equirect"),
+    ("flat_space", 128, 72, dict(rs=0.0, state=0), dict(rs=0.0, max_steps=512), "equirect"),
+    ("far_ref_scale", 200, 120, dict(pos=(25.0, 0.0, 1.0), rs=10.0),
+     dict(rs=10.0, sphere_r=500.0, r_obs=math.sqrt(626.0), max_steps=1000), "equirect"),
+    ("single_row", 97, 1, {}, dict(max_steps=512), "equirect"),
+    ("single_col", 1, 77, {}, dict(max_steps=512), "equirect"),
+]
+
+
+@pytest.mark.parametrize("name,w,h,fk,sk,skykind", SCENES, ids=[s[0] for s in SCENES])
+def test_direct_mode_matches_oracle_bitexact(geo, torch_mod, name, w, h, fk, sk, skykind):
+    from schwarzschild_raytracer_wgpu_amd.scenes import make_sky
+
+    sky = make_sky(skykind, (1, 1) if skykind == "flat" else (512, 256))
+    frame = default_frame(w, h, **fk)
+    scene = default_scene(**sk)
+    ctx = make_ctx(geo, sky)
+    hip = render(geo, torch_mod, ctx, frame, scene, w, h)
+    ref = O.render_f32(frame, scene, sky, w, h, threads=8)
+    assert_same(hip, ref)
+    assert hip["total"] == int(ref["steps"].sum()) == ref["steps_total"]
+
+
+def test_row_blocks_compose_full_frame(geo, torch_mod):
+    from schwarzschild_raytracer_wgpu_amd.scenes import make_sky
+
+    w, h = 320, 181
+    sky = make_sky("equirect", (256, 128))
+    frame, scene = default_frame(w, h), default_scene(2048)
+    ctx = make_ctx(geo, sky)
+    full = render(geo, torch_mod, ctx, frame, scene, w, h)
+    parts = [render(geo, torch_mod, ctx, frame, scene, w, h, r0, n) for r0, n in ((0, 50), (50, 1), (51, 100),
+                                                                                   (151, 30))]
+    for f in ("rgba", "mask", "uv", "steps"):
+        assert np.array_equal(np.concatenate([p[f] for p in parts]), full[f])
+    assert sum(p["total"] for p in parts) == full["total"]
+
+
+def test_fan_kernel_matches_oracle(geo, torch_mod):
+    ctx = geo.Context(0)
+    for args in [(500.0, 10.0, 1000, math.pi / 100, 400, math.sqrt(626.0)),
+                 (100.0, 10.0, 100, math.pi / 100, 20, 25.0),
+                 (50.0, 1.0, 1000, math.pi / 100, 400, R_OBS),
+                 (50.0, 1.0, 1000, math.pi / 100, 400, 0.7),  # inside the horizon
+                 (50.0, 0.0, 1000, math.pi / 100, 64, 3.0)]:  # flat space
+        gpu = ctx.solve_ray_fan(*args)
+        ref = O.solve_ray_fan(*args)
+        # f64 on both sides; device cos/sin may differ from glibc by an f64 ulp,
+        # which survives the f32 rounding at most as one f32 ulp.
+        d = np.abs(gpu.astype(np.float64) - ref)
+        assert np.all(d <= np.spacing(np.abs(ref)).astype(np.float64)), (args, d.max())
+        assert np.mean(gpu == ref) > 0.99
+
+
+def test_sphere_buffer_fan_mode_matches_oracle(geo, torch_mod):
+    """Reference-exact mode: BasicSphereBuffer.update_ray_fan + draw = fan lerp
+    (shader.wgsl:77-84) with the GPU-solved fan."""
+    from schwarzschild_raytracer_wgpu_amd.scenes import make_sky
+
+    w, h = 256, 144
+    sky = make_sky("equirect", (512, 256))
+    ctx = geo.Context(0)
+    buf = geo.BasicSphereBuffer(ctx, 50.0, 1.0, sky, mode=geo.GEO_MODE_FAN)
+    buf.update_ray_fan(R_OBS)
+    fan = buf.ray_tracer.interpolation_grid.copy()
+    frame = default_frame(w, h)
+    dev = torch_mod.device("cuda:0")
+    tgt = geo.RenderTarget(w, h, torch_mod.empty(w * h * 4, dtype=torch_mod.uint8, device=dev),
+                           torch_mod.empty(w * h, dtype=torch_mod.uint8, device=dev),
+                           torch_mod.empty(w * h * 2, dtype=torch_mod.float32, device=dev))
+    buf.draw(frame, tgt)
+    torch_mod.cuda.synchronize()
+    ref = O.render_f32(frame, buf.scene(), sky, w, h, fan=fan, threads=8)
+    hip = dict(rgba=tgt.rgba.cpu().numpy().reshape(h, w, 4), mask=tgt.mask.cpu().numpy().reshape(h, w),
+               uv=tgt.uv.cpu().numpy().reshape(h, w, 2))
+    assert_same(hip, ref, fields=("mask", "uv", "rgba"))
+    # fan mode vs f64 literal shader with the same fan: UV tolerance, mask equal off the lerp edge
+    r64 = O.render_f64(frame, buf.scene(), w, h, fan=fan)
+    agree = np.mean(hip["mask"] == r64["mask"])
+    assert agree > 0.999
+
+
+def test_1080p_rows_bitexact(geo, torch_mod):
+    from schwarzschild_raytracer_wgpu_amd.scenes import make_sky
+
+    w, h = 1920, 1080
+    sky = make_sky("equirect", (4096, 2048))
+    frame, scene = default_frame(w, h), default_scene(512)
+    ctx = make_ctx(geo, sky)
+    hip = render(geo, torch_mod, ctx, frame, scene, w, h)
+    step = 9
+    ref = O.render_f32(frame, scene, sky, w, h, row0=4, nrows=h // step, row_step=step, threads=16)
+    sub = {k: hip[k][4::step][: h // step] for k in ("rgba", "mask", "uv", "steps")}
+    assert_same(sub, ref)
+
+
+def test_4k_2048_properties(geo, torch_mod):
+    """Full config-3 frame: size-independent properties + sampled bit-exact rows."""
+    from schwarzschild_raytracer_wgpu_amd.scenes import make_sky
+
+    w, h = 3840, 2160
+    sky = make_sky("equirect", (4096, 2048))
+    frame, scene = default_frame(w, h), default_scene(2048)
+    ctx = make_ctx(geo, sky)
+    a = render(geo, torch_mod, ctx, frame, scene, w, h)
+    b = render(geo, torch_mod, ctx, frame, scene, w, h)
+    for f in ("rgba", "mask", "uv", "steps"):
+        assert np.array_equal(a[f], b[f])  # deterministic
+    assert a["total"] == int(a["steps"].astype(np.uint64).sum())
+    assert a["steps"].max() < 2048  # budget never binds at step PI/100
+    frac = a["mask"].mean()
+    assert 0.15 < frac < 0.25  # analytic shadow: ~20.4 % of this frame
+    assert np.all(a["rgba"][a["mask"] == 1] == np.array([0, 0, 0, 255], np.uint8))
+    ref = O.render_f32(frame, scene, sky, w, h, row0=13, nrows=h // 97, row_step=97, threads=16)
+    sub = {k: a[k][13::97][: h // 97] for k in ("rgba", "mask", "uv", "steps")}
+    assert_same(sub, ref)
+
+
+def test_invalid_arguments(geo, torch_mod):
+    from schwarzschild_raytracer_wgpu_amd import _lib
+
+    ctx = geo.Context(0)
+    frame, scene = default_frame(8, 8), default_scene(16)
+    dev = torch_mod.device("cuda:0")
+    out = torch_mod.empty(8 * 8 * 4, dtype=torch_mod.uint8, device=dev)
+    # render before set_sky
+    st = _lib.lib.geo_render_rows(ctx._h, ctypes.byref(frame), ctypes.byref(scene), 8, 8, 0, 8, out.data_ptr(),
+                                  None, None, None, None, None)
+    assert st == _lib.GEO_ESTATE
+    ctx.set_sky(np.zeros((1, 1, 4), np.uint8))
+    # rows out of range
+    st = _lib.lib.geo_render_rows(ctx._h, ctypes.byref(frame), ctypes.byref(scene), 8, 8, 4, 5, out.data_ptr(),
+                                  None, None, None, None, None)
+    assert st == _lib.GEO_EINVAL
+    # fan mode without a fan
+    sc2 = default_scene(16, mode=geo.GEO_MODE_FAN)
+    st = _lib.lib.geo_render_rows(ctx._h, ctypes.byref(frame), ctypes.byref(sc2), 8, 8, 0, 8, out.data_ptr(),
+                                  None, None, None, None, None)
+    assert st == _lib.GEO_ESTATE
+    with pytest.raises(geo.GeoError):
+        ctx.set_fan(np.zeros(1, np.float32))
+    with pytest.raises(geo.GeoError):
+        geo.Context(99)

@@ -1,0 +1,31 @@
+#!/bin/bash
+# One GPU session: parity tests, smoke, bench, rocprofv3 kernel-trace profile.
+# Each GPU step has its own time limit; a crash/timeout (exit >= 124 or a
+# signal) ends the script, a plain test failure (pytest exit 1) does not.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+ROOT=$(pwd)
+OUT=$ROOT/gpurun_out
+mkdir -p "$OUT"
+TAG=${1:-r01}
+STEPS=${STEPS:-20}
+
+fatal() { local rc=$1; [ "$rc" -ge 124 ] || [ "$rc" -ge 128 ]; }
+
+timeout -k 10 420 python -m pytest tests -m gpu -q -rf > "$OUT/pytest_gpu_$TAG.log" 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -5 "$OUT/pytest_gpu_$TAG.log"
+if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+
+timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke_$TAG.log" 2>&1
+rc=$?; echo "smoke rc=$rc"; tail -2 "$OUT/smoke_$TAG.log"
+if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+
+timeout -k 10 300 python bench.py --steps "$STEPS" > "$OUT/bench_$TAG.json" 2> "$OUT/bench_$TAG.err"
+rc=$?; echo "bench rc=$rc"; cat "$OUT/bench_$TAG.json"; tail -3 "$OUT/bench_$TAG.err"
+if [ $rc -ne 0 ]; then exit $rc; fi
+
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$TAG" -o run \
+    -- python3 "$ROOT/bench.py" --steps "$STEPS" --no-cpu-baseline > "$OUT/prof_$TAG.log" 2>&1
+rc=$?; echo "rocprof rc=$rc"; tail -3 "$OUT/prof_$TAG.log"
+exit $rc

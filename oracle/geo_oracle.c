@@ -292,7 +292,7 @@ float geo_oracle_atan2f(float y, float x) {
 typedef struct {
     float rs, sphere_r, r, step;
     uint32_t max_steps;
-    float hh, h6, r3_2, sphere_u, schwarz_u, u0, h_over_r2, bound, e_out, e_in, barrier;
+    float hh, h6, hh2, hhh, h2_6, r3_2, sphere_u, schwarz_u, u0, h_over_r2, bound, e_out, e_in, barrier;
     int r_inside_h, outside, sphere_outside, inside_sphere, diff_sides, rs_nonzero;
 } fconsts;
 
@@ -305,6 +305,9 @@ static fconsts make_fconsts(const geo_scene* s) {
     k.max_steps = s->max_steps;
     k.hh = k.step * 0.5f;
     k.h6 = k.step / 6.0f;
+    k.hh2 = (k.step * k.step) * 0.25f;
+    k.hhh = (k.step * k.step) * 0.5f;
+    k.h2_6 = (k.step * k.step) / 6.0f;
     k.r3_2 = 1.5f * k.rs;
     k.sphere_u = 1.0f / k.sphere_r;
     k.schwarz_u = 1.0f / k.rs;
@@ -325,27 +328,27 @@ static fconsts make_fconsts(const geo_scene* s) {
     return k;
 }
 
-/* the RK4 step of sphere_ray_tracer.rs:137-146 with f(x) = x*(c*x - 1) */
-static inline void rk4f(float u, float ub, float h, float hh, float h6, float c, float* nu, float* nub) {
+/* the RK4 step of sphere_ray_tracer.rs:137-146 with f(x) = x*(c*x - 1), stage
+ * values in the algebraically identical forms of DESIGN.md §3:
+ *   a_u = u + h/2 ub, b_u = a_u + h^2/4 f(u), u_h = u + h ub, c_u = u_h + h^2/2 f(a_u),
+ *   next_u = u_h + h^2/6 (f(u)+f(a_u)+f(b_u)), next_ub = ub + h/6 (f(u)+2f(a_u)+2f(b_u)+f(c_u)). */
+static inline void rk4f(float u, float ub, float h, float hh, float hh2, float hhh, float h6, float h2_6,
+                        float c, float* nu, float* nub) {
     float fu = fmaf(c, u, -1.0f) * u;
     float au = fmaf(hh, ub, u);
-    float aub = fmaf(hh, fu, ub);
+    float uh = fmaf(h, ub, u);
     float fa = fmaf(c, au, -1.0f) * au;
-    float bu = fmaf(hh, aub, u);
-    float bub = fmaf(hh, fa, ub);
+    float bu = fmaf(hh2, fu, au);
     float fb = fmaf(c, bu, -1.0f) * bu;
-    float cu = fmaf(h, bub, u);
-    float cub = fmaf(h, fb, ub);
+    float cu = fmaf(hhh, fa, uh);
     float fc = fmaf(c, cu, -1.0f) * cu;
-    float s1 = fmaf(2.0f, aub + bub, ub) + cub;
-    float s2 = fmaf(2.0f, fa + fb, fu) + fc;
-    *nu = fmaf(h6, s1, u);
-    *nub = fmaf(h6, s2, ub);
+    float fab = fa + fb;
+    *nu = fmaf(h2_6, fu + fab, uh);
+    *nub = fmaf(h6, fmaf(2.0f, fab, fu) + fc, ub);
 }
 
-static float geodesic_f32(const fconsts* k, float st, uint32_t* steps) {
+static float geodesic_f32(const fconsts* k, float st, float ct, uint32_t* steps) {
     *steps = 0;
-    float ct = sqrtf(maxz(0.0f, (1.0f - st) * (1.0f + st)));
     float rotation = k->r * ct;
     int falling;
     float energy;
@@ -367,8 +370,7 @@ static float geodesic_f32(const fconsts* k, float st, uint32_t* steps) {
         }
         return (k->sphere_outside && falling) ? 0.0f : 15.0f;
     }
-    float b = rotation / energy;
-    float inv_b2 = 1.0f / (b * b);
+    float inv_b2 = (energy * energy) / (rotation * rotation); /* 1/b^2, b = L/E */
     int barrier = k->rs > 0.0f && inv_b2 < k->barrier;
     if ((k->inside_sphere && !k->sphere_outside) || (!k->outside && k->sphere_outside && energy < 0.0f) ||
         (barrier && k->diff_sides) || (k->r < k->r3_2 && k->inside_sphere && falling) ||
@@ -381,7 +383,7 @@ static float geodesic_f32(const fconsts* k, float st, uint32_t* steps) {
     uint32_t it = 0;
     while (!(k->rs_nonzero && u > k->schwarz_u && ub > 0.0f) && it < k->max_steps && u > 0.0f) {
         float nu, nub;
-        rk4f(u, ub, k->step, k->hh, k->h6, c, &nu, &nub);
+        rk4f(u, ub, k->step, k->hh, k->hh2, k->hhh, k->h6, k->h2_6, c, &nu, &nub);
         ++it;
         if ((nu > su) != (u > su)) {
             float ns, wu, wub;
@@ -392,7 +394,9 @@ static float geodesic_f32(const fconsts* k, float st, uint32_t* steps) {
             }
             for (int n = 0; n < 3; ++n) {
                 ns = ns - (wu - su) / wub;
-                rk4f(u, ub, ns, ns * 0.5f, ns / 6.0f, c, &wu, &wub);
+                float n2 = ns * ns;
+                float n6 = ns * (1.0f / 6.0f);
+                rk4f(u, ub, ns, ns * 0.5f, n2 * 0.25f, n2 * 0.5f, n6, ns * n6, c, &wu, &wub);
             }
             *steps = it;
             return (float)(it - 1u) * k->step + ns;
@@ -421,27 +425,20 @@ static void pixel_f32(const geo_frame* f, const fconsts* k, int mode, const floa
                       const uint32_t* sky, uint32_t sw, uint32_t sh, uint32_t width, uint32_t height,
                       uint32_t px, uint32_t py, uint32_t* rgba, uint8_t* bh_out, float* uv, uint32_t* steps) {
     const float* m0 = f->display_to_movement;
-    float nx = ((float)(2u * px + 1u) - (float)width) / (float)width;
-    float ny = ((float)height - (float)(2u * py + 1u)) / (float)height;
+    float nx = ((float)(2u * px + 1u) - (float)width) * (1.0f / (float)width);
+    float ny = ((float)height - (float)(2u * py + 1u)) * (1.0f / (float)height);
     float d[3];
     m3vf(m0, -ny * m0[12], -nx * m0[13], m0[14], d);
-    float inv = 1.0f / sqrtf(fmaf(d[2], d[2], fmaf(d[1], d[1], d[0] * d[0])));
-    d[0] *= inv;
-    d[1] *= inv;
-    d[2] *= inv;
+    /* aberration (shader.wgsl:69-70) as a boost along z on the unnormalised ray */
     float kk = f->psi_factor_and_position[0];
-    float s = clampf(d[2], -1.0f, 1.0f);
-    float q = clampf((s - kk) / fmaf(-s, kk, 1.0f), -1.0f, 1.0f);
-    float cl = sqrtf(maxz(0.0f, (1.0f - q) * (1.0f + q)));
-    float rho = sqrtf(fmaf(d[1], d[1], d[0] * d[0]));
-    float cp = 1.0f, sp = 0.0f;
-    if (rho > 0.0f) {
-        cp = d[0] / rho;
-        sp = d[1] / rho;
-    }
+    float kt = sqrtf(fmaf(-kk, kk, 1.0f));
+    float len = sqrtf(fmaf(d[2], d[2], fmaf(d[1], d[1], d[0] * d[0])));
+    float id = 1.0f / fmaf(-kk, d[2], len);
+    float g = kt * id;
     float c2[3];
-    m3vf(f->movement_to_central, cp * cl, sp * cl, q, c2);
+    m3vf(f->movement_to_central, d[0] * g, d[1] * g, fmaf(-kk, len, d[2]) * id, c2);
     float st = clampf(c2[2], -1.0f, 1.0f);
+    float rho2 = sqrtf(fmaf(c2[1], c2[1], c2[0] * c2[0])); /* cos theta */
     float lam;
     *steps = 0;
     if (mode == (int)GEO_MODE_FAN) {
@@ -454,20 +451,20 @@ static void pixel_f32(const geo_frame* f, const fconsts* k, int mode, const floa
         uint32_t i1 = (i + 1u < n_fan) ? i + 1u : n_fan - 1u;
         lam = fan[i] * (1.0f - w) + fan[i1] * w;
     } else {
-        lam = F_PI2 - geodesic_f32(k, st, steps);
+        lam = F_PI2 - geodesic_f32(k, st, rho2, steps);
     }
     int bh = lam < -7.0f;
     /* sky_uv */
-    float rho2 = sqrtf(fmaf(c2[1], c2[1], c2[0] * c2[0]));
-    float cp2 = 1.0f, sp2 = 0.0f;
-    if (rho2 > 0.0f) {
-        cp2 = c2[0] / rho2;
-        sp2 = c2[1] / rho2;
-    }
     float sl, cll;
     geo_oracle_sincosf(lam, &sl, &cll);
+    float ex = cll, ey = 0.0f;
+    if (rho2 > 0.0f) {
+        float w = cll / rho2;
+        ex = c2[0] * w;
+        ey = c2[1] * w;
+    }
     float c3[3];
-    m3vf(f->central_to_uv, cp2 * cll, sp2 * cll, sl, c3);
+    m3vf(f->central_to_uv, ex, ey, sl, c3);
     float U = geo_oracle_atan2f(c3[1], c3[0]) * 0.159154943091895335769f;
     if (U < 0.0f) U += 1.0f;
     float V = 0.5f - geo_oracle_asinf(c3[2]) * 0.318309886183790671538f;

@@ -105,6 +105,15 @@ class GeoError(RuntimeError):
 
 
 def _load() -> ctypes.CDLL:
+    # One HIP runtime per process: torch's libtorch_hip NEEDs "libamdhip64.so"
+    # while libgeo NEEDs the soname "libamdhip64.so.7".  Loading torch first
+    # makes libgeo bind to torch's already-loaded runtime (soname match), so
+    # torch tensors' device pointers are valid in libgeo.  Without torch in the
+    # process (a plain C/Rust host) libgeo uses /opt/rocm's runtime.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     if not os.path.exists(LIB_PATH):
         raise ImportError(
             f"libgeo.so not found at {LIB_PATH}; build it with `python -c 'import __graft_entry__ as g; g.build()'`"

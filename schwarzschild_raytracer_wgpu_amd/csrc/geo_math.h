@@ -21,6 +21,13 @@
 #define GEO_HD static inline
 #endif
 
+// Makes the compiler forget what it knows about a VGPR value (no code).
+#if defined(__HIP_DEVICE_COMPILE__)
+#define GEO_OPAQUE(x) asm volatile("" : "+v"(x))
+#else
+#define GEO_OPAQUE(x) ((void)0)
+#endif
+
 namespace geo {
 
 constexpr float kPi = 3.14159265358979323846f;

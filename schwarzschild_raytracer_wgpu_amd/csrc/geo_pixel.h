@@ -23,6 +23,7 @@ namespace geo {
 constexpr float kNoValue = 15.0f;          // SphereRayTracer::NO_VALUE, sphere_ray_tracer.rs:22
 constexpr float kBlackHoleLambda = -7.0f;  // hit_black_hole threshold, shader.wgsl:88
 constexpr int kNewtonIters = 3;            // final_newton_refinements, sphere_ray_tracer.rs:129
+constexpr float kSixth = 1.0f / 6.0f;
 
 // Frame-constant scalars derived from the scene, evaluated identically on
 // every lane (and by the oracle).  Names follow sphere_ray_tracer.rs:60-132.
@@ -30,6 +31,7 @@ struct PixelConsts {
     float rs, sphere_r, r, step;
     uint32_t max_steps;
     float hh, h6;          // step/2 (step_half :130), step/6
+    float hh2, hhh, h2_6;  // step^2/4, step^2/2, step^2/6
     float r3_2;            // 3*rs/2 (:109)
     float sphere_u;        // 1/sphere_r (:131)
     float schwarz_u;       // 1/rs (:132)
@@ -45,6 +47,10 @@ struct PixelConsts {
     bool inside_sphere;    // r < sphere_r (:64)
     bool diff_sides;       // different_sides_3r_2 (:110)
     bool rs_nonzero;
+    // frame-uniform parts of the radial cases (:67-104) and pre-filters (:113-117)
+    float radial_falling, radial_outgoing;  // result for rotation < 1e-10, by `falling`
+    bool radial_by_energy;                  // radial result decided by energy > 0 instead
+    bool pf_always, pf_falling, pf_outgoing, pf_eneg, pf_barrier;
 };
 
 GEO_HD PixelConsts make_consts(float rs, float sphere_r, float r, float step, uint32_t max_steps) {
@@ -56,6 +62,9 @@ GEO_HD PixelConsts make_consts(float rs, float sphere_r, float r, float step, ui
     k.max_steps = max_steps;
     k.hh = step * 0.5f;
     k.h6 = step / 6.0f;
+    k.hh2 = (step * step) * 0.25f;
+    k.hhh = (step * step) * 0.5f;
+    k.h2_6 = (step * step) / 6.0f;
     k.r3_2 = 1.5f * rs;
     k.sphere_u = 1.0f / sphere_r;
     k.schwarz_u = 1.0f / rs;
@@ -73,35 +82,87 @@ GEO_HD PixelConsts make_consts(float rs, float sphere_r, float r, float step, ui
     const float dr = r - k.r3_2;
     k.diff_sides = ((r < k.r3_2) != (sphere_r < k.r3_2)) && (__builtin_fabsf(dr) > 1e-10f);
     k.rs_nonzero = rs != 0.0f;
+    // radial rays (:67-104)
+    k.radial_by_energy = false;
+    if (k.inside_sphere) {
+        if (k.outside) {
+            k.radial_falling = k.rs_nonzero ? kNoValue : kPi;
+            k.radial_outgoing = 0.0f;
+        } else if (k.sphere_outside) {
+            k.radial_by_energy = true;  // energy > 0 ? 0 : NO_VALUE
+            k.radial_falling = k.radial_outgoing = 0.0f;
+        } else {
+            k.radial_falling = k.radial_outgoing = 0.0f;
+        }
+    } else {
+        k.radial_falling = k.sphere_outside ? 0.0f : kNoValue;
+        k.radial_outgoing = kNoValue;
+    }
+    // pre-filters (:113-117): NO_VALUE when any term holds
+    k.pf_always = k.inside_sphere && !k.sphere_outside;
+    k.pf_eneg = !k.outside && k.sphere_outside;     // & energy < 0
+    k.pf_barrier = k.rs > 0.0f && k.diff_sides;     // & 1/b^2 < 4/(27 rs^2)
+    k.pf_falling = r < k.r3_2 && k.inside_sphere;   // & falling
+    k.pf_outgoing = r > k.r3_2 && !k.inside_sphere; // & !falling
     return k;
 }
 
 // One classic RK4 step of u'' = -u + c u^2 (sphere_ray_tracer.rs:137-146),
-// f(x) = x (c x - 1).
-GEO_HD void rk4_step(float u, float ub, float h, float hh, float h6, float c, float* nu,
-                     float* nub) {
+// f(x) = x (c x - 1), in 18 VALU ops.  The reference's stage values are
+// evaluated in algebraically identical forms that need neither a_ub, b_ub
+// nor c_ub:
+//   a_u = u + h/2 ub            b_u = a_u + h^2/4 f(u)      [= u + h/2 a_ub]
+//   u_h = u + h ub              c_u = u_h + h^2/2 f(a_u)    [= u + h b_ub]
+//   next_u  = u_h + h^2/6 (f(u) + f(a_u) + f(b_u))          [= u + h/6 (ub + 2a_ub + 2b_ub + c_ub)]
+//   next_ub = ub + h/6 (f(u) + 2 f(a_u) + 2 f(b_u) + f(c_u))
+// hh = h/2, hh2 = h^2/4, hhh = h^2/2, h6 = h/6, h2_6 = h^2/6.
+GEO_HD void rk4_step(float u, float ub, float h, float hh, float hh2, float hhh, float h6, float h2_6,
+                     float c, float* nu, float* nub) {
     const float fu = fmaf_(c, u, -1.0f) * u;
     const float au = fmaf_(hh, ub, u);
-    const float aub = fmaf_(hh, fu, ub);
+    const float uh = fmaf_(h, ub, u);
     const float fa = fmaf_(c, au, -1.0f) * au;
-    const float bu = fmaf_(hh, aub, u);
-    const float bub = fmaf_(hh, fa, ub);
+    const float bu = fmaf_(hh2, fu, au);
     const float fb = fmaf_(c, bu, -1.0f) * bu;
-    const float cu = fmaf_(h, bub, u);
-    const float cub = fmaf_(h, fb, ub);
+    const float cu = fmaf_(hhh, fa, uh);
     const float fc = fmaf_(c, cu, -1.0f) * cu;
-    const float s1 = fmaf_(2.0f, aub + bub, ub) + cub;
-    const float s2 = fmaf_(2.0f, fa + fb, fu) + fc;
-    *nu = fmaf_(h6, s1, u);
-    *nub = fmaf_(h6, s2, ub);
+    const float fab = fa + fb;
+    *nu = fmaf_(h2_6, fu + fab, uh);
+    *nub = fmaf_(h6, fmaf_(2.0f, fab, fu) + fc, ub);
 }
 
+// Newton on the step length from the steeper end (:150-182), from the
+// pre-step state (u, ub) and the post-step state (nu, nub) of step `it`.
+GEO_HD float newton_angle(const PixelConsts& k, float u, float ub, float nu, float nub, uint32_t it) {
+    const float su = k.sphere_u;
+    const float c = k.r3_2;
+    float ns, wu, wub;
+    if (__builtin_fabsf(ub) > __builtin_fabsf(nub)) {
+        ns = 0.0f;
+        wu = u;
+        wub = ub;
+    } else {
+        ns = k.step;
+        wu = nu;
+        wub = nub;
+    }
+    for (int n = 0; n < kNewtonIters; ++n) {
+        ns = ns - (wu - su) / wub;
+        const float n2 = ns * ns;
+        const float n6 = ns * kSixth;
+        rk4_step(u, ub, ns, ns * 0.5f, n2 * 0.25f, n2 * 0.5f, n6, ns * n6, c, &wu, &wub);
+    }
+    return (float)(it - 1u) * k.step + ns;
+}
+
+
 // Traveled angle of the ray seen at angle theta from the black hole
-// (st = sin theta), or kNoValue.  *steps = executed main-loop RK4 steps.
-GEO_HD float geodesic_angle(const PixelConsts& k, float st, uint32_t* steps) {
+// or kNoValue.  *steps = executed main-loop RK4 steps.
+// (st, ct) = (sin theta, cos theta >= 0) of the central-frame direction.
+template <int LOOP>
+GEO_HD float geodesic_angle_v(const PixelConsts& k, float st, float ct, uint32_t* steps) {
     *steps = 0;
-    // solve_ray_fan per node (sphere_ray_tracer.rs:38-49), theta = asin(st)
-    const float ct = __builtin_sqrtf(fmaxf_(0.0f, (1.0f - st) * (1.0f + st)));
+    // solve_ray_fan per node (sphere_ray_tracer.rs:38-49)
     const float rotation = k.r * ct;
     bool falling;
     float energy;
@@ -112,25 +173,16 @@ GEO_HD float geodesic_angle(const PixelConsts& k, float st, uint32_t* steps) {
         falling = st > 0.0f;
         energy = k.e_out;
     }
-    // radial rays (:67-104)
+    // radial rays (:67-104), frame-uniform table
     if (rotation < 1e-10f) {
-        if (k.inside_sphere) {
-            if (k.outside) {
-                if (falling) return k.rs_nonzero ? kNoValue : kPi;
-                return 0.0f;
-            }
-            if (k.sphere_outside) return energy > 0.0f ? 0.0f : kNoValue;
-            return 0.0f;
-        }
-        return (k.sphere_outside && falling) ? 0.0f : kNoValue;
+        if (k.radial_by_energy) return energy > 0.0f ? 0.0f : kNoValue;
+        return falling ? k.radial_falling : k.radial_outgoing;
     }
-    const float b = rotation / energy;
-    const float inv_b2 = 1.0f / (b * b);
-    // pre-filters (:106-119)
-    const bool barrier = k.rs > 0.0f && inv_b2 < k.barrier_thresh;
-    if ((k.inside_sphere && !k.sphere_outside) || (!k.outside && k.sphere_outside && energy < 0.0f) ||
-        (barrier && k.diff_sides) || (k.r < k.r3_2 && k.inside_sphere && falling) ||
-        (k.r > k.r3_2 && !k.inside_sphere && !falling)) {
+    // 1/b^2 with b = rotation/energy (:61): one division
+    const float inv_b2 = (energy * energy) / (rotation * rotation);
+    // pre-filters (:106-119), frame-uniform terms precomputed
+    if (k.pf_always | (k.pf_eneg & (energy < 0.0f)) | (k.pf_barrier & (inv_b2 < k.barrier_thresh)) |
+        (k.pf_falling & falling) | (k.pf_outgoing & !falling)) {
         return kNoValue;
     }
     // RK4 init (:122-132); the radicand is clamped at 0 (the reference yields
@@ -140,40 +192,171 @@ GEO_HD float geodesic_angle(const PixelConsts& k, float st, uint32_t* steps) {
     if (!falling) ub = -ub;
     const float su = k.sphere_u;
     const float c = k.r3_2;
-    uint32_t it = 0;
-    // main loop (:134-191)
-    while (!(k.rs_nonzero && u > k.schwarz_u && ub > 0.0f) && it < k.max_steps && u > 0.0f) {
+    // Loop test of :134-135 on the initial state.  schwarz_u = 1/rs is +inf
+    // for rs = 0, so `u > schwarz_u` already encodes `rs != 0 &&`.
+    if ((u > k.schwarz_u && ub > 0.0f) || k.max_steps == 0u || !(u > 0.0f)) return kNoValue;
+    if constexpr (LOOP == 0) {
+        // Single step per exit test (one lane-exit flag per step).
+        uint32_t it = 0;
+        bool above = u > su;
+        bool cross;
         float nu, nub;
-        rk4_step(u, ub, k.step, k.hh, k.h6, c, &nu, &nub);
-        ++it;
-        if ((nu > su) != (u > su)) {
-            // Newton on the step length from the steeper end (:150-182)
-            float ns, wu, wub;
-            if (__builtin_fabsf(ub) > __builtin_fabsf(nub)) {
-                ns = 0.0f;
-                wu = u;
-                wub = ub;
+        for (;;) {
+            rk4_step(u, ub, k.step, k.hh, k.hh2, k.hhh, k.h6, k.h2_6, c, &nu, &nub);
+            ++it;
+            const bool nabove = nu > su;
+            cross = nabove != above;
+            const bool stop = cross | !(nu >= k.bound) | ((nu > k.schwarz_u) & (nub > 0.0f)) |
+                              (it >= k.max_steps);
+            if (stop) break;
+            u = nu;
+            ub = nub;
+            above = nabove;
+        }
+        *steps = it;
+        if (!cross) return kNoValue;
+        return newton_angle(k, u, ub, nu, nub, it);
+    }
+    if constexpr (LOOP == 1) {
+        // Two steps per exit test, budget as a uniform pair bound, no ping-pong.
+        const float hu = k.schwarz_u, bd = k.bound;
+        const uint32_t ms = k.max_steps;
+        const uint32_t npairs = ms >> 1;
+        uint32_t it = npairs << 1;
+        bool above = u > su;
+        float n1u = u, n1b = ub, n2u = u, n2b = ub;
+        for (uint32_t q = 0; q < npairs; ++q) {
+            rk4_step(u, ub, k.step, k.hh, k.hh2, k.hhh, k.h6, k.h2_6, c, &n1u, &n1b);
+            const bool a1 = n1u > su;
+            const bool s1 = (a1 != above) | !(n1u >= bd) | ((n1u > hu) & (n1b > 0.0f));
+            rk4_step(n1u, n1b, k.step, k.hh, k.hh2, k.hhh, k.h6, k.h2_6, c, &n2u, &n2b);
+            const bool a2 = n2u > su;
+            const bool s2 = (a2 != a1) | !(n2u >= bd) | ((n2u > hu) & (n2b > 0.0f));
+            if (s1 | s2) {
+                it = q << 1;
+                break;
+            }
+            u = n2u;
+            ub = n2b;
+            above = a2;
+        }
+        GEO_OPAQUE(u);
+        GEO_OPAQUE(ub);
+        GEO_OPAQUE(n1u);
+        GEO_OPAQUE(n1b);
+        GEO_OPAQUE(n2u);
+        GEO_OPAQUE(n2b);
+        GEO_OPAQUE(it);
+        float ou, oub, nu, nub;
+        if (it + 2u <= ms) {
+            const bool s1 = ((n1u > su) != (u > su)) | !(n1u >= bd) | ((n1u > hu) & (n1b > 0.0f));
+            if (s1) {
+                ou = u; oub = ub; nu = n1u; nub = n1b; it += 1u;
             } else {
-                ns = k.step;
-                wu = nu;
-                wub = nub;
+                ou = n1u; oub = n1b; nu = n2u; nub = n2b; it += 2u;
             }
-            for (int n = 0; n < kNewtonIters; ++n) {
-                ns = ns - (wu - su) / wub;
-                rk4_step(u, ub, ns, ns * 0.5f, ns / 6.0f, c, &wu, &wub);
+        } else {
+            ou = u; oub = ub; nu = u; nub = ub;
+            if (it < ms) {
+                rk4_step(u, ub, k.step, k.hh, k.hh2, k.hhh, k.h6, k.h2_6, c, &nu, &nub);
+                it += 1u;
             }
-            *steps = it;
-            return (float)(it - 1u) * k.step + ns;
         }
-        if (nu < k.bound) {
-            *steps = it;
-            return kNoValue;
+        *steps = it;
+        if ((nu > su) == (ou > su)) return kNoValue;
+        return newton_angle(k, ou, oub, nu, nub, it);
+    }
+    // Main loop (:134-191), restructured for the wave64 VALU:
+    //  * TWO RK4 steps per exit test; the per-step stop flag is crossing
+    //    (:150) | escape (:184) | the horizon part of the next loop test
+    //    (:134).  `!(nu >= bound)` is (nu < bound) or NaN and, with bound > 0,
+    //    also covers `u > 0`.  A lane whose first step stops discards the second.
+    //  * the budget (:135) is a wave-uniform bound on a scalar pair counter;
+    //  * the state ping-pongs between register sets A = (u, ub) and
+    //    B = (bu, bb) (A -> t -> B, then B -> t -> A): no copies.
+    // Results equal the literal loop's (the oracle keeps that form; tests
+    // require bit equality).
+    if constexpr (LOOP == 2) {
+    const float hu = k.schwarz_u, bd = k.bound;
+    const uint32_t ms = k.max_steps;
+    const uint32_t npairs = ms >> 1;  // wave-uniform pair budget
+    uint32_t it = npairs << 1;        // per lane: steps before the stopping pair (budget exit: all pairs)
+    bool above = u > su;
+    float bu = u, bb = ub, tu = u, tb = ub;
+    for (uint32_t q = 0;;) {
+        if (q >= npairs) break;
+        {
+            rk4_step(u, ub, k.step, k.hh, k.hh2, k.hhh, k.h6, k.h2_6, c, &tu, &tb);
+            const bool a1 = tu > su;
+            const bool s1 = (a1 != above) | !(tu >= bd) | ((tu > hu) & (tb > 0.0f));
+            rk4_step(tu, tb, k.step, k.hh, k.hh2, k.hhh, k.h6, k.h2_6, c, &bu, &bb);
+            const bool a2 = bu > su;
+            const bool s2 = (a2 != a1) | !(bu >= bd) | ((bu > hu) & (bb > 0.0f));
+            if (s1 | s2) {
+                it = q << 1;
+                break;
+            }
+            above = a2;
         }
-        u = nu;
-        ub = nub;
+        if (++q >= npairs) break;
+        {
+            rk4_step(bu, bb, k.step, k.hh, k.hh2, k.hhh, k.h6, k.h2_6, c, &tu, &tb);
+            const bool a1 = tu > su;
+            const bool s1 = (a1 != above) | !(tu >= bd) | ((tu > hu) & (tb > 0.0f));
+            rk4_step(tu, tb, k.step, k.hh, k.hh2, k.hhh, k.h6, k.h2_6, c, &u, &ub);
+            const bool a2 = u > su;
+            const bool s2 = (a2 != a1) | !(u >= bd) | ((u > hu) & (ub > 0.0f));
+            if (s1 | s2) {
+                it = q << 1;
+                break;
+            }
+            above = a2;
+        }
+        ++q;
+    }
+    // Opaque copies: the flags below are recomputed from the state rather
+    // than carried out of the loop as lane masks.
+    GEO_OPAQUE(u);
+    GEO_OPAQUE(ub);
+    GEO_OPAQUE(bu);
+    GEO_OPAQUE(bb);
+    GEO_OPAQUE(tu);
+    GEO_OPAQUE(tb);
+    GEO_OPAQUE(it);
+    // the last pair started from A after an even number of pairs, else from B
+    const bool odd = ((it >> 1) & 1u) != 0u;
+    const float s0u = odd ? bu : u, s0b = odd ? bb : ub;  // pair start / current state
+    const float e0u = odd ? u : bu, e0b = odd ? ub : bb;  // pair end
+    float ou, oub, nu, nub;
+    if (it + 2u <= ms) {
+        // stopped inside the pair at steps it+1 or it+2
+        const bool s1 = ((tu > su) != (s0u > su)) | !(tu >= bd) | ((tu > hu) & (tb > 0.0f));
+        if (s1) {
+            ou = s0u; oub = s0b; nu = tu; nub = tb; it += 1u;
+        } else {
+            ou = tu; oub = tb; nu = e0u; nub = e0b; it += 2u;
+        }
+    } else {
+        // budget exit: at most one step left
+        ou = s0u; oub = s0b; nu = s0u; nub = s0b;
+        if (it < ms) {
+            rk4_step(s0u, s0b, k.step, k.hh, k.hh2, k.hhh, k.h6, k.h2_6, c, &nu, &nub);
+            it += 1u;
+        }
     }
     *steps = it;
-    return kNoValue;
+    if ((nu > su) == (ou > su)) return kNoValue;  // stopped without a crossing
+    u = ou;
+    ub = oub;
+    return newton_angle(k, u, ub, nu, nub, it);
+    }
+}
+
+#ifndef GEO_LOOP_VARIANT
+#define GEO_LOOP_VARIANT 1  // fastest on gfx950 (tools/ubench/loop_ab.hip)
+#endif
+GEO_HD float geodesic_angle(const PixelConsts& k, float st, float ct, uint32_t* steps) {
+    return geodesic_angle_v<GEO_LOOP_VARIANT>(k, st, ct, steps);
 }
 
 // 3x3 part of a column-major mat4 times v (w = 0).
@@ -183,37 +366,32 @@ GEO_HD void mat3_mul(const float* m, float x, float y, float z, float* ox, float
     *oz = fmaf_(m[10], z, fmaf_(m[6], y, m[2] * x));
 }
 
-// shader.wgsl:60-75 — pixel (px, py) of a width x height frame to the unit
-// direction in the black-hole-central frame.  The aberration is applied to
-// sin(lambda) directly; cos/sin of phi come from the direction itself, so
-// steps 3-5 need no transcendental (the f64 oracle keeps the literal form).
-GEO_HD void pixel_central_dir(const float* m0, const float* m1, float psi_k, uint32_t width,
-                              uint32_t height, uint32_t px, uint32_t py, float* c2x, float* c2y,
-                              float* c2z) {
-    const float nx = ((float)(2u * px + 1u) - (float)width) / (float)width;
-    const float ny = ((float)height - (float)(2u * py + 1u)) / (float)height;
+// shader.wgsl:60-75 — pixel (px, py) of a width x height frame to the
+// direction in the black-hole-central frame (unit up to rounding).
+// The aberration (:69-70), sin(l') = (s - k)/(1 - s k) with phi kept, is
+// applied as the boost along z it is: for the unnormalised ray d, |d| = L,
+//   e_z = (d_z - k L)/(L - k d_z),   e_xy = d_xy sqrt(1 - k^2)/(L - k d_z),
+// (|e| = 1), so steps 2-5 need one sqrt, one division and no
+// transcendental.  kt = sqrt(1 - k^2) is a frame constant (aberration_kt).
+// inv_w = 1/width, inv_h = 1/height (f32, rounded once).
+GEO_HD float aberration_kt(float psi_k) { return __builtin_sqrtf(fmaf_(-psi_k, psi_k, 1.0f)); }
+
+GEO_HD void pixel_central_dir(const float* m0, const float* m1, float psi_k, float kt, uint32_t width,
+                              uint32_t height, float inv_w, float inv_h, uint32_t px, uint32_t py,
+                              float* c2x, float* c2y, float* c2z) {
+    const float nx = ((float)(2u * px + 1u) - (float)width) * inv_w;
+    const float ny = ((float)height - (float)(2u * py + 1u)) * inv_h;
     // carthesic = (-pos.y, -pos.x, 1, 0) * screen_to_movement.w (:60-63)
     const float cx = -ny * m0[12];
     const float cy = -nx * m0[13];
     const float cz = m0[14];
     float dx, dy, dz;
     mat3_mul(m0, cx, cy, cz, &dx, &dy, &dz);
-    const float inv = 1.0f / __builtin_sqrtf(fmaf_(dz, dz, fmaf_(dy, dy, dx * dx)));
-    dx *= inv;
-    dy *= inv;
-    dz *= inv;
-    // aberration (:69-70): sin(lambda') = (s - k)/(1 - s k)
-    const float s = clampf_(dz, -1.0f, 1.0f);
-    const float q = clampf_((s - psi_k) / fmaf_(-s, psi_k, 1.0f), -1.0f, 1.0f);
-    const float cl = __builtin_sqrtf(fmaxf_(0.0f, (1.0f - q) * (1.0f + q)));
-    const float rho = __builtin_sqrtf(fmaf_(dy, dy, dx * dx));
-    float cp = 1.0f, sp = 0.0f;
-    if (rho > 0.0f) {
-        cp = dx / rho;
-        sp = dy / rho;
-    }
+    const float len = __builtin_sqrtf(fmaf_(dz, dz, fmaf_(dy, dy, dx * dx)));
+    const float id = 1.0f / fmaf_(-psi_k, dz, len);
+    const float g = kt * id;
     // to_cart, then movement_to_central (:72-74)
-    mat3_mul(m1, cp * cl, sp * cl, q, c2x, c2y, c2z);
+    mat3_mul(m1, dx * g, dy * g, fmaf_(-psi_k, len, dz) * id, c2x, c2y, c2z);
 }
 
 // Fan lookup (shader.wgsl:77-84); i+1 clamped to n-1 (weight 0 there).
@@ -228,18 +406,22 @@ GEO_HD float fan_lerp(const float* fan, uint32_t n, float st) {
     return fan[i] * (1.0f - w) + fan[i1] * w;
 }
 
-// shader.wgsl:90-100 — (phi of c2, lambda') to sky-sphere (U, V).
-GEO_HD void sky_uv(const float* m2, float c2x, float c2y, float lam, float* U, float* V) {
-    const float rho = __builtin_sqrtf(fmaf_(c2y, c2y, c2x * c2x));
-    float cp = 1.0f, sp = 0.0f;
-    if (rho > 0.0f) {
-        cp = c2x / rho;
-        sp = c2y / rho;
-    }
+// |(c2x, c2y)| = cos theta of the central-frame direction (to_polar, :75).
+GEO_HD float central_rho(float c2x, float c2y) { return __builtin_sqrtf(fmaf_(c2y, c2y, c2x * c2x)); }
+
+// shader.wgsl:90-100 — (phi of c2, lambda') to sky-sphere (U, V); rho = central_rho.
+GEO_HD void sky_uv(const float* m2, float c2x, float c2y, float rho, float lam, float* U, float* V) {
     float sl, cl;
     sincosf_(lam, &sl, &cl);
+    // to_cart(phi, lam) with (cos phi, sin phi) = (c2x, c2y)/rho
+    float ex = cl, ey = 0.0f;
+    if (rho > 0.0f) {
+        const float w = cl / rho;
+        ex = c2x * w;
+        ey = c2y * w;
+    }
     float x, y, z;
-    mat3_mul(m2, cp * cl, sp * cl, sl, &x, &y, &z);
+    mat3_mul(m2, ex, ey, sl, &x, &y, &z);
     float u = atan2f_(y, x) * kInvTwoPi;
     if (u < 0.0f) u += 1.0f;
     float v = 0.5f - asinf_(z) * kInvPi;

@@ -7,8 +7,8 @@
 //                            (sphere_ray_tracer.rs:35-193)
 //   geo_steps_finalize       folds the sharded step counters into the caller's u64
 //
-// Work decomposition: one 256-thread workgroup per 16x16 pixel tile, each
-// wave64 a 16x4 sub-tile (compact 2-D footprint = coherent step counts);
+// Work decomposition: one 256-thread workgroup per 8x32 pixel tile, each
+// wave64 an 8x8 square (compact 2-D footprint = coherent step counts);
 // the frame uniform rides in the kernarg segment (SGPRs, wave-uniform), the
 // ray fan is staged in LDS; per-lane ray state lives in VGPRs.  The hot loop
 // is pure FP32 VALU — no MFMA, no LDS, no memory traffic.
@@ -23,8 +23,8 @@
 
 namespace {
 
-constexpr int kTileW = 16;
-constexpr int kTileH = 16;
+constexpr int kTileW = 8;   // a wave64 covers an 8x8 pixel square (fewest divergent
+constexpr int kTileH = 32;  // steps per wave; tools/ubench/loop_ab.hip), a block 8x32
 constexpr int kBlock = kTileW * kTileH;  // 256 threads = 4 waves
 constexpr uint32_t kMaxFan = 4096;       // LDS fan capacity (16 KiB)
 constexpr int kStepSlots = 64;           // sharded step counters
@@ -36,6 +36,7 @@ struct RenderArgs {
     uint32_t width, height, row0, nrows;
     uint32_t band_rows, band_stride;  // local row lr -> row0 + (lr/band_rows)*band_stride + lr%band_rows
     uint32_t tiles_x;
+    float inv_w, inv_h, kt;
     const uint32_t* sky;
     uint32_t sky_w, sky_h;
     const float* fan;
@@ -64,18 +65,19 @@ __global__ __launch_bounds__(kBlock) void geo_render_kernel(const RenderArgs a) 
     if (px < a.width && ly < a.nrows && py < a.height) {
         float c2x, c2y, c2z;
         geo::pixel_central_dir(a.frame.display_to_movement, a.frame.movement_to_central,
-                               a.frame.psi_factor_and_position[0], a.width, a.height, px, py,
-                               &c2x, &c2y, &c2z);
+                               a.frame.psi_factor_and_position[0], a.kt, a.width, a.height, a.inv_w,
+                               a.inv_h, px, py, &c2x, &c2y, &c2z);
         const float st = geo::clampf_(c2z, -1.0f, 1.0f);
+        const float ct = geo::central_rho(c2x, c2y);
         float lam;
         if constexpr (MODE == GEO_MODE_FAN) {
             lam = geo::fan_lerp(s_fan, a.n_fan, st);
         } else {
-            lam = geo::kPi2 - geo::geodesic_angle(a.k, st, &steps);
+            lam = geo::kPi2 - geo::geodesic_angle(a.k, st, ct, &steps);
         }
         const bool bh = lam < geo::kBlackHoleLambda;
         float U, V;
-        geo::sky_uv(a.frame.central_to_uv, c2x, c2y, lam, &U, &V);
+        geo::sky_uv(a.frame.central_to_uv, c2x, c2y, ct, lam, &U, &V);
         const uint32_t* sky = a.sky;
         const uint32_t rgba = bh ? geo::kBlackRGBA
                                  : geo::sample_sky([sky](uint32_t i) { return sky[i]; },
@@ -382,7 +384,10 @@ static int render_impl(geo_ctx* c, const geo_frame* frame, const geo_scene* scen
     if (scene->flags != 0 || scene->reserved != 0) return GEO_EINVAL;
     if (!c->sky) return GEO_ESTATE;
     if (scene->mode == GEO_MODE_FAN && (!c->fan || c->n_fan < 2)) return GEO_ESTATE;
-    if (scene->mode == GEO_MODE_DIRECT && !(scene->step > 0.0f)) return GEO_EINVAL;
+    // bound > 0 (escape test folding, geo_pixel.h) needs r_obs > 0 and sphere_r > 0
+    if (scene->mode == GEO_MODE_DIRECT &&
+        (!(scene->step > 0.0f) || !(scene->r_obs > 0.0f) || !(scene->sphere_r > 0.0f) || !(scene->rs >= 0.0f)))
+        return GEO_EINVAL;
     DeviceGuard g(c->device);
     if (!g.ok) return GEO_EHIP;
     RenderArgs a;
@@ -395,6 +400,9 @@ static int render_impl(geo_ctx* c, const geo_frame* frame, const geo_scene* scen
     a.band_rows = band_rows;
     a.band_stride = band_stride;
     a.tiles_x = (width + kTileW - 1) / kTileW;
+    a.inv_w = 1.0f / (float)width;
+    a.inv_h = 1.0f / (float)height;
+    a.kt = geo::aberration_kt(frame->psi_factor_and_position[0]);
     const uint32_t tiles_y = (nrows + kTileH - 1) / kTileH;
     a.sky = c->sky;
     a.sky_w = c->sky_w;

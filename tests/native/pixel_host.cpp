@@ -1,0 +1,44 @@
+// Host build of the PRODUCT's per-pixel header (geo_pixel.h) for CPU tests:
+// checks, without a GPU, that the kernel's exact f32 operation sequence
+// equals the oracle's independent restatement bit for bit.  Test-only.
+#include <cstdint>
+#include <cstring>
+
+#include "../../include/geo/geo.h"
+#include "../../schwarzschild_raytracer_wgpu_amd/csrc/geo_pixel.h"
+
+extern "C" int host_render(const geo_frame* f, const geo_scene* s, const float* fan, uint32_t n_fan,
+                           const uint32_t* sky, uint32_t sw, uint32_t sh, uint32_t width, uint32_t height,
+                           uint32_t row0, uint32_t nrows, uint32_t* rgba, uint8_t* mask, float* uv,
+                           uint32_t* steps, int variant) {
+    const geo::PixelConsts k = geo::make_consts(s->rs, s->sphere_r, s->r_obs, s->step, s->max_steps);
+    const float inv_w = 1.0f / (float)width, inv_h = 1.0f / (float)height;
+    for (uint32_t ly = 0; ly < nrows; ++ly) {
+        const uint32_t py = row0 + ly;
+        for (uint32_t px = 0; px < width; ++px) {
+            float c2x, c2y, c2z;
+            geo::pixel_central_dir(f->display_to_movement, f->movement_to_central, f->psi_factor_and_position[0],
+                                   geo::aberration_kt(f->psi_factor_and_position[0]), width, height, inv_w, inv_h, px, py, &c2x, &c2y, &c2z);
+            const float st = geo::clampf_(c2z, -1.0f, 1.0f);
+            const float ct = geo::central_rho(c2x, c2y);
+            uint32_t n = 0;
+            float lam;
+            if (s->mode == GEO_MODE_FAN)
+                lam = geo::fan_lerp(fan, n_fan, st);
+            else
+                lam = geo::kPi2 - (variant == 0   ? geo::geodesic_angle_v<0>(k, st, ct, &n)
+                                   : variant == 1 ? geo::geodesic_angle_v<1>(k, st, ct, &n)
+                                                  : geo::geodesic_angle_v<2>(k, st, ct, &n));
+            const bool bh = lam < geo::kBlackHoleLambda;
+            float U, V;
+            geo::sky_uv(f->central_to_uv, c2x, c2y, ct, lam, &U, &V);
+            const size_t o = (size_t)ly * width + px;
+            rgba[o] = bh ? geo::kBlackRGBA : geo::sample_sky([sky](uint32_t i) { return sky[i]; }, sw, sh, U, V);
+            mask[o] = bh ? 1 : 0;
+            uv[2 * o] = U;
+            uv[2 * o + 1] = V;
+            steps[o] = n;
+        }
+    }
+    return 0;
+}

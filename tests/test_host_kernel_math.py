@@ -1,0 +1,89 @@
+"""The kernel's per-pixel header (geo_pixel.h), compiled for the HOST with the
+same no-contraction rules, must equal the oracle's independent f32
+restatement bit for bit.  CPU only: catches restatement/restructuring bugs
+before the GPU parity tests (which run the same sequence on gfx950)."""
+import ctypes
+import math
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import oracle as O
+from helpers import default_frame, default_scene
+from schwarzschild_raytracer_wgpu_amd._lib import GEO_MODE_FAN
+from schwarzschild_raytracer_wgpu_amd.scenes import make_sky
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+SRC = os.path.join(HERE, "native", "pixel_host.cpp")
+SO = os.path.join(HERE, "native", "libpixel_host.so")
+
+
+@pytest.fixture(scope="module")
+def host():
+    deps = [SRC] + [os.path.join(HERE, "..", "schwarzschild_raytracer_wgpu_amd", "csrc", h)
+                    for h in ("geo_pixel.h", "geo_math.h")]
+    if not os.path.exists(SO) or any(os.path.getmtime(d) > os.path.getmtime(SO) for d in deps):
+        subprocess.run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", "-mfma", "-msse4.1",
+                        "-o", SO, SRC], check=True)
+    lib = ctypes.CDLL(SO)
+    lib.host_render.restype = ctypes.c_int
+    return lib
+
+
+def run_host(lib, frame, scene, sky, w, h, fan=None, variant=2):
+    fr, sc = O.as_frame(frame), O.as_scene(scene)
+    sky = np.ascontiguousarray(sky)
+    fan_a = np.ascontiguousarray(fan, np.float32) if fan is not None else None
+    rgba = np.empty((h, w, 4), np.uint8)
+    mask = np.empty((h, w), np.uint8)
+    uv = np.empty((h, w, 2), np.float32)
+    steps = np.empty((h, w), np.uint32)
+    vp = ctypes.c_void_p
+    lib.host_render(ctypes.byref(fr), ctypes.byref(sc), vp(fan_a.ctypes.data if fan_a is not None else 0),
+                    ctypes.c_uint32(0 if fan_a is None else fan_a.size), vp(sky.ctypes.data),
+                    ctypes.c_uint32(sky.shape[1]), ctypes.c_uint32(sky.shape[0]), ctypes.c_uint32(w),
+                    ctypes.c_uint32(h), ctypes.c_uint32(0), ctypes.c_uint32(h), vp(rgba.ctypes.data),
+                    vp(mask.ctypes.data), vp(uv.ctypes.data), vp(steps.ctypes.data), ctypes.c_int(variant))
+    return dict(rgba=rgba, mask=mask, uv=uv, steps=steps)
+
+
+CASES = [
+    ("default_16x9", 160, 90, {}, dict(max_steps=2048)),
+    ("budget_128", 128, 128, {}, dict(max_steps=128)),
+    ("budget_odd_37", 96, 54, {}, dict(max_steps=37)),
+    ("budget_1", 64, 36, {}, dict(max_steps=1)),
+    ("budget_0", 32, 18, {}, dict(max_steps=0)),
+    ("unmoving", 96, 54, dict(state=0), dict(max_steps=512)),
+    ("inside_photon_sphere", 96, 54, dict(pos=(1.3, 0.2, 0.05), camera=(math.pi + 0.6, 0.3)),
+     dict(r_obs=math.sqrt(1.3 ** 2 + 0.2 ** 2 + 0.05 ** 2))),
+    ("inside_horizon", 64, 64, dict(pos=(0.8, 0.0, 0.05)), dict(r_obs=math.sqrt(0.64 + 0.0025))),
+    ("flat_space", 64, 36, dict(rs=0.0, state=0), dict(rs=0.0)),
+    ("outside_sphere", 64, 36, dict(pos=(60.0, 0.0, 1.0)), dict(r_obs=math.sqrt(3601.0))),
+]
+
+
+@pytest.mark.parametrize("variant", [0, 1, 2])
+@pytest.mark.parametrize("name,w,h,fk,sk", CASES, ids=[c[0] for c in CASES])
+def test_host_header_equals_oracle(host, name, w, h, fk, sk, variant):
+    """Every RK4 loop structure of geo_pixel.h (LOOP 0/1/2) equals the literal loop."""
+    sky = make_sky("equirect", (128, 64))
+    frame, scene = default_frame(w, h, **fk), default_scene(**sk)
+    a = run_host(host, frame, scene, sky, w, h, variant=variant)
+    b = O.render_f32(frame, scene, sky, w, h, threads=4)
+    for f in ("mask", "steps", "rgba"):
+        assert np.array_equal(a[f], b[f]), (f, np.argwhere(a[f] != b[f])[:5])
+    assert np.array_equal(a["uv"].view(np.uint32), b["uv"].view(np.uint32))
+
+
+def test_host_header_fan_mode(host):
+    sky = make_sky("equirect", (128, 64))
+    w, h = 96, 54
+    fan = O.solve_ray_fan(50.0, 1.0, 1000, math.pi / 100, 400, math.sqrt(2.5 ** 2 + 0.01))
+    frame, scene = default_frame(w, h), default_scene(1000, mode=GEO_MODE_FAN)
+    a = run_host(host, frame, scene, sky, w, h, fan=fan)
+    b = O.render_f32(frame, scene, sky, w, h, fan=fan, threads=4)
+    for f in ("mask", "rgba"):
+        assert np.array_equal(a[f], b[f])
+    assert np.array_equal(a["uv"].view(np.uint32), b["uv"].view(np.uint32))

@@ -33,14 +33,23 @@ NEWTON_EVALS = 3  # per sphere crossing (sphere_ray_tracer.rs:129)
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=20)
-    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--steps", type=int, default=200)
+    p.add_argument("--warmup", type=int, default=20)
+    p.add_argument("--spinup-frames", type=int, default=300,
+                   help="untimed GPU clock spin-up frames x n_gpus before the warmup steps (the clock settles "
+                        "after ~100 full frames); a frame count, identical on every rank")
+    p.add_argument("--event-every", type=int, default=4,
+                   help="time every k-th timed frame's kernel with a fence-free HIP event pair")
     p.add_argument("--config", default="cfg3_4k")
-    p.add_argument("--band-rows", type=int, default=16)
+    p.add_argument("--band-rows", type=int, default=8)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-threads", type=int, default=16)
     p.add_argument("--cpu-row-step", type=int, default=4)
     p.add_argument("--mode", default="direct", choices=["direct", "fan"])
+    p.add_argument("--check-frame", action="store_true",
+                   help="rank 0 checks the assembled frame against a single-launch full frame")
+    p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                   help="nccl (= RCCL over xGMI); gloo stages the gather through host memory (tests only)")
     return p.parse_args()
 
 
@@ -58,10 +67,15 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    ndev = torch.cuda.device_count()
+    local = local % max(1, ndev)  # >1 rank per GPU only for gloo rehearsals on a 1-GPU box
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
 
     cfg = CONFIGS[args.config]
     W, H = cfg.width, cfg.height
@@ -78,102 +92,87 @@ def main():
     if mode == g.GEO_MODE_FAN:
         ctx.solve_ray_fan(cfg.sphere_r, cfg.rs, cfg.max_steps, cfg.step, 400, obs.get_radial_position())
 
-    # interleaved row bands: rank g owns bands g, g+N, ... (balances the centre-heavy frame)
-    B = args.band_rows
-    nb_total = (H + B - 1) // B
-    nb_max = (nb_total + world - 1) // world
-    nb_mine = len(range(rank, nb_total, world))
-    band_bytes = B * W * 4
-    bufs = [torch.empty(nb_max * band_bytes, dtype=torch.uint8, device=dev) for _ in range(2)]
-    steps_ctr = torch.zeros(1, dtype=torch.int64, device=dev)
+    # interleaved 8-row bands: rank g owns bands g, g+N, ... (balances the centre-heavy frame:
+    # 270 bands of the 4K frame -> 34 vs 33.75 per rank at N=8); gather to rank 0 over RCCL
+    from schwarzschild_raytracer_wgpu_amd.dist import ShardedFrame
 
-    def render(buf, **kw):
-        ctx.render_bands(frame, scene, W, H, B, rank, world, nb_mine, buf, **kw)
+    sf = ShardedFrame(ctx, frame, scene, W, H, args.band_rows, rank, world, dev, dist if world > 1 else None,
+                      host_gather=args.dist_backend == "gloo")
+    L = sf.layout
+    steps_ctr = torch.zeros(1, dtype=torch.int64, device=dev)
 
     # untimed diagnostic pass: per-pixel steps + mask give the RK4 evaluations
     # per launch (main-loop steps + 3 Newton evaluations per sphere crossing)
-    diag_mask = torch.zeros(nb_max * B * W, dtype=torch.uint8, device=dev)
-    diag_steps = torch.zeros(nb_max * B * W, dtype=torch.int32, device=dev)
+    n_loc = L.nb_max * L.band_rows * W
+    diag_mask = torch.zeros(n_loc, dtype=torch.uint8, device=dev)
+    diag_steps = torch.zeros(n_loc, dtype=torch.int32, device=dev)
     diag_ctr = torch.zeros(1, dtype=torch.int64, device=dev)
-    render(bufs[0], out_mask=diag_mask, out_steps=diag_steps, steps_total=diag_ctr)
+    sf.render_local(sf.bufs[0], out_mask=diag_mask, out_steps=diag_steps, steps_total=diag_ctr)
     torch.cuda.synchronize()
-    n_valid = nb_mine * B * W
-    st = diag_steps[: n_valid].to(torch.int64)
-    hits = int(((diag_mask[: n_valid] == 0) & (st > 0)).sum().item())
-    # clipped rows of the last band are not written: count rows that exist
-    rows_mine = sum(min(B, H - b * B) for b in range(rank, nb_total, world))
+    st = diag_steps.to(torch.int64)
+    hits = int(((diag_mask == 0) & (st > 0)).sum().item())  # unwritten (clipped) rows are 0
+    rows_mine = L.rows_mine()
     steps_diag = int(diag_ctr.item())
     evals_per_launch = steps_diag + NEWTON_EVALS * hits
 
-    full = None
-    recv = None
-    if world > 1 and rank == 0:
-        full = torch.empty(nb_total * band_bytes, dtype=torch.uint8, device=dev)
-        recv = [[torch.empty(nb_max * band_bytes, dtype=torch.uint8, device=dev) for _ in range(world)]
-                for _ in range(2)]
-    works = [None, None]
-
-    def one_frame(i, ev=None):
-        slot = i % 2
-        if works[slot] is not None:
-            works[slot].wait()
-            works[slot] = None
-            if rank == 0:
-                assemble(slot)
-        if ev is not None:
-            ev[0].record()
-        render(bufs[slot], steps_total=steps_ctr)
-        if ev is not None:
-            ev[1].record()
-        if world > 1:
-            works[slot] = dist.gather(bufs[slot], gather_list=recv[slot] if rank == 0 else None, dst=0,
-                                      async_op=True)
-
-    def assemble(slot):
-        fv = full.view(nb_total, band_bytes)
-        for r in range(world):
-            n = len(range(r, nb_total, world))
-            fv[r::world] = recv[slot][r].view(nb_max, band_bytes)[:n]
-
-    def drain():
-        for s in (0, 1):
-            if works[s] is not None:
-                works[s].wait()
-                works[s] = None
-                if rank == 0:
-                    assemble(s)
-
+    # GPU clock spin-up (untimed, not counted as warmup): from idle the first
+    # frames run up to 5x slower while the clock ramps (tools/ubench/gap_probe2.py)
+    spin = args.spinup_frames * world
+    for i in range(spin):
+        sf.step(i)
+        if i % 50 == 49:
+            sf.drain()
+            torch.cuda.synchronize()
     for i in range(args.warmup):
-        one_frame(i)
-    drain()
+        sf.step(spin + i)
+    sf.drain()
     torch.cuda.synchronize()
+
+    # timed region: K frames; steps counted in the context (GEO_FLAG_DEFER_STEPS)
+    # and flushed once at the end; fence-free event pairs on every k-th frame
+    from schwarzschild_raytracer_wgpu_amd.timing import HipEvent
+
+    scene_defer = g.make_scene(cfg.rs, cfg.sphere_r, obs.get_radial_position(), cfg.step, cfg.max_steps, mode,
+                               flags=g._lib.GEO_FLAG_DEFER_STEPS)
+    timed = set(range(0, args.steps, max(1, args.event_every)))
+    evs = {i: (HipEvent(), HipEvent()) for i in timed}
     steps_ctr.zero_()
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        one_frame(i, evs[i])
-    drain()
+        sf.step(i, events=evs.get(i), scene=scene_defer)
+    ctx.steps_flush(steps_ctr)
+    sf.drain()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
     elapsed = t1 - t0
-    kernel_ms = sorted(a.elapsed_time(b) for a, b in evs)
+    kernel_ms = sorted(a.elapsed_time(b) for a, b in evs.values())
     kernel_ms_avg = sum(kernel_ms) / len(kernel_ms)
 
     steps_done = int(steps_ctr.item())
     if steps_done != steps_diag * args.steps:
         raise SystemExit(f"step counter mismatch: {steps_done} vs {steps_diag} x {args.steps}")
-    stats = torch.tensor([elapsed, kernel_ms_avg], dtype=torch.float64, device=dev)
-    tot = torch.tensor([steps_done, rows_mine * W * args.steps, evals_per_launch], dtype=torch.int64, device=dev)
+    rdev = dev if args.dist_backend == "nccl" else "cpu"
+    stats = torch.tensor([elapsed, kernel_ms_avg], dtype=torch.float64, device=rdev)
+    tot = torch.tensor([steps_done, rows_mine * W * args.steps, evals_per_launch], dtype=torch.int64, device=rdev)
     if world > 1:
         dist.all_reduce(stats, op=dist.ReduceOp.MAX)
         dist.all_reduce(tot, op=dist.ReduceOp.SUM)
     elapsed_max, kernel_ms_max = float(stats[0]), float(stats[1])
     total_steps, total_pixels, evals_all = (int(x) for x in tot.tolist())
+
+    if args.check_frame and rank == 0:
+        ref = torch.empty(H * W * 4, dtype=torch.uint8, device=dev)
+        ctx.render_rows(frame, scene, W, H, 0, H, ref)
+        torch.cuda.synchronize()
+        if not torch.equal(sf.frame_rgba(), ref):
+            raise SystemExit("assembled frame differs from the single-launch frame")
+        print(f"check-frame: assembled {W}x{H} frame from {world} rank(s) equals the single-launch frame",
+              file=sys.stderr)
 
     if rank != 0:
         dist.destroy_process_group()
@@ -201,7 +200,7 @@ def main():
                         f"step pi/100, {cfg.max_steps} max RK4 steps, mode {args.mode}",
             "width": W, "height": H, "max_steps": cfg.max_steps,
             "parallelism": f"rowbands{world}" if world > 1 else "single",
-            "band_rows": B,
+            "band_rows": args.band_rows,
         },
         "per_gpu": value / world,
         "pixels_per_s": total_pixels / elapsed_max,
@@ -209,7 +208,9 @@ def main():
         "steps_per_frame": total_steps // args.steps,
         "mean_steps_per_pixel": total_steps / total_pixels,
         "kernel_ms": {"avg": kernel_ms_avg, "median": kernel_ms[len(kernel_ms) // 2], "min": kernel_ms[0],
-                      "max_over_ranks_avg": kernel_ms_max},
+                      "max_over_ranks_avg": kernel_ms_max, "frames_timed": len(kernel_ms),
+                      "events": "hipEventDisableSystemFence pairs on every %d-th timed frame" % args.event_every},
+        "spinup_frames": spin,
         "roofline": {
             "bound": "valu",
             "achieved": achieved_tflops,

@@ -55,6 +55,11 @@ typedef enum geo_status {
 #define GEO_MODE_DIRECT 0u /* per-pixel RK4 of the null geodesic at the pixel's own angle */
 #define GEO_MODE_FAN 1u    /* reference-exact: lerp into the ray fan (shader.wgsl:77-84) */
 
+/* geo_scene.flags */
+#define GEO_FLAG_DEFER_STEPS 1u /* executed steps accumulate in the context (no per-call
+                                   fold); read them with geo_steps_flush.  steps_total
+                                   must then be NULL. */
+
 /* Observer motion states, ObserverState (SR/simulation/observer.rs:12-16). */
 #define GEO_OBSERVER_UNMOVING 0
 #define GEO_OBSERVER_FROZEN_FALL 1
@@ -80,9 +85,9 @@ typedef struct geo_scene {
     float sphere_r;     /* radius of the textured sky sphere */
     float r_obs;        /* observer radial position |pos| (lib.rs:292) */
     float step;         /* RK4 step in traveled angle (PI/100 in the reference) */
-    uint32_t max_steps; /* RK4 budget per ray (1000 in the reference) */
+    uint32_t max_steps; /* RK4 budget per ray (1000 in the reference), <= 2^24 */
     uint32_t mode;      /* GEO_MODE_* */
-    uint32_t flags;     /* reserved, must be 0 */
+    uint32_t flags;     /* GEO_FLAG_* */
     uint32_t reserved;  /* must be 0 */
 } geo_scene;
 
@@ -130,7 +135,8 @@ int geo_render_rows(geo_ctx* ctx, const geo_frame* frame, const geo_scene* scene
                     uint32_t* out_steps, unsigned long long* steps_total, void* stream);
 
 /* Renders an interleaved set of row bands (balanced multi-GPU sharding): bands
- * band0, band0+band_step, ..., nbands of them, each band_rows tall; band b
+ * band0, band0+band_step, ..., nbands of them, each band_rows tall (a
+ * multiple of 8, the pixel rows of one wave); band b
  * covers rows [b*band_rows, (b+1)*band_rows) clipped to height.  Outputs are
  * packed band after band (nbands*band_rows rows; clipped rows are not
  * written).  geo_render_rows(row0, nrows) is the single-band case. */
@@ -140,8 +146,9 @@ int geo_render_bands(geo_ctx* ctx, const geo_frame* frame, const geo_scene* scen
                      float* out_uv, uint32_t* out_steps, unsigned long long* steps_total,
                      void* stream);
 
-/* Sets the persistent-grid size used by geo_render_rows (0 = automatic). */
-int geo_set_launch_blocks(geo_ctx* ctx, uint32_t blocks);
+/* Adds the steps accumulated under GEO_FLAG_DEFER_STEPS to *steps_total
+ * (device u64) and clears the context's counter.  Asynchronous on `stream`. */
+int geo_steps_flush(geo_ctx* ctx, unsigned long long* steps_total, void* stream);
 
 /* ---- observer (host, f64; SR/simulation/observer.rs) ----------------- */
 /* Observer::new (observer.rs:68-87): pos (25,0,1), camera (PI,0), FrozenFall,

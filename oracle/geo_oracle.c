@@ -294,6 +294,7 @@ typedef struct {
     uint32_t max_steps;
     float hh, h6, hh2, hhh, h2_6, r3_2, sphere_u, schwarz_u, u0, h_over_r2, bound, e_out, e_in, barrier;
     int r_inside_h, outside, sphere_outside, inside_sphere, diff_sides, rs_nonzero;
+    float scale, U0, SU, BD, HU; /* scaled state U = scale*u */
 } fconsts;
 
 static fconsts make_fconsts(const geo_scene* s) {
@@ -325,26 +326,34 @@ static fconsts make_fconsts(const geo_scene* s) {
     k.inside_sphere = k.r < k.sphere_r;
     k.diff_sides = ((k.r < k.r3_2) != (k.sphere_r < k.r3_2)) && (fabsf(k.r - k.r3_2) > 1e-10f);
     k.rs_nonzero = k.rs != 0.0f;
+    k.scale = k.rs_nonzero ? k.r3_2 : 1.0f;
+    k.U0 = k.scale * k.u0;
+    k.SU = k.scale * k.sphere_u;
+    k.BD = k.scale * k.bound;
+    k.HU = k.scale * k.schwarz_u;
     return k;
 }
 
-/* the RK4 step of sphere_ray_tracer.rs:137-146 with f(x) = x*(c*x - 1), stage
+/* the RK4 step of sphere_ray_tracer.rs:137-146 on the scaled state U = c*u
+ * (c = 3rs/2; c*f(u) = F(U) = U*(U - 1), or F(U) = -U for rs = 0), stage
  * values in the algebraically identical forms of DESIGN.md §3:
- *   a_u = u + h/2 ub, b_u = a_u + h^2/4 f(u), u_h = u + h ub, c_u = u_h + h^2/2 f(a_u),
- *   next_u = u_h + h^2/6 (f(u)+f(a_u)+f(b_u)), next_ub = ub + h/6 (f(u)+2f(a_u)+2f(b_u)+f(c_u)). */
-static inline void rk4f(float u, float ub, float h, float hh, float hh2, float hhh, float h6, float h2_6,
-                        float c, float* nu, float* nub) {
-    float fu = fmaf(c, u, -1.0f) * u;
-    float au = fmaf(hh, ub, u);
-    float uh = fmaf(h, ub, u);
-    float fa = fmaf(c, au, -1.0f) * au;
+ *   a = U + h/2 UB, b = a + h^2/4 F(U), U_h = U + h UB, c = U_h + h^2/2 F(a),
+ *   next_U = U_h + h^2/6 (F(U)+F(a)+F(b)), next_UB = UB + h/6 (F(U)+2F(a)+2F(b)+F(c)). */
+static inline float Ff(float U, int flat) { return flat ? -U : fmaf(U, U, -U); }
+
+static inline void rk4f(float U, float UB, float h, float hh, float hh2, float hhh, float h6, float h2_6,
+                        int flat, float* NU, float* NUB) {
+    float fu = Ff(U, flat);
+    float au = fmaf(hh, UB, U);
+    float uh = fmaf(h, UB, U);
+    float fa = Ff(au, flat);
     float bu = fmaf(hh2, fu, au);
-    float fb = fmaf(c, bu, -1.0f) * bu;
+    float fb = Ff(bu, flat);
     float cu = fmaf(hhh, fa, uh);
-    float fc = fmaf(c, cu, -1.0f) * cu;
+    float fc = Ff(cu, flat);
     float fab = fa + fb;
-    *nu = fmaf(h2_6, fu + fab, uh);
-    *nub = fmaf(h6, fmaf(2.0f, fab, fu) + fc, ub);
+    *NU = fmaf(h2_6, fu + fab, uh);
+    *NUB = fmaf(h6, fmaf(2.0f, fab, fu) + fc, UB);
 }
 
 static float geodesic_f32(const fconsts* k, float st, float ct, uint32_t* steps) {
@@ -376,37 +385,41 @@ static float geodesic_f32(const fconsts* k, float st, float ct, uint32_t* steps)
         (barrier && k->diff_sides) || (k->r < k->r3_2 && k->inside_sphere && falling) ||
         (k->r > k->r3_2 && !k->inside_sphere && !falling))
         return 15.0f;
-    float u = k->u0;
     float ub = sqrtf(maxz(0.0f, inv_b2 - k->h_over_r2));
     if (!falling) ub = -ub;
-    float su = k->sphere_u, c = k->r3_2;
+    /* loop test (:134-135) for the initial state, in the reference's variables */
+    if ((k->rs_nonzero && k->u0 > k->schwarz_u && ub > 0.0f) || k->max_steps == 0u || !(k->u0 > 0.0f)) return 15.0f;
+    int flat = !k->rs_nonzero;
+    float U = k->U0, UB = k->scale * ub;
     uint32_t it = 0;
-    while (!(k->rs_nonzero && u > k->schwarz_u && ub > 0.0f) && it < k->max_steps && u > 0.0f) {
-        float nu, nub;
-        rk4f(u, ub, k->step, k->hh, k->hh2, k->hhh, k->h6, k->h2_6, c, &nu, &nub);
+    for (;;) { /* :134-191, one step per iteration */
+        float NU, NUB;
+        rk4f(U, UB, k->step, k->hh, k->hh2, k->hhh, k->h6, k->h2_6, flat, &NU, &NUB);
         ++it;
-        if ((nu > su) != (u > su)) {
+        if ((NU > k->SU) != (U > k->SU)) {
             float ns, wu, wub;
-            if (fabsf(ub) > fabsf(nub)) {
-                ns = 0.0f; wu = u; wub = ub;
+            if (fabsf(UB) > fabsf(NUB)) {
+                ns = 0.0f; wu = U; wub = UB;
             } else {
-                ns = k->step; wu = nu; wub = nub;
+                ns = k->step; wu = NU; wub = NUB;
             }
             for (int n = 0; n < 3; ++n) {
-                ns = ns - (wu - su) / wub;
+                ns = ns - (wu - k->SU) / wub;
                 float n2 = ns * ns;
                 float n6 = ns * (1.0f / 6.0f);
-                rk4f(u, ub, ns, ns * 0.5f, n2 * 0.25f, n2 * 0.5f, n6, ns * n6, c, &wu, &wub);
+                rk4f(U, UB, ns, ns * 0.5f, n2 * 0.25f, n2 * 0.5f, n6, ns * n6, flat, &wu, &wub);
             }
             *steps = it;
             return (float)(it - 1u) * k->step + ns;
         }
-        if (nu < k->bound) {
+        if (NU < k->BD) {
             *steps = it;
             return 15.0f;
         }
-        u = nu;
-        ub = nub;
+        U = NU;
+        UB = NUB;
+        /* loop test: not inside the horizon and falling, budget, u > 0 */
+        if ((k->rs_nonzero && U > k->HU && UB > 0.0f) || !(it < k->max_steps) || !(U > 0.0f)) break;
     }
     *steps = it;
     return 15.0f;

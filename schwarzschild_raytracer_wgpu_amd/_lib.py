@@ -20,6 +20,7 @@ GEO_ESTATE = -5
 
 GEO_MODE_DIRECT = 0
 GEO_MODE_FAN = 1
+GEO_FLAG_DEFER_STEPS = 1
 
 GEO_OBSERVER_UNMOVING = 0
 GEO_OBSERVER_FROZEN_FALL = 1
@@ -79,7 +80,7 @@ SIGNATURES = {
         [_vp, ctypes.POINTER(GeoFrame), ctypes.POINTER(GeoScene), _u32, _u32, _u32, _u32, _u32, _u32, _vp,
          _vp, _vp, _vp, _vp, _vp],
     ),
-    "geo_set_launch_blocks": (_int, [_vp, _u32]),
+    "geo_steps_flush": (_int, [_vp, _vp, _vp]),
     "geo_observer_create": (_int, [_f64, _f64, _f64, _f64, ctypes.POINTER(_vp)]),
     "geo_observer_destroy": (None, [_vp]),
     "geo_observer_set_position": (_int, [_vp, _f64, _f64, _f64]),

@@ -142,8 +142,9 @@ class Context:
                                                          out.ctypes.data, _stream_handle(stream)))
         return out
 
-    def set_launch_blocks(self, blocks: int) -> None:
-        check("geo_set_launch_blocks", lib.geo_set_launch_blocks(self._h, blocks))
+    def steps_flush(self, steps_total, stream=None) -> None:
+        """geo_steps_flush: add the GEO_FLAG_DEFER_STEPS accumulator to steps_total (device u64)."""
+        check("geo_steps_flush", lib.geo_steps_flush(self._h, _ptr(steps_total), _stream_handle(stream)))
 
     def render_rows(self, frame: GeoFrame, scene: GeoScene, width: int, height: int, row0: int, nrows: int,
                     out_rgba, out_mask=None, out_uv=None, out_steps=None, steps_total=None, stream=None) -> None:
@@ -174,8 +175,8 @@ class Context:
 
 
 def make_scene(rs: float, sphere_r: float, r_obs: float, step: float = math.pi / 100.0, max_steps: int = 1000,
-               mode: int = _lib.GEO_MODE_DIRECT) -> GeoScene:
-    return GeoScene(rs, sphere_r, r_obs, step, max_steps, mode, 0, 0)
+               mode: int = _lib.GEO_MODE_DIRECT, flags: int = 0) -> GeoScene:
+    return GeoScene(rs, sphere_r, r_obs, step, max_steps, mode, flags, 0)
 
 
 class SphereRayTracer:

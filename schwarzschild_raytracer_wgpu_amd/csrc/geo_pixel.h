@@ -51,7 +51,14 @@ struct PixelConsts {
     float radial_falling, radial_outgoing;  // result for rotation < 1e-10, by `falling`
     bool radial_by_energy;                  // radial result decided by energy > 0 instead
     bool pf_always, pf_falling, pf_outgoing, pf_eneg, pf_barrier;
+    // the integrator's scaled state U = scale*u (scale = 3 rs/2, or 1 for rs = 0)
+    float scale, U0, SU, BD, HU;
 };
+
+// Integration kinds (frame-uniform, chosen on the host):
+constexpr int kCurvedOut = 0;  // rs > 0, observer outside the horizon (r > rs)
+constexpr int kCurvedIn = 1;   // rs > 0, observer on/inside the horizon
+constexpr int kFlat = 2;       // rs = 0: straight lines
 
 GEO_HD PixelConsts make_consts(float rs, float sphere_r, float r, float step, uint32_t max_steps) {
     PixelConsts k;
@@ -104,62 +111,99 @@ GEO_HD PixelConsts make_consts(float rs, float sphere_r, float r, float step, ui
     k.pf_barrier = k.rs > 0.0f && k.diff_sides;     // & 1/b^2 < 4/(27 rs^2)
     k.pf_falling = r < k.r3_2 && k.inside_sphere;   // & falling
     k.pf_outgoing = r > k.r3_2 && !k.inside_sphere; // & !falling
+    k.scale = k.rs_nonzero ? k.r3_2 : 1.0f;
+    k.U0 = k.scale * k.u0;
+    k.SU = k.scale * k.sphere_u;
+    k.BD = k.scale * k.bound;
+    k.HU = k.scale * k.schwarz_u;
     return k;
 }
 
-// One classic RK4 step of u'' = -u + c u^2 (sphere_ray_tracer.rs:137-146),
-// f(x) = x (c x - 1), in 18 VALU ops.  The reference's stage values are
-// evaluated in algebraically identical forms that need neither a_ub, b_ub
-// nor c_ub:
-//   a_u = u + h/2 ub            b_u = a_u + h^2/4 f(u)      [= u + h/2 a_ub]
-//   u_h = u + h ub              c_u = u_h + h^2/2 f(a_u)    [= u + h b_ub]
-//   next_u  = u_h + h^2/6 (f(u) + f(a_u) + f(b_u))          [= u + h/6 (ub + 2a_ub + 2b_ub + c_ub)]
-//   next_ub = ub + h/6 (f(u) + 2 f(a_u) + 2 f(b_u) + f(c_u))
+GEO_HD int geodesic_kind(const PixelConsts& k) {
+    return !k.rs_nonzero ? kFlat : (k.outside ? kCurvedOut : kCurvedIn);
+}
+
+// The integrator works on the scaled state U = c u (c = 3 rs/2): RK4 commutes
+// with a linear rescaling of the state, and c f(u) = c(-u + c u^2) becomes
+//   F(U) = U (U - 1) = fma(U, U, -U)                     (one FMA),
+// or F(U) = -U in flat space (rs = 0, scale 1).  The sphere, escape and
+// horizon thresholds are scaled alike (SU, BD, HU); Newton's ratio
+// (u - su)/ub is scale-free.
+template <int KIND>
+GEO_HD float F_(float U) {
+    if constexpr (KIND == kFlat)
+        return -U;
+    else
+        return fmaf_(U, U, -U);
+}
+
+// One classic RK4 step of U'' = F(U) (sphere_ray_tracer.rs:137-146) in 14
+// VALU ops.  The reference's stage values are evaluated in algebraically
+// identical forms that need neither a_ub, b_ub nor c_ub:
+//   a = U + h/2 UB            b = a + h^2/4 F(U)        [= U + h/2 a_ub]
+//   U_h = U + h UB            c = U_h + h^2/2 F(a)      [= U + h b_ub]
+//   next_U  = U_h + h^2/6 (F(U) + F(a) + F(b))          [= U + h/6 (UB + 2a_ub + 2b_ub + c_ub)]
+//   next_UB = UB + h/6 (F(U) + 2 F(a) + 2 F(b) + F(c))
 // hh = h/2, hh2 = h^2/4, hhh = h^2/2, h6 = h/6, h2_6 = h^2/6.
-GEO_HD void rk4_step(float u, float ub, float h, float hh, float hh2, float hhh, float h6, float h2_6,
-                     float c, float* nu, float* nub) {
-    const float fu = fmaf_(c, u, -1.0f) * u;
-    const float au = fmaf_(hh, ub, u);
-    const float uh = fmaf_(h, ub, u);
-    const float fa = fmaf_(c, au, -1.0f) * au;
+template <int KIND>
+GEO_HD void rk4_step(float U, float UB, float h, float hh, float hh2, float hhh, float h6, float h2_6,
+                     float* NU, float* NUB) {
+    const float fu = F_<KIND>(U);
+    const float au = fmaf_(hh, UB, U);
+    const float uh = fmaf_(h, UB, U);
+    const float fa = F_<KIND>(au);
     const float bu = fmaf_(hh2, fu, au);
-    const float fb = fmaf_(c, bu, -1.0f) * bu;
+    const float fb = F_<KIND>(bu);
     const float cu = fmaf_(hhh, fa, uh);
-    const float fc = fmaf_(c, cu, -1.0f) * cu;
+    const float fc = F_<KIND>(cu);
     const float fab = fa + fb;
-    *nu = fmaf_(h2_6, fu + fab, uh);
-    *nub = fmaf_(h6, fmaf_(2.0f, fab, fu) + fc, ub);
+    *NU = fmaf_(h2_6, fu + fab, uh);
+    *NUB = fmaf_(h6, fmaf_(2.0f, fab, fu) + fc, UB);
+}
+
+// The horizon half of the loop test (:134), `u > 1/rs && ub > 0`.  For an
+// observer outside the horizon it reduces to `u > 1/rs`: beyond the photon
+// sphere u'' > 0, so a ray from r > rs reaches u > 1/rs only while ub > 0.
+// (The oracle keeps the full test; tests require bit equality.)
+template <int KIND>
+GEO_HD bool horizon_(float NU, float NUB, float HU) {
+    if constexpr (KIND == kCurvedOut)
+        return NU > HU;
+    else if constexpr (KIND == kCurvedIn)
+        return (NU > HU) & (NUB > 0.0f);
+    else
+        return false;
 }
 
 // Newton on the step length from the steeper end (:150-182), from the
-// pre-step state (u, ub) and the post-step state (nu, nub) of step `it`.
-GEO_HD float newton_angle(const PixelConsts& k, float u, float ub, float nu, float nub, uint32_t it) {
-    const float su = k.sphere_u;
-    const float c = k.r3_2;
+// pre-step state (U, UB) and the post-step state (NU, NUB) of step `it`.
+template <int KIND>
+GEO_HD float newton_angle(const PixelConsts& k, float U, float UB, float NU, float NUB, uint32_t it) {
     float ns, wu, wub;
-    if (__builtin_fabsf(ub) > __builtin_fabsf(nub)) {
+    if (__builtin_fabsf(UB) > __builtin_fabsf(NUB)) {
         ns = 0.0f;
-        wu = u;
-        wub = ub;
+        wu = U;
+        wub = UB;
     } else {
         ns = k.step;
-        wu = nu;
-        wub = nub;
+        wu = NU;
+        wub = NUB;
     }
     for (int n = 0; n < kNewtonIters; ++n) {
-        ns = ns - (wu - su) / wub;
+        ns = ns - (wu - k.SU) / wub;
         const float n2 = ns * ns;
         const float n6 = ns * kSixth;
-        rk4_step(u, ub, ns, ns * 0.5f, n2 * 0.25f, n2 * 0.5f, n6, ns * n6, c, &wu, &wub);
+        rk4_step<KIND>(U, UB, ns, ns * 0.5f, n2 * 0.25f, n2 * 0.5f, n6, ns * n6, &wu, &wub);
     }
     return (float)(it - 1u) * k.step + ns;
 }
 
-
-// Traveled angle of the ray seen at angle theta from the black hole
-// or kNoValue.  *steps = executed main-loop RK4 steps.
-// (st, ct) = (sin theta, cos theta >= 0) of the central-frame direction.
-template <int LOOP>
+// Traveled angle of the ray at angle theta to the black hole, or kNoValue.
+// (st, ct) = (sin theta, cos theta >= 0) of the central-frame direction;
+// *steps = executed main-loop RK4 steps.  LOOP selects the loop structure
+// (0: one step per exit test, 1: two; tools/ubench/loop_ab.hip), KIND the
+// integration kind (geodesic_kind).
+template <int LOOP, int KIND>
 GEO_HD float geodesic_angle_v(const PixelConsts& k, float st, float ct, uint32_t* steps) {
     *steps = 0;
     // solve_ray_fan per node (sphere_ray_tracer.rs:38-49)
@@ -187,61 +231,63 @@ GEO_HD float geodesic_angle_v(const PixelConsts& k, float st, float ct, uint32_t
     }
     // RK4 init (:122-132); the radicand is clamped at 0 (the reference yields
     // NaN there only for |theta| < ~1e-8, never at a fan node).
-    float u = k.u0;
     float ub = __builtin_sqrtf(fmaxf_(0.0f, inv_b2 - k.h_over_r2));
     if (!falling) ub = -ub;
-    const float su = k.sphere_u;
-    const float c = k.r3_2;
-    // Loop test of :134-135 on the initial state.  schwarz_u = 1/rs is +inf
-    // for rs = 0, so `u > schwarz_u` already encodes `rs != 0 &&`.
-    if ((u > k.schwarz_u && ub > 0.0f) || k.max_steps == 0u || !(u > 0.0f)) return kNoValue;
+    // loop test of :134-135 on the initial state (schwarz_u = +inf for rs = 0)
+    if ((k.u0 > k.schwarz_u && ub > 0.0f) || k.max_steps == 0u || !(k.u0 > 0.0f)) return kNoValue;
+    float U = k.U0, UB = k.scale * ub;
+    const float SU = k.SU, BD = k.BD, HU = k.HU;
+    const float h = k.step, hh = k.hh, hh2 = k.hh2, hhh = k.hhh, h6 = k.h6, h2_6 = k.h2_6;
+    // Main loop (:134-191), restructured for the wave64 VALU.  Per step the
+    // lane-exit flag is crossing (:150) | escape (:184) | horizon (:134);
+    // `!(NU >= BD)` is (NU < BD) or NaN and, with BD > 0, also covers the
+    // `u > 0` test; the budget (:135) is wave-uniform.  Results equal the
+    // literal loop's (the oracle keeps that form; tests require bit equality).
     if constexpr (LOOP == 0) {
-        // Single step per exit test (one lane-exit flag per step).
         uint32_t it = 0;
-        bool above = u > su;
+        bool above = U > SU;
         bool cross;
-        float nu, nub;
+        float NU, NUB;
         for (;;) {
-            rk4_step(u, ub, k.step, k.hh, k.hh2, k.hhh, k.h6, k.h2_6, c, &nu, &nub);
+            rk4_step<KIND>(U, UB, h, hh, hh2, hhh, h6, h2_6, &NU, &NUB);
             ++it;
-            const bool nabove = nu > su;
+            const bool nabove = NU > SU;
             cross = nabove != above;
-            const bool stop = cross | !(nu >= k.bound) | ((nu > k.schwarz_u) & (nub > 0.0f)) |
-                              (it >= k.max_steps);
-            if (stop) break;
-            u = nu;
-            ub = nub;
+            if (cross | !(NU >= BD) | horizon_<KIND>(NU, NUB, HU) | (it >= k.max_steps)) break;
+            U = NU;
+            UB = NUB;
             above = nabove;
         }
         *steps = it;
         if (!cross) return kNoValue;
-        return newton_angle(k, u, ub, nu, nub, it);
-    }
-    if constexpr (LOOP == 1) {
-        // Two steps per exit test, budget as a uniform pair bound, no ping-pong.
-        const float hu = k.schwarz_u, bd = k.bound;
+        return newton_angle<KIND>(k, U, UB, NU, NUB, it);
+    } else {
+        // TWO RK4 steps per exit test; a lane whose first step stops discards
+        // the second.  The pair budget is a wave-uniform loop bound.
         const uint32_t ms = k.max_steps;
         const uint32_t npairs = ms >> 1;
-        uint32_t it = npairs << 1;
-        bool above = u > su;
-        float n1u = u, n1b = ub, n2u = u, n2b = ub;
+        uint32_t it = npairs << 1;  // per lane: steps before the stopping pair (budget: all)
+        bool above = U > SU;
+        float n1u = U, n1b = UB, n2u = U, n2b = UB;
         for (uint32_t q = 0; q < npairs; ++q) {
-            rk4_step(u, ub, k.step, k.hh, k.hh2, k.hhh, k.h6, k.h2_6, c, &n1u, &n1b);
-            const bool a1 = n1u > su;
-            const bool s1 = (a1 != above) | !(n1u >= bd) | ((n1u > hu) & (n1b > 0.0f));
-            rk4_step(n1u, n1b, k.step, k.hh, k.hh2, k.hhh, k.h6, k.h2_6, c, &n2u, &n2b);
-            const bool a2 = n2u > su;
-            const bool s2 = (a2 != a1) | !(n2u >= bd) | ((n2u > hu) & (n2b > 0.0f));
+            rk4_step<KIND>(U, UB, h, hh, hh2, hhh, h6, h2_6, &n1u, &n1b);
+            const bool a1 = n1u > SU;
+            const bool s1 = (a1 != above) | !(n1u >= BD) | horizon_<KIND>(n1u, n1b, HU);
+            rk4_step<KIND>(n1u, n1b, h, hh, hh2, hhh, h6, h2_6, &n2u, &n2b);
+            const bool a2 = n2u > SU;
+            const bool s2 = (a2 != a1) | !(n2u >= BD) | horizon_<KIND>(n2u, n2b, HU);
             if (s1 | s2) {
                 it = q << 1;
                 break;
             }
-            u = n2u;
-            ub = n2b;
+            U = n2u;
+            UB = n2b;
             above = a2;
         }
-        GEO_OPAQUE(u);
-        GEO_OPAQUE(ub);
+        // Opaque copies: the flags below are recomputed from the state rather
+        // than carried out of the loop as lane masks (fewer SALU per pair).
+        GEO_OPAQUE(U);
+        GEO_OPAQUE(UB);
         GEO_OPAQUE(n1u);
         GEO_OPAQUE(n1b);
         GEO_OPAQUE(n2u);
@@ -249,114 +295,37 @@ GEO_HD float geodesic_angle_v(const PixelConsts& k, float st, float ct, uint32_t
         GEO_OPAQUE(it);
         float ou, oub, nu, nub;
         if (it + 2u <= ms) {
-            const bool s1 = ((n1u > su) != (u > su)) | !(n1u >= bd) | ((n1u > hu) & (n1b > 0.0f));
+            // stopped inside the pair, at step it+1 or it+2
+            const bool s1 = ((n1u > SU) != (U > SU)) | !(n1u >= BD) | horizon_<KIND>(n1u, n1b, HU);
             if (s1) {
-                ou = u; oub = ub; nu = n1u; nub = n1b; it += 1u;
+                ou = U; oub = UB; nu = n1u; nub = n1b; it += 1u;
             } else {
                 ou = n1u; oub = n1b; nu = n2u; nub = n2b; it += 2u;
             }
         } else {
-            ou = u; oub = ub; nu = u; nub = ub;
+            // budget exit: at most one step left
+            ou = U; oub = UB; nu = U; nub = UB;
             if (it < ms) {
-                rk4_step(u, ub, k.step, k.hh, k.hh2, k.hhh, k.h6, k.h2_6, c, &nu, &nub);
+                rk4_step<KIND>(U, UB, h, hh, hh2, hhh, h6, h2_6, &nu, &nub);
                 it += 1u;
             }
         }
         *steps = it;
-        if ((nu > su) == (ou > su)) return kNoValue;
-        return newton_angle(k, ou, oub, nu, nub, it);
-    }
-    // Main loop (:134-191), restructured for the wave64 VALU:
-    //  * TWO RK4 steps per exit test; the per-step stop flag is crossing
-    //    (:150) | escape (:184) | the horizon part of the next loop test
-    //    (:134).  `!(nu >= bound)` is (nu < bound) or NaN and, with bound > 0,
-    //    also covers `u > 0`.  A lane whose first step stops discards the second.
-    //  * the budget (:135) is a wave-uniform bound on a scalar pair counter;
-    //  * the state ping-pongs between register sets A = (u, ub) and
-    //    B = (bu, bb) (A -> t -> B, then B -> t -> A): no copies.
-    // Results equal the literal loop's (the oracle keeps that form; tests
-    // require bit equality).
-    if constexpr (LOOP == 2) {
-    const float hu = k.schwarz_u, bd = k.bound;
-    const uint32_t ms = k.max_steps;
-    const uint32_t npairs = ms >> 1;  // wave-uniform pair budget
-    uint32_t it = npairs << 1;        // per lane: steps before the stopping pair (budget exit: all pairs)
-    bool above = u > su;
-    float bu = u, bb = ub, tu = u, tb = ub;
-    for (uint32_t q = 0;;) {
-        if (q >= npairs) break;
-        {
-            rk4_step(u, ub, k.step, k.hh, k.hh2, k.hhh, k.h6, k.h2_6, c, &tu, &tb);
-            const bool a1 = tu > su;
-            const bool s1 = (a1 != above) | !(tu >= bd) | ((tu > hu) & (tb > 0.0f));
-            rk4_step(tu, tb, k.step, k.hh, k.hh2, k.hhh, k.h6, k.h2_6, c, &bu, &bb);
-            const bool a2 = bu > su;
-            const bool s2 = (a2 != a1) | !(bu >= bd) | ((bu > hu) & (bb > 0.0f));
-            if (s1 | s2) {
-                it = q << 1;
-                break;
-            }
-            above = a2;
-        }
-        if (++q >= npairs) break;
-        {
-            rk4_step(bu, bb, k.step, k.hh, k.hh2, k.hhh, k.h6, k.h2_6, c, &tu, &tb);
-            const bool a1 = tu > su;
-            const bool s1 = (a1 != above) | !(tu >= bd) | ((tu > hu) & (tb > 0.0f));
-            rk4_step(tu, tb, k.step, k.hh, k.hh2, k.hhh, k.h6, k.h2_6, c, &u, &ub);
-            const bool a2 = u > su;
-            const bool s2 = (a2 != a1) | !(u >= bd) | ((u > hu) & (ub > 0.0f));
-            if (s1 | s2) {
-                it = q << 1;
-                break;
-            }
-            above = a2;
-        }
-        ++q;
-    }
-    // Opaque copies: the flags below are recomputed from the state rather
-    // than carried out of the loop as lane masks.
-    GEO_OPAQUE(u);
-    GEO_OPAQUE(ub);
-    GEO_OPAQUE(bu);
-    GEO_OPAQUE(bb);
-    GEO_OPAQUE(tu);
-    GEO_OPAQUE(tb);
-    GEO_OPAQUE(it);
-    // the last pair started from A after an even number of pairs, else from B
-    const bool odd = ((it >> 1) & 1u) != 0u;
-    const float s0u = odd ? bu : u, s0b = odd ? bb : ub;  // pair start / current state
-    const float e0u = odd ? u : bu, e0b = odd ? ub : bb;  // pair end
-    float ou, oub, nu, nub;
-    if (it + 2u <= ms) {
-        // stopped inside the pair at steps it+1 or it+2
-        const bool s1 = ((tu > su) != (s0u > su)) | !(tu >= bd) | ((tu > hu) & (tb > 0.0f));
-        if (s1) {
-            ou = s0u; oub = s0b; nu = tu; nub = tb; it += 1u;
-        } else {
-            ou = tu; oub = tb; nu = e0u; nub = e0b; it += 2u;
-        }
-    } else {
-        // budget exit: at most one step left
-        ou = s0u; oub = s0b; nu = s0u; nub = s0b;
-        if (it < ms) {
-            rk4_step(s0u, s0b, k.step, k.hh, k.hh2, k.hhh, k.h6, k.h2_6, c, &nu, &nub);
-            it += 1u;
-        }
-    }
-    *steps = it;
-    if ((nu > su) == (ou > su)) return kNoValue;  // stopped without a crossing
-    u = ou;
-    ub = oub;
-    return newton_angle(k, u, ub, nu, nub, it);
+        if ((nu > SU) == (ou > SU)) return kNoValue;  // stopped without a crossing
+        return newton_angle<KIND>(k, ou, oub, nu, nub, it);
     }
 }
 
 #ifndef GEO_LOOP_VARIANT
 #define GEO_LOOP_VARIANT 1  // fastest on gfx950 (tools/ubench/loop_ab.hip)
 #endif
+// Runtime-dispatched form (host tests); the kernel instantiates per kind.
 GEO_HD float geodesic_angle(const PixelConsts& k, float st, float ct, uint32_t* steps) {
-    return geodesic_angle_v<GEO_LOOP_VARIANT>(k, st, ct, steps);
+    switch (geodesic_kind(k)) {
+        case kCurvedOut: return geodesic_angle_v<GEO_LOOP_VARIANT, kCurvedOut>(k, st, ct, steps);
+        case kCurvedIn: return geodesic_angle_v<GEO_LOOP_VARIANT, kCurvedIn>(k, st, ct, steps);
+        default: return geodesic_angle_v<GEO_LOOP_VARIANT, kFlat>(k, st, ct, steps);
+    }
 }
 
 // 3x3 part of a column-major mat4 times v (w = 0).

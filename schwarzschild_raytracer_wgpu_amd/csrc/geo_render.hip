@@ -26,8 +26,9 @@ namespace {
 constexpr int kTileW = 8;   // a wave64 covers an 8x8 pixel square (fewest divergent
 constexpr int kTileH = 32;  // steps per wave; tools/ubench/loop_ab.hip), a block 8x32
 constexpr int kBlock = kTileW * kTileH;  // 256 threads = 4 waves
+constexpr int kWaveRows = 64 / kTileW;   // rows covered by one wave
 constexpr uint32_t kMaxFan = 4096;       // LDS fan capacity (16 KiB)
-constexpr int kStepSlots = 64;           // sharded step counters
+constexpr int kStepSlots = 256;          // sharded step counters (one per 128-B line)
 constexpr int kSlotStride = 16;          // u64 per slot = 128 B (own cache line)
 
 struct RenderArgs {
@@ -48,10 +49,23 @@ struct RenderArgs {
     unsigned long long* step_slots;
 };
 
-template <int MODE>
+// MODE: GEO_MODE_DIRECT / GEO_MODE_FAN; KIND: geo::kCurvedOut/kCurvedIn/kFlat
+// (frame-uniform integration kind, geo::geodesic_kind; ignored in fan mode).
+// Sum of v over the 64 lanes of a fully active wave (DPP inclusive scan:
+// row_shr 1/2/4/8 within rows of 16, then row_bcast 15/31; lane 63 holds it).
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);  // row_shr:1
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);  // row_shr:2
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);  // row_shr:4
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);  // row_shr:8
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);  // row_bcast:15
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);  // row_bcast:31
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+
+template <int MODE, int KIND>
 __global__ __launch_bounds__(kBlock) void geo_render_kernel(const RenderArgs a) {
     __shared__ float s_fan[MODE == GEO_MODE_FAN ? kMaxFan : 1];
-    __shared__ unsigned long long s_red[kBlock / 64];
     if constexpr (MODE == GEO_MODE_FAN) {
         for (uint32_t i = threadIdx.x; i < a.n_fan; i += kBlock) s_fan[i] = a.fan[i];
         __syncthreads();
@@ -60,8 +74,12 @@ __global__ __launch_bounds__(kBlock) void geo_render_kernel(const RenderArgs a) 
     const uint32_t ty = blockIdx.x / a.tiles_x;
     const uint32_t px = tx * kTileW + (threadIdx.x % kTileW);
     const uint32_t ly = ty * kTileH + (threadIdx.x / kTileW);
+    // local row -> frame row.  band_rows % 8 == 0 (checked on the host) keeps
+    // each 8-row wave inside one band, so the division is wave-uniform (SALU).
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x) >> 6;
+    const uint32_t wl0 = ty * kTileH + wave * kWaveRows;
+    const uint32_t py = a.row0 + (wl0 / a.band_rows) * a.band_stride + (wl0 % a.band_rows) + (ly - wl0);
     uint32_t steps = 0;
-    const uint32_t py = a.row0 + (ly / a.band_rows) * a.band_stride + (ly % a.band_rows);
     if (px < a.width && ly < a.nrows && py < a.height) {
         float c2x, c2y, c2z;
         geo::pixel_central_dir(a.frame.display_to_movement, a.frame.movement_to_central,
@@ -73,7 +91,7 @@ __global__ __launch_bounds__(kBlock) void geo_render_kernel(const RenderArgs a) 
         if constexpr (MODE == GEO_MODE_FAN) {
             lam = geo::fan_lerp(s_fan, a.n_fan, st);
         } else {
-            lam = geo::kPi2 - geo::geodesic_angle(a.k, st, ct, &steps);
+            lam = geo::kPi2 - geo::geodesic_angle_v<GEO_LOOP_VARIANT, KIND>(a.k, st, ct, &steps);
         }
         const bool bh = lam < geo::kBlackHoleLambda;
         float U, V;
@@ -90,27 +108,30 @@ __global__ __launch_bounds__(kBlock) void geo_render_kernel(const RenderArgs a) 
     }
     if constexpr (MODE == GEO_MODE_DIRECT) {
         if (a.step_slots) {
-            unsigned long long s = steps;
-            for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
-            if ((threadIdx.x & 63) == 0) s_red[threadIdx.x >> 6] = s;
-            __syncthreads();
-            if (threadIdx.x == 0) {
-                const unsigned long long t = s_red[0] + s_red[1] + s_red[2] + s_red[3];
-                if (t) atomicAdd(&a.step_slots[(blockIdx.x % kStepSlots) * kSlotStride], t);
-            }
+            // One atomic per wave (all 64 lanes active here; a wave's sum fits
+            // u32: 64 x 2^20 steps at most) into one of kStepSlots sharded
+            // slots.  No block barrier, so a wave that finishes early frees
+            // its slot at once.
+            const uint32_t total = wave_sum_u32(steps);
+            const uint32_t slot = (blockIdx.x * (kBlock / 64) + wave) % kStepSlots;
+            if ((threadIdx.x & 63) == 0 && total)
+                atomicAdd(&a.step_slots[slot * kSlotStride], (unsigned long long)total);
         }
     }
 }
 
-__global__ void geo_steps_finalize(unsigned long long* slots, unsigned long long* total) {
-    __shared__ unsigned long long s[kStepSlots];
+__global__ __launch_bounds__(kStepSlots) void geo_steps_finalize(unsigned long long* slots,
+                                                                  unsigned long long* total) {
+    __shared__ unsigned long long s[kStepSlots / 64];
     const int i = threadIdx.x;
-    s[i] = slots[i * kSlotStride];
+    unsigned long long v = slots[i * kSlotStride];
     slots[i * kSlotStride] = 0;
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    if ((i & 63) == 0) s[i >> 6] = v;
     __syncthreads();
     if (i == 0) {
         unsigned long long t = 0;
-        for (int j = 0; j < kStepSlots; ++j) t += s[j];
+        for (int j = 0; j < kStepSlots / 64; ++j) t += s[j];
         *total += t;
     }
 }
@@ -230,7 +251,6 @@ __global__ void geo_fan_kernel(double sphere_r, double schwarz_r, uint32_t max_i
 struct geo_ctx {
     int device;
     int num_cus;
-    uint32_t launch_blocks;
     uint32_t* sky;
     uint32_t sky_w, sky_h;
     float* fan;
@@ -286,7 +306,6 @@ int geo_ctx_create(int device, geo_ctx** out) {
         return GEO_EHIP;
     }
     c->num_cus = prop.multiProcessorCount;
-    c->launch_blocks = 0;
     if (hipMalloc(&c->step_slots, sizeof(unsigned long long) * kStepSlots * kSlotStride) != hipSuccess) {
         delete c;
         return GEO_ENOMEM;
@@ -370,18 +389,15 @@ int geo_solve_ray_fan(geo_ctx* c, double sphere_r, double schwarz_r, uint32_t ma
     return GEO_OK;
 }
 
-int geo_set_launch_blocks(geo_ctx* c, uint32_t blocks) {
-    if (!c) return GEO_EINVAL;
-    c->launch_blocks = blocks;
-    return GEO_OK;
-}
-
 static int render_impl(geo_ctx* c, const geo_frame* frame, const geo_scene* scene, uint32_t width,
                        uint32_t height, uint32_t row0, uint32_t nrows, uint32_t band_rows,
                        uint32_t band_stride, uint8_t* out_rgba8, uint8_t* out_mask, float* out_uv,
                        uint32_t* out_steps, unsigned long long* steps_total, void* stream) {
     if (scene->mode != GEO_MODE_DIRECT && scene->mode != GEO_MODE_FAN) return GEO_EINVAL;
-    if (scene->flags != 0 || scene->reserved != 0) return GEO_EINVAL;
+    if ((scene->flags & ~GEO_FLAG_DEFER_STEPS) != 0 || scene->reserved != 0) return GEO_EINVAL;
+    const bool defer = (scene->flags & GEO_FLAG_DEFER_STEPS) != 0;
+    if (scene->max_steps > (1u << 24)) return GEO_EINVAL;  // a wave's step sum must fit u32
+    if (defer && steps_total) return GEO_EINVAL;
     if (!c->sky) return GEO_ESTATE;
     if (scene->mode == GEO_MODE_FAN && (!c->fan || c->n_fan < 2)) return GEO_ESTATE;
     // bound > 0 (escape test folding, geo_pixel.h) needs r_obs > 0 and sphere_r > 0
@@ -413,13 +429,23 @@ static int render_impl(geo_ctx* c, const geo_frame* frame, const geo_scene* scen
     a.out_mask = out_mask;
     a.out_uv = reinterpret_cast<float2*>(out_uv);
     a.out_steps = out_steps;
-    a.step_slots = steps_total ? c->step_slots : nullptr;
+    a.step_slots = (steps_total || defer) ? c->step_slots : nullptr;
     hipStream_t s = (hipStream_t)stream;
     const dim3 grid(a.tiles_x * tiles_y);
-    if (scene->mode == GEO_MODE_FAN)
-        hipLaunchKernelGGL(geo_render_kernel<GEO_MODE_FAN>, grid, dim3(kBlock), 0, s, a);
-    else
-        hipLaunchKernelGGL(geo_render_kernel<GEO_MODE_DIRECT>, grid, dim3(kBlock), 0, s, a);
+    if (scene->mode == GEO_MODE_FAN) {
+        hipLaunchKernelGGL((geo_render_kernel<GEO_MODE_FAN, geo::kCurvedOut>), grid, dim3(kBlock), 0, s, a);
+    } else {
+        switch (geo::geodesic_kind(a.k)) {
+            case geo::kCurvedOut:
+                hipLaunchKernelGGL((geo_render_kernel<GEO_MODE_DIRECT, geo::kCurvedOut>), grid, dim3(kBlock), 0, s, a);
+                break;
+            case geo::kCurvedIn:
+                hipLaunchKernelGGL((geo_render_kernel<GEO_MODE_DIRECT, geo::kCurvedIn>), grid, dim3(kBlock), 0, s, a);
+                break;
+            default:
+                hipLaunchKernelGGL((geo_render_kernel<GEO_MODE_DIRECT, geo::kFlat>), grid, dim3(kBlock), 0, s, a);
+        }
+    }
     if (hipGetLastError() != hipSuccess) return GEO_EHIP;
     if (steps_total && scene->mode == GEO_MODE_DIRECT) {
         hipLaunchKernelGGL(geo_steps_finalize, dim3(1), dim3(kStepSlots), 0, s, c->step_slots,
@@ -427,6 +453,15 @@ static int render_impl(geo_ctx* c, const geo_frame* frame, const geo_scene* scen
         if (hipGetLastError() != hipSuccess) return GEO_EHIP;
     }
     return GEO_OK;
+}
+
+int geo_steps_flush(geo_ctx* c, unsigned long long* steps_total, void* stream) {
+    if (!c || !steps_total) return GEO_EINVAL;
+    DeviceGuard g(c->device);
+    if (!g.ok) return GEO_EHIP;
+    hipLaunchKernelGGL(geo_steps_finalize, dim3(1), dim3(kStepSlots), 0, (hipStream_t)stream, c->step_slots,
+                       steps_total);
+    return hipGetLastError() == hipSuccess ? GEO_OK : GEO_EHIP;
 }
 
 int geo_render_rows(geo_ctx* c, const geo_frame* frame, const geo_scene* scene, uint32_t width,
@@ -437,7 +472,8 @@ int geo_render_rows(geo_ctx* c, const geo_frame* frame, const geo_scene* scene, 
         return GEO_EINVAL;
     if ((uint64_t)row0 + nrows > height || width > (1u << 20) || height > (1u << 20))
         return GEO_EINVAL;
-    return render_impl(c, frame, scene, width, height, row0, nrows, nrows, nrows, out_rgba8, out_mask,
+    // one band covering every row (band_rows >= nrows, a multiple of 8)
+    return render_impl(c, frame, scene, width, height, row0, nrows, 1u << 21, 1u << 21, out_rgba8, out_mask,
                        out_uv, out_steps, steps_total, stream);
 }
 
@@ -446,7 +482,7 @@ int geo_render_bands(geo_ctx* c, const geo_frame* frame, const geo_scene* scene,
                      uint32_t nbands, uint8_t* out_rgba8, uint8_t* out_mask, float* out_uv,
                      uint32_t* out_steps, unsigned long long* steps_total, void* stream) {
     if (!c || !frame || !scene || !out_rgba8 || width == 0 || height == 0 || band_rows == 0 ||
-        nbands == 0 || band_step == 0)
+        nbands == 0 || band_step == 0 || band_rows % kWaveRows != 0)
         return GEO_EINVAL;
     if (width > (1u << 20) || height > (1u << 20)) return GEO_EINVAL;
     const uint64_t first = (uint64_t)band0 * band_rows;

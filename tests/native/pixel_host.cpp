@@ -7,6 +7,15 @@
 #include "../../include/geo/geo.h"
 #include "../../schwarzschild_raytracer_wgpu_amd/csrc/geo_pixel.h"
 
+template <int LOOP>
+static float geo_v(const geo::PixelConsts& k, float st, float ct, uint32_t* n) {
+    switch (geo::geodesic_kind(k)) {
+        case geo::kCurvedOut: return geo::geodesic_angle_v<LOOP, geo::kCurvedOut>(k, st, ct, n);
+        case geo::kCurvedIn: return geo::geodesic_angle_v<LOOP, geo::kCurvedIn>(k, st, ct, n);
+        default: return geo::geodesic_angle_v<LOOP, geo::kFlat>(k, st, ct, n);
+    }
+}
+
 extern "C" int host_render(const geo_frame* f, const geo_scene* s, const float* fan, uint32_t n_fan,
                            const uint32_t* sky, uint32_t sw, uint32_t sh, uint32_t width, uint32_t height,
                            uint32_t row0, uint32_t nrows, uint32_t* rgba, uint8_t* mask, float* uv,
@@ -26,9 +35,7 @@ extern "C" int host_render(const geo_frame* f, const geo_scene* s, const float* 
             if (s->mode == GEO_MODE_FAN)
                 lam = geo::fan_lerp(fan, n_fan, st);
             else
-                lam = geo::kPi2 - (variant == 0   ? geo::geodesic_angle_v<0>(k, st, ct, &n)
-                                   : variant == 1 ? geo::geodesic_angle_v<1>(k, st, ct, &n)
-                                                  : geo::geodesic_angle_v<2>(k, st, ct, &n));
+                lam = geo::kPi2 - (variant == 0 ? geo_v<0>(k, st, ct, &n) : geo_v<1>(k, st, ct, &n));
             const bool bh = lam < geo::kBlackHoleLambda;
             float U, V;
             geo::sky_uv(f->central_to_uv, c2x, c2y, ct, lam, &U, &V);

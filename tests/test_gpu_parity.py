@@ -132,6 +132,38 @@ def test_row_blocks_compose_full_frame(geo, torch_mod):
     assert sum(p["total"] for p in parts) == full["total"]
 
 
+def test_render_bands_interleaved(geo, torch_mod):
+    """geo_render_bands for 3 ranks x 8-row bands == the full frame's rows."""
+    from schwarzschild_raytracer_wgpu_amd.dist import BandLayout
+    from schwarzschild_raytracer_wgpu_amd.scenes import make_sky
+
+    w, h, B, world = 120, 101, 8, 3
+    sky = make_sky("equirect", (256, 128))
+    frame, scene = default_frame(w, h), default_scene(2048)
+    ctx = make_ctx(geo, sky)
+    full = render(geo, torch_mod, ctx, frame, scene, w, h)
+    dev = torch_mod.device("cuda:0")
+    tot = 0
+    for r in range(world):
+        L = BandLayout(h, B, world, r)
+        n = L.nb_mine * B * w
+        rgba = torch_mod.zeros(n * 4, dtype=torch_mod.uint8, device=dev)
+        steps = torch_mod.zeros(n, dtype=torch_mod.int32, device=dev)
+        ctr = torch_mod.zeros(1, dtype=torch_mod.int64, device=dev)
+        ctx.render_bands(frame, scene, w, h, B, r, world, L.nb_mine, rgba, out_steps=steps, steps_total=ctr)
+        torch_mod.cuda.synchronize()
+        rgba = rgba.cpu().numpy().reshape(-1, w, 4)
+        steps = steps.cpu().numpy().view(np.uint32).reshape(-1, w)
+        for i, fr in enumerate(L.local_to_frame_rows()):
+            if fr >= 0:
+                assert np.array_equal(rgba[i], full["rgba"][fr]) and np.array_equal(steps[i], full["steps"][fr])
+        tot += int(ctr.item())
+    assert tot == full["total"]
+    with pytest.raises(geo.GeoError):  # band_rows must be a multiple of 8
+        ctx.render_bands(frame, scene, w, h, 12, 0, 1, 2, torch_mod.zeros(24 * w * 4, dtype=torch_mod.uint8,
+                                                                         device=dev))
+
+
 def test_fan_kernel_matches_oracle(geo, torch_mod):
     ctx = geo.Context(0)
     for args in [(500.0, 10.0, 1000, math.pi / 100, 400, math.sqrt(626.0)),

@@ -44,7 +44,8 @@ def parse():
     p.add_argument("--band-rows", type=int, default=8)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-threads", type=int, default=16)
-    p.add_argument("--cpu-row-step", type=int, default=4)
+    p.add_argument("--cpu-row-step", type=int, default=1)
+    p.add_argument("--cpu-seconds", type=float, default=1.0)
     p.add_argument("--mode", default="direct", choices=["direct", "fan"])
     p.add_argument("--check-frame", action="store_true",
                    help="rank 0 checks the assembled frame against a single-launch full frame")
@@ -217,7 +218,7 @@ def main():
             "peak": PEAK_FP32_TFLOPS,
             "unit": "TFLOP/s",
             "frac": achieved_tflops / PEAK_FP32_TFLOPS,
-            "traffic": None,
+            "traffic": pmc_traffic(args.config, args.mode),
             "kernel": "geo_render_kernel<0>",
             "algorithmic_flops_per_launch": FLOPS_PER_EVAL * evals_per_launch,
             "evals_per_launch": evals_per_launch,
@@ -230,25 +231,49 @@ def main():
         dist.destroy_process_group()
 
 
+def pmc_traffic(config, mode):
+    """HBM bytes per launch of the render kernel from the committed rocprofv3
+    PMC summary of this workload (profiles/*_<config>_pmc.json, made by
+    tools/gpu_pmc.sh + tools/pmc_to_profile.py), or None."""
+    import glob
+
+    if mode != "direct":
+        return None
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_{config}_pmc.json")))
+    if not files:
+        return None
+    with open(files[-1]) as f:
+        return json.load(f)["derived"]["traffic_bytes"]
+
+
 def cpu_baseline(frame, scene, sky, W, H, args):
     """The oracle's scalar f32 restatement of the same per-pixel integrator
-    (oracle/geo_oracle.c), pthreads over rows, on every k-th row of the frame."""
+    (oracle/geo_oracle.c: pthreads over rows, one pixel per thread-iteration),
+    on whole frames of the same workload until >= --cpu-seconds of wall time."""
     import oracle as O
 
     threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
     k = args.cpu_row_step
     nrows = (H + k - 1) // k
+    steps = 0
+    frames = 0
     t0 = time.perf_counter()
-    r = O.render_f32(frame, scene, sky, W, H, row0=0, nrows=nrows, row_step=k, threads=threads,
-                     want_uv=False, want_steps=False)
-    dt = time.perf_counter() - t0
+    while True:
+        r = O.render_f32(frame, scene, sky, W, H, row0=0, nrows=nrows, row_step=k, threads=threads,
+                         want_uv=False, want_steps=False)
+        steps += r["steps_total"]
+        frames += 1
+        dt = time.perf_counter() - t0
+        if dt >= args.cpu_seconds:
+            break
+    what = "full" if k == 1 else f"every {k}th row of the"
     return {
-        "value": r["steps_total"] / dt,
+        "value": steps / dt,
         "unit": "geodesic-steps·pixels/s",
         "cores": threads,
         "kind": "port",
-        "sample": f"every {k}th row of the same {W}x{H} frame ({nrows} rows, {nrows * W} pixels, "
-                  f"{r['steps_total']} RK4 steps) in {dt:.2f} s on {threads} threads",
+        "sample": f"{frames} x {what} {W}x{H} frame ({nrows * W} pixels, {steps // frames} RK4 steps each) "
+                  f"in {dt:.2f} s wall on {threads} threads",
         "seconds": dt,
     }
 

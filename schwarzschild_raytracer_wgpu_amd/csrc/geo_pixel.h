@@ -53,12 +53,33 @@ struct PixelConsts {
     bool pf_always, pf_falling, pf_outgoing, pf_eneg, pf_barrier;
     // the integrator's scaled state U = scale*u (scale = 3 rs/2, or 1 for rs = 0)
     float scale, U0, SU, BD, HU;
+    float SUp;  // next float above SU: (U > SU) == (U >= SUp) for every float U
 };
 
 // Integration kinds (frame-uniform, chosen on the host):
 constexpr int kCurvedOut = 0;  // rs > 0, observer outside the horizon (r > rs)
 constexpr int kCurvedIn = 1;   // rs > 0, observer on/inside the horizon
 constexpr int kFlat = 2;       // rs = 0: straight lines
+
+// Next float above a positive finite x.
+GEO_HD float next_up_(float x) {
+    uint32_t b;
+    __builtin_memcpy(&b, &x, 4);
+    b += 1u;
+    __builtin_memcpy(&x, &b, 4);
+    return x;
+}
+
+// median of three; for lo <= hi: med3(x, lo, hi) == x  <=>  lo <= x <= hi, and
+// a NaN x never compares equal.
+GEO_HD float med3_(float x, float lo, float hi) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_fmed3f(x, lo, hi);
+#else
+    const float m = x > lo ? x : lo;  // NaN x -> lo
+    return m < hi ? m : hi;
+#endif
+}
 
 GEO_HD PixelConsts make_consts(float rs, float sphere_r, float r, float step, uint32_t max_steps) {
     PixelConsts k;
@@ -116,6 +137,7 @@ GEO_HD PixelConsts make_consts(float rs, float sphere_r, float r, float step, ui
     k.SU = k.scale * k.sphere_u;
     k.BD = k.scale * k.bound;
     k.HU = k.scale * k.schwarz_u;
+    k.SUp = next_up_(k.SU);
     return k;
 }
 
@@ -200,9 +222,8 @@ GEO_HD float newton_angle(const PixelConsts& k, float U, float UB, float NU, flo
 
 // Traveled angle of the ray at angle theta to the black hole, or kNoValue.
 // (st, ct) = (sin theta, cos theta >= 0) of the central-frame direction;
-// *steps = executed main-loop RK4 steps.  LOOP selects the loop structure
-// (0: one step per exit test, 1: two; tools/ubench/loop_ab.hip), KIND the
-// integration kind (geodesic_kind).
+// *steps = executed main-loop RK4 steps.  LOOP = RK4 steps per exit test
+// (tools/ubench/loop_ab.hip), KIND the integration kind (geodesic_kind).
 template <int LOOP, int KIND>
 GEO_HD float geodesic_angle_v(const PixelConsts& k, float st, float ct, uint32_t* steps) {
     *steps = 0;
@@ -243,81 +264,98 @@ GEO_HD float geodesic_angle_v(const PixelConsts& k, float st, float ct, uint32_t
     // `!(NU >= BD)` is (NU < BD) or NaN and, with BD > 0, also covers the
     // `u > 0` test; the budget (:135) is wave-uniform.  Results equal the
     // literal loop's (the oracle keeps that form; tests require bit equality).
-    if constexpr (LOOP == 0) {
-        uint32_t it = 0;
-        bool above = U > SU;
-        bool cross;
-        float NU, NUB;
-        for (;;) {
-            rk4_step<KIND>(U, UB, h, hh, hh2, hhh, h6, h2_6, &NU, &NUB);
-            ++it;
-            const bool nabove = NU > SU;
-            cross = nabove != above;
-            if (cross | !(NU >= BD) | horizon_<KIND>(NU, NUB, HU) | (it >= k.max_steps)) break;
-            U = NU;
-            UB = NUB;
-            above = nabove;
-        }
-        *steps = it;
-        if (!cross) return kNoValue;
-        return newton_angle<KIND>(k, U, UB, NU, NUB, it);
-    } else {
-        // TWO RK4 steps per exit test; a lane whose first step stops discards
-        // the second.  The pair budget is a wave-uniform loop bound.
-        const uint32_t ms = k.max_steps;
-        const uint32_t npairs = ms >> 1;
-        uint32_t it = npairs << 1;  // per lane: steps before the stopping pair (budget: all)
-        bool above = U > SU;
-        float n1u = U, n1b = UB, n2u = U, n2b = UB;
-        for (uint32_t q = 0; q < npairs; ++q) {
-            rk4_step<KIND>(U, UB, h, hh, hh2, hhh, h6, h2_6, &n1u, &n1b);
-            const bool a1 = n1u > SU;
-            const bool s1 = (a1 != above) | !(n1u >= BD) | horizon_<KIND>(n1u, n1b, HU);
-            rk4_step<KIND>(n1u, n1b, h, hh, hh2, hhh, h6, h2_6, &n2u, &n2b);
-            const bool a2 = n2u > SU;
-            const bool s2 = (a2 != a1) | !(n2u >= BD) | horizon_<KIND>(n2u, n2b, HU);
-            if (s1 | s2) {
-                it = q << 1;
-                break;
-            }
-            U = n2u;
-            UB = n2b;
-            above = a2;
-        }
-        // Opaque copies: the flags below are recomputed from the state rather
-        // than carried out of the loop as lane masks (fewer SALU per pair).
-        GEO_OPAQUE(U);
-        GEO_OPAQUE(UB);
-        GEO_OPAQUE(n1u);
-        GEO_OPAQUE(n1b);
-        GEO_OPAQUE(n2u);
-        GEO_OPAQUE(n2b);
-        GEO_OPAQUE(it);
-        float ou, oub, nu, nub;
-        if (it + 2u <= ms) {
-            // stopped inside the pair, at step it+1 or it+2
-            const bool s1 = ((n1u > SU) != (U > SU)) | !(n1u >= BD) | horizon_<KIND>(n1u, n1b, HU);
-            if (s1) {
-                ou = U; oub = UB; nu = n1u; nub = n1b; it += 1u;
-            } else {
-                ou = n1u; oub = n1b; nu = n2u; nub = n2b; it += 2u;
-            }
-        } else {
-            // budget exit: at most one step left
-            ou = U; oub = UB; nu = U; nub = UB;
-            if (it < ms) {
-                rk4_step<KIND>(U, UB, h, hh, hh2, hhh, h6, h2_6, &nu, &nub);
-                it += 1u;
-            }
-        }
-        *steps = it;
-        if ((nu > SU) == (ou > SU)) return kNoValue;  // stopped without a crossing
-        return newton_angle<KIND>(k, ou, oub, nu, nub, it);
+    // Stop flag of one step (reference order: crossing :150, escape :184,
+    // loop test :134-135).  The loop ends at the first crossing, so "above
+    // the sphere" (U > SU) is fixed for the whole integration and frame-
+    // uniform (U0 vs SU).  Outside the horizon the flag is then ONE interval
+    // test (v_med3_f32 + compare):
+    //   inside the sphere (U0 > SU): stop <=> NU not in [SU+, HU]
+    //       (crossing outward | horizon; escape NU < BD < SU is a crossing too)
+    //   outside (U0 <= SU):          stop <=> NU not in [BD, SU]
+    //       (crossing inward | escape; the horizon HU > SU is a crossing too)
+    // NaN always stops.  Inside the horizon the general test is kept.
+    const bool above0 = k.U0 > SU;
+    const float lo = above0 ? k.SUp : BD;
+    const float hi = above0 ? HU : SU;
+    auto stop_at = [&](float NU, float NUB) -> bool {
+        if constexpr (KIND == kCurvedIn)
+            return ((NU > SU) != above0) | !(NU >= BD) | ((NU > HU) & (NUB > 0.0f));
+        else
+            return med3_(NU, lo, hi) != NU;
+    };
+    // LOOP = G: G RK4 steps per exit test (the budget in whole groups is a
+    // wave-uniform bound); a lane that stops inside a group discards the rest
+    // of it.  Results equal the literal loop's (the oracle keeps that form;
+    // tests require bit equality).
+    constexpr int G = LOOP;
+    const uint32_t ms = k.max_steps;
+    const uint32_t ngroups = ms / (uint32_t)G;
+    uint32_t it = ngroups * (uint32_t)G;  // per lane: steps before its stopping group (budget: all)
+    float su_[G + 1], sb_[G + 1];
+    su_[0] = U;
+    sb_[0] = UB;
+#pragma unroll
+    for (int j = 1; j <= G; ++j) {
+        su_[j] = U;
+        sb_[j] = UB;
     }
+    for (uint32_t q = 0; q < ngroups; ++q) {
+        bool stop = false;
+#pragma unroll
+        for (int j = 0; j < G; ++j) {
+            rk4_step<KIND>(su_[j], sb_[j], h, hh, hh2, hhh, h6, h2_6, &su_[j + 1], &sb_[j + 1]);
+            stop = stop | stop_at(su_[j + 1], sb_[j + 1]);
+        }
+        if (stop) {
+            it = q * (uint32_t)G;
+            break;
+        }
+        su_[0] = su_[G];
+        sb_[0] = sb_[G];
+    }
+    // Opaque copies: the per-step flags are recomputed from the state rather
+    // than carried out of the loop as lane masks.
+#pragma unroll
+    for (int j = 0; j <= G; ++j) {
+        GEO_OPAQUE(su_[j]);
+        GEO_OPAQUE(sb_[j]);
+    }
+    GEO_OPAQUE(it);
+    float ou = su_[0], oub = sb_[0], nu = su_[0], nub = sb_[0];
+    if (it + (uint32_t)G <= ms) {
+        // stopped inside the group: the first step j whose flag holds
+        bool found = false;
+#pragma unroll
+        for (int j = 0; j < G; ++j) {
+            const bool sj = !found && stop_at(su_[j + 1], sb_[j + 1]);
+            if (sj) {
+                ou = su_[j]; oub = sb_[j]; nu = su_[j + 1]; nub = sb_[j + 1];
+                it += (uint32_t)j + 1u;
+            }
+            found = found | sj;
+        }
+    } else {
+        // budget exit: fewer than G steps left, one test per step
+        float cu = su_[0], cb = sb_[0];
+        for (uint32_t r = it; r < ms; ++r) {
+            rk4_step<KIND>(cu, cb, h, hh, hh2, hhh, h6, h2_6, &nu, &nub);
+            ou = cu;
+            oub = cb;
+            ++it;
+            if (stop_at(nu, nub)) break;
+            cu = nu;
+            cb = nub;
+            ou = nu;  // no crossing if the budget ends here
+            oub = nub;
+        }
+    }
+    *steps = it;
+    if ((nu > SU) == (ou > SU)) return kNoValue;  // stopped without a crossing
+    return newton_angle<KIND>(k, ou, oub, nu, nub, it);
 }
 
 #ifndef GEO_LOOP_VARIANT
-#define GEO_LOOP_VARIANT 1  // fastest on gfx950 (tools/ubench/loop_ab.hip)
+#define GEO_LOOP_VARIANT 4  // RK4 steps per exit test; fastest on gfx950 (tools/ubench/loop_ab.hip)
 #endif
 // Runtime-dispatched form (host tests); the kernel instantiates per kind.
 GEO_HD float geodesic_angle(const PixelConsts& k, float st, float ct, uint32_t* steps) {

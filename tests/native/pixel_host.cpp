@@ -35,7 +35,7 @@ extern "C" int host_render(const geo_frame* f, const geo_scene* s, const float* 
             if (s->mode == GEO_MODE_FAN)
                 lam = geo::fan_lerp(fan, n_fan, st);
             else
-                lam = geo::kPi2 - (variant == 0 ? geo_v<0>(k, st, ct, &n) : geo_v<1>(k, st, ct, &n));
+                lam = geo::kPi2 - (variant == 1 ? geo_v<1>(k, st, ct, &n) : variant == 2 ? geo_v<2>(k, st, ct, &n) : variant == 3 ? geo_v<3>(k, st, ct, &n) : geo_v<4>(k, st, ct, &n));
             const bool bh = lam < geo::kBlackHoleLambda;
             float U, V;
             geo::sky_uv(f->central_to_uv, c2x, c2y, ct, lam, &U, &V);

@@ -64,10 +64,10 @@ CASES = [
 ]
 
 
-@pytest.mark.parametrize("variant", [0, 1])
+@pytest.mark.parametrize("variant", [1, 2, 3, 4])
 @pytest.mark.parametrize("name,w,h,fk,sk", CASES, ids=[c[0] for c in CASES])
 def test_host_header_equals_oracle(host, name, w, h, fk, sk, variant):
-    """Every RK4 loop structure of geo_pixel.h (LOOP 0/1) equals the literal loop."""
+    """Every RK4 loop structure of geo_pixel.h (G = 1..4 steps per exit test) equals the literal loop."""
     sky = make_sky("equirect", (128, 64))
     frame, scene = default_frame(w, h, **fk), default_scene(**sk)
     a = run_host(host, frame, scene, sky, w, h, variant=variant)

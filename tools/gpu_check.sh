@@ -8,7 +8,6 @@ ROOT=$(pwd)
 OUT=$ROOT/gpurun_out
 mkdir -p "$OUT"
 TAG=${1:-r01}
-STEPS=${STEPS:-20}
 
 fatal() { local rc=$1; [ "$rc" -ge 124 ] || [ "$rc" -ge 128 ]; }
 
@@ -20,12 +19,12 @@ timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smo
 rc=$?; echo "smoke rc=$rc"; tail -2 "$OUT/smoke_$TAG.log"
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 
-timeout -k 10 300 python bench.py --steps "$STEPS" > "$OUT/bench_$TAG.json" 2> "$OUT/bench_$TAG.err"
+timeout -k 10 300 python bench.py > "$OUT/bench_$TAG.json" 2> "$OUT/bench_$TAG.err"
 rc=$?; echo "bench rc=$rc"; cat "$OUT/bench_$TAG.json"; tail -3 "$OUT/bench_$TAG.err"
 if [ $rc -ne 0 ]; then exit $rc; fi
 
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$TAG" -o run \
-    -- python3 "$ROOT/bench.py" --steps "$STEPS" --no-cpu-baseline > "$OUT/prof_$TAG.log" 2>&1
+    -- python3 "$ROOT/bench.py" --no-cpu-baseline > "$OUT/prof_$TAG.log" 2>&1
 rc=$?; echo "rocprof rc=$rc"; tail -3 "$OUT/prof_$TAG.log"
 exit $rc

@@ -58,7 +58,10 @@ __global__ __launch_bounds__(256) void kern(const Args a) {
 // flags can never fire: su < 0, bound = -inf, hu = +inf), bounded orbit.
 template <int V>
 __global__ __launch_bounds__(256) void loop_only(geo::PixelConsts k, float* out) {
-    k.SU = -1.0f;
+    // never stops: inside-sphere interval [SU+, HU] = (-inf, inf)
+    k.U0 = 0.1f;  // bounded orbit (U = 1 is the unstable photon-sphere equilibrium)
+    k.SU = -__builtin_inff();
+    k.SUp = -__builtin_inff();
     k.BD = -__builtin_inff();
     k.HU = __builtin_inff();
     k.pf_always = k.pf_eneg = k.pf_barrier = k.pf_falling = k.pf_outgoing = false;
@@ -92,9 +95,9 @@ int main() {
     CK(hipMalloc(&a.slots, 64 * 16 * 8));
     struct Var { const char* name; KFn fn; int tw; };
     Var vars[] = {
-        {"loop0 single-step 16x16", kern<0, 16>, 16}, {"loop1 two-step 16x16", kern<1, 16>, 16},
-        {"loop1 two-step 32x8", kern<1, 32>, 32},
-        {"loop1 two-step 8x32", kern<1, 8>, 8},       {"loop0 single 8x32", kern<0, 8>, 8},
+        {"G=1 8x32", kern<1, 8>, 8}, {"G=2 8x32", kern<2, 8>, 8}, {"G=3 8x32", kern<3, 8>, 8},
+        {"G=4 8x32", kern<4, 8>, 8}, {"G=2 16x16", kern<2, 16>, 16}, {"G=4 16x16", kern<4, 16>, 16},
+        {"G=4 32x8", kern<4, 32>, 32},
     };
     const int NV = sizeof(vars) / sizeof(vars[0]);
     std::vector<uint32_t*> outs(NV);
@@ -132,8 +135,8 @@ int main() {
         float* dummy;
         CK(hipMalloc(&dummy, 1 << 20));
         const int blocks = 256 * 8 * 4;
-        void (*lk[2])(geo::PixelConsts, float*) = {loop_only<0>, loop_only<1>};
-        for (int v = 0; v < 2; ++v) {
+        void (*lk[4])(geo::PixelConsts, float*) = {loop_only<1>, loop_only<2>, loop_only<3>, loop_only<4>};
+        for (int v = 0; v < 4; ++v) {
             std::vector<float> tt;
             for (int r = 0; r < 7; ++r) {
                 hipEventRecord(e0);
@@ -146,7 +149,7 @@ int main() {
             }
             std::sort(tt.begin(), tt.end());
             const double st = 2000.0 * blocks * 256;
-            printf("loop-only LOOP=%d: %.3f ms, %.3e steps/s = %.1f TF(alg 40 flop/step)\n", v, tt[tt.size() / 2],
+            printf("loop-only G=%d: %.3f ms, %.3e steps/s = %.1f TF(alg 40 flop/step)\n", v + 1, tt[tt.size() / 2],
                    st / (tt[tt.size() / 2] * 1e-3), 40.0 * st / (tt[tt.size() / 2] * 1e-3) / 1e12);
         }
     }

@@ -105,7 +105,8 @@ int geo_ctx_create(int device, geo_ctx** out);
 void geo_ctx_destroy(geo_ctx* ctx);
 
 /* Uploads an equirect RGBA8 sky (row-major, w*h*4 bytes, host memory; the
- * bytes are copied, synchronously).  U wraps, V clamps, LOD-0 bilinear. */
+ * bytes are copied, synchronously).  U wraps, V clamps, LOD-0 bilinear with
+ * 8-bit sub-texel weights. */
 int geo_set_sky(geo_ctx* ctx, const uint8_t* rgba8, uint32_t w, uint32_t h);
 
 /* Uploads a ray fan of n >= 2 nodes (host memory, copied synchronously):
@@ -136,7 +137,7 @@ int geo_render_rows(geo_ctx* ctx, const geo_frame* frame, const geo_scene* scene
 
 /* Renders an interleaved set of row bands (balanced multi-GPU sharding): bands
  * band0, band0+band_step, ..., nbands of them, each band_rows tall (a
- * multiple of 8, the pixel rows of one wave); band b
+ * power of two >= 8, the pixel rows of one wave); band b
  * covers rows [b*band_rows, (b+1)*band_rows) clipped to height.  Outputs are
  * packed band after band (nbands*band_rows rows; clipped rows are not
  * written).  geo_render_rows(row0, nrows) is the single-band case. */

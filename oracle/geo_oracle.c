@@ -431,11 +431,9 @@ static inline void m3vf(const float* m, float x, float y, float z, float* o) {
     o[2] = fmaf(m[10], z, fmaf(m[6], y, m[2] * x));
 }
 
-static inline float lerpf(float a, float b, float t) { return fmaf(t, b - a, a); }
-static inline uint32_t u8f(float v) { return (uint32_t)clampf(v + 0.5f, 0.0f, 255.0f); }
 
 static void pixel_f32(const geo_frame* f, const fconsts* k, int mode, const float* fan, uint32_t n_fan,
-                      const uint32_t* sky, uint32_t sw, uint32_t sh, uint32_t width, uint32_t height,
+                      const uint32_t* sky, uint32_t sw, uint32_t sh, int opaque, uint32_t width, uint32_t height,
                       uint32_t px, uint32_t py, uint32_t* rgba, uint8_t* bh_out, float* uv, uint32_t* steps) {
     const float* m0 = f->display_to_movement;
     float nx = ((float)(2u * px + 1u) - (float)width) * (1.0f / (float)width);
@@ -492,11 +490,14 @@ static void pixel_f32(const geo_frame* f, const fconsts* k, int mode, const floa
         *rgba = 0xFF000000u;
         return;
     }
-    /* bilinear LOD-0, U wraps, V clamps; alpha blend over (0,0,0,1) */
+    /* bilinear LOD-0, U wraps, V clamps, 8-bit sub-texel weights; per
+     * channel: horizontal lerp truncated to 8 bits, vertical lerp rounded;
+     * then the alpha blend over (0,0,0,1): round(c*a/255), alpha 255. */
     float x = fmaf(U, (float)sw, -0.5f);
     float y = fmaf(V, (float)sh, -0.5f);
     float fx0 = floorf(x), fy0 = floorf(y);
-    float fx = x - fx0, fy = y - fy0;
+    uint32_t wx = (uint32_t)((x - fx0) * 256.0f);
+    uint32_t wy = (uint32_t)((y - fy0) * 256.0f);
     int ix0 = (int)fx0, iy0 = (int)fy0;
     int w = (int)sw, h = (int)sh;
     if (ix0 < 0) ix0 += w;
@@ -505,18 +506,23 @@ static void pixel_f32(const geo_frame* f, const fconsts* k, int mode, const floa
     int iy1 = iy0 + 1;
     iy0 = iy0 < 0 ? 0 : (iy0 > h - 1 ? h - 1 : iy0);
     iy1 = iy1 < 0 ? 0 : (iy1 > h - 1 ? h - 1 : iy1);
-    uint32_t t00 = sky[(uint32_t)iy0 * sw + (uint32_t)ix0];
-    uint32_t t10 = sky[(uint32_t)iy0 * sw + (uint32_t)ix1];
-    uint32_t t01 = sky[(uint32_t)iy1 * sw + (uint32_t)ix0];
-    uint32_t t11 = sky[(uint32_t)iy1 * sw + (uint32_t)ix1];
-    float cc[4];
+    uint32_t t[4] = {sky[(uint32_t)iy0 * sw + (uint32_t)ix0], sky[(uint32_t)iy0 * sw + (uint32_t)ix1],
+                     sky[(uint32_t)iy1 * sw + (uint32_t)ix0], sky[(uint32_t)iy1 * sw + (uint32_t)ix1]};
+    uint32_t c[4];
     for (int ch = 0; ch < 4; ++ch) {
-        float a = lerpf((float)((t00 >> (8 * ch)) & 255u), (float)((t10 >> (8 * ch)) & 255u), fx);
-        float b = lerpf((float)((t01 >> (8 * ch)) & 255u), (float)((t11 >> (8 * ch)) & 255u), fx);
-        cc[ch] = lerpf(a, b, fy);
+        uint32_t v00 = (t[0] >> (8 * ch)) & 255u, v10 = (t[1] >> (8 * ch)) & 255u;
+        uint32_t v01 = (t[2] >> (8 * ch)) & 255u, v11 = (t[3] >> (8 * ch)) & 255u;
+        uint32_t top = (v00 * (256u - wx) + v10 * wx) >> 8;
+        uint32_t bot = (v01 * (256u - wx) + v11 * wx) >> 8;
+        c[ch] = (top * (256u - wy) + bot * wy + 128u) >> 8;
     }
-    float alpha = cc[3] * (1.0f / 255.0f);
-    *rgba = u8f(cc[0] * alpha) | (u8f(cc[1] * alpha) << 8) | (u8f(cc[2] * alpha) << 16) | (255u << 24);
+    if (!opaque) {
+        for (int ch = 0; ch < 3; ++ch) {
+            uint32_t p = c[ch] * c[3] + 128u;
+            c[ch] = (p + (p >> 8)) >> 8;
+        }
+    }
+    *rgba = c[0] | (c[1] << 8) | (c[2] << 16) | (255u << 24);
 }
 
 typedef struct {
@@ -527,6 +533,7 @@ typedef struct {
     uint32_t n_fan;
     const uint32_t* sky;
     uint32_t sw, sh, width, height, row0, nrows, row_step;
+    int opaque;
     int threads, tid;
     uint8_t* rgba;
     uint8_t* mask;
@@ -546,7 +553,7 @@ static void* job_f32(void* arg) {
             uint32_t rgba, st;
             uint8_t bh;
             float uv[2];
-            pixel_f32(j->f, &j->k, (int)j->s->mode, j->fan, j->n_fan, j->sky, j->sw, j->sh, j->width, j->height,
+            pixel_f32(j->f, &j->k, (int)j->s->mode, j->fan, j->n_fan, j->sky, j->sw, j->sh, j->opaque, j->width, j->height,
                       px, py, &rgba, &bh, uv, &st);
             memcpy(j->rgba + 4 * o, &rgba, 4);
             if (j->mask) j->mask[o] = bh;
@@ -635,6 +642,12 @@ int geo_oracle_render_f32(const geo_frame* f, const geo_scene* s, const float* f
     j.sky = (const uint32_t*)sky;
     j.sw = sky_w;
     j.sh = sky_h;
+    j.opaque = 1;
+    for (size_t i = 0; i < (size_t)sky_w * sky_h; ++i)
+        if (sky[4 * i + 3] != 255u) {
+            j.opaque = 0;
+            break;
+        }
     j.width = width;
     j.height = height;
     j.row0 = row0;

@@ -220,14 +220,12 @@ GEO_HD float newton_angle(const PixelConsts& k, float U, float UB, float NU, flo
     return (float)(it - 1u) * k.step + ns;
 }
 
-// Traveled angle of the ray at angle theta to the black hole, or kNoValue.
-// (st, ct) = (sin theta, cos theta >= 0) of the central-frame direction;
-// *steps = executed main-loop RK4 steps.  LOOP = RK4 steps per exit test
-// (tools/ubench/loop_ab.hip), KIND the integration kind (geodesic_kind).
-template <int LOOP, int KIND>
-GEO_HD float geodesic_angle_v(const PixelConsts& k, float st, float ct, uint32_t* steps) {
-    *steps = 0;
-    // solve_ray_fan per node (sphere_ray_tracer.rs:38-49)
+// Ray set-up of solve_ray_fan + solve_geodesic (sphere_ray_tracer.rs:38-132)
+// for (st, ct) = (sin theta, cos theta >= 0) of the central-frame direction.
+// Returns false with the traveled angle in *early (radial case, pre-filter
+// or failed initial loop test); else the scaled initial state (U, UB).
+GEO_HD bool geodesic_init(const PixelConsts& k, float st, float ct, float* early, float* U0, float* UB0) {
+    // solve_ray_fan per node (:38-49)
     const float rotation = k.r * ct;
     bool falling;
     float energy;
@@ -240,23 +238,40 @@ GEO_HD float geodesic_angle_v(const PixelConsts& k, float st, float ct, uint32_t
     }
     // radial rays (:67-104), frame-uniform table
     if (rotation < 1e-10f) {
-        if (k.radial_by_energy) return energy > 0.0f ? 0.0f : kNoValue;
-        return falling ? k.radial_falling : k.radial_outgoing;
+        *early = k.radial_by_energy ? (energy > 0.0f ? 0.0f : kNoValue)
+                                    : (falling ? k.radial_falling : k.radial_outgoing);
+        return false;
     }
     // 1/b^2 with b = rotation/energy (:61): one division
     const float inv_b2 = (energy * energy) / (rotation * rotation);
     // pre-filters (:106-119), frame-uniform terms precomputed
     if (k.pf_always | (k.pf_eneg & (energy < 0.0f)) | (k.pf_barrier & (inv_b2 < k.barrier_thresh)) |
         (k.pf_falling & falling) | (k.pf_outgoing & !falling)) {
-        return kNoValue;
+        *early = kNoValue;
+        return false;
     }
     // RK4 init (:122-132); the radicand is clamped at 0 (the reference yields
     // NaN there only for |theta| < ~1e-8, never at a fan node).
     float ub = __builtin_sqrtf(fmaxf_(0.0f, inv_b2 - k.h_over_r2));
     if (!falling) ub = -ub;
     // loop test of :134-135 on the initial state (schwarz_u = +inf for rs = 0)
-    if ((k.u0 > k.schwarz_u && ub > 0.0f) || k.max_steps == 0u || !(k.u0 > 0.0f)) return kNoValue;
-    float U = k.U0, UB = k.scale * ub;
+    if ((k.u0 > k.schwarz_u && ub > 0.0f) || k.max_steps == 0u || !(k.u0 > 0.0f)) {
+        *early = kNoValue;
+        return false;
+    }
+    *U0 = k.U0;
+    *UB0 = k.scale * ub;
+    return true;
+}
+
+// Traveled angle of the ray at angle theta to the black hole, or kNoValue.
+// *steps = executed main-loop RK4 steps.  LOOP = RK4 steps per exit test
+// (tools/ubench/loop_ab.hip), KIND the integration kind (geodesic_kind).
+template <int LOOP, int KIND>
+GEO_HD float geodesic_angle_v(const PixelConsts& k, float st, float ct, uint32_t* steps) {
+    *steps = 0;
+    float U, UB, early;
+    if (!geodesic_init(k, st, ct, &early, &U, &UB)) return early;
     const float SU = k.SU, BD = k.BD, HU = k.HU;
     const float h = k.step, hh = k.hh, hh2 = k.hh2, hhh = k.hhh, h6 = k.h6, h2_6 = k.h2_6;
     // Main loop (:134-191), restructured for the wave64 VALU.  Per step the
@@ -438,25 +453,28 @@ GEO_HD void sky_uv(const float* m2, float c2x, float c2y, float rho, float lam, 
     *V = clampf_(v, 0.0f, 1.0f);
 }
 
-GEO_HD float lerpf_(float a, float b, float t) { return fmaf_(t, b - a, a); }
-
-GEO_HD float texel_channel(uint32_t t, int ch) { return (float)((t >> (8 * ch)) & 255u); }
-
-GEO_HD uint32_t to_u8(float v) {
-    v = clampf_(v + 0.5f, 0.0f, 255.0f);
-    return (uint32_t)v;
+// LOD-0 bilinear sample of an RGBA8 equirect (U wraps, V clamps) with 8-bit
+// sub-texel weights, as texture units do, on packed channel pairs
+// (R|B and G|A in the two 16-bit halves of a u32; no field overflows), then
+// the reference's alpha blend over the clear colour (0,0,0,1): rgb*a/255,
+// alpha 1 (pipeline.rs:49, renderer.rs:233-238).  `opaque` (every texel
+// alpha 255, checked on upload) skips the blend, which is exact there.
+GEO_HD uint32_t rb_(uint32_t t) { return t & 0x00FF00FFu; }
+GEO_HD uint32_t ga_(uint32_t t) { return (t >> 8) & 0x00FF00FFu; }
+GEO_HD uint32_t lerp2_(uint32_t a, uint32_t b, uint32_t ia, uint32_t wb) { return a * ia + b * wb; }
+GEO_HD uint32_t blend255_(uint32_t c, uint32_t a) {  // round(c*a/255) for c, a <= 255
+    const uint32_t p = c * a + 128u;
+    return (p + (p >> 8)) >> 8;
 }
 
-// LOD-0 bilinear sample of an RGBA8 equirect (U wraps, V clamps), then the
-// reference's alpha blend over the clear colour (0,0,0,1): rgb*a, alpha 1.
 template <typename Fetch>
-GEO_HD uint32_t sample_sky(Fetch fetch, uint32_t tw, uint32_t th, float U, float V) {
+GEO_HD uint32_t sample_sky(Fetch fetch, uint32_t tw, uint32_t th, bool opaque, float U, float V) {
     const float x = fmaf_(U, (float)tw, -0.5f);
     const float y = fmaf_(V, (float)th, -0.5f);
     const float fx0 = __builtin_floorf(x);
     const float fy0 = __builtin_floorf(y);
-    const float fx = x - fx0;
-    const float fy = y - fy0;
+    const uint32_t wx = (uint32_t)((x - fx0) * 256.0f);  // 0..255
+    const uint32_t wy = (uint32_t)((y - fy0) * 256.0f);
     int ix0 = (int)fx0;
     int iy0 = (int)fy0;
     const int w = (int)tw, h = (int)th;
@@ -466,19 +484,23 @@ GEO_HD uint32_t sample_sky(Fetch fetch, uint32_t tw, uint32_t th, float U, float
     int iy1 = iy0 + 1;
     iy0 = iy0 < 0 ? 0 : (iy0 > h - 1 ? h - 1 : iy0);
     iy1 = iy1 < 0 ? 0 : (iy1 > h - 1 ? h - 1 : iy1);
-    const uint32_t t00 = fetch((uint32_t)iy0 * tw + (uint32_t)ix0);
-    const uint32_t t10 = fetch((uint32_t)iy0 * tw + (uint32_t)ix1);
-    const uint32_t t01 = fetch((uint32_t)iy1 * tw + (uint32_t)ix0);
-    const uint32_t t11 = fetch((uint32_t)iy1 * tw + (uint32_t)ix1);
-    float c[4];
-    for (int ch = 0; ch < 4; ++ch) {
-        const float a = lerpf_(texel_channel(t00, ch), texel_channel(t10, ch), fx);
-        const float b = lerpf_(texel_channel(t01, ch), texel_channel(t11, ch), fx);
-        c[ch] = lerpf_(a, b, fy);
-    }
-    const float alpha = c[3] * (1.0f / 255.0f);
-    return to_u8(c[0] * alpha) | (to_u8(c[1] * alpha) << 8) | (to_u8(c[2] * alpha) << 16) |
-           (255u << 24);
+    const uint32_t r0 = (uint32_t)iy0 * tw, r1 = (uint32_t)iy1 * tw;
+    const uint32_t t00 = fetch(r0 + (uint32_t)ix0);
+    const uint32_t t10 = fetch(r0 + (uint32_t)ix1);
+    const uint32_t t01 = fetch(r1 + (uint32_t)ix0);
+    const uint32_t t11 = fetch(r1 + (uint32_t)ix1);
+    const uint32_t iwx = 256u - wx, iwy = 256u - wy;
+    // horizontal (fields <= 255*256), truncated to 8 bits, then vertical, rounded
+    const uint32_t trb = (lerp2_(rb_(t00), rb_(t10), iwx, wx) >> 8) & 0x00FF00FFu;
+    const uint32_t brb = (lerp2_(rb_(t01), rb_(t11), iwx, wx) >> 8) & 0x00FF00FFu;
+    const uint32_t tga = (lerp2_(ga_(t00), ga_(t10), iwx, wx) >> 8) & 0x00FF00FFu;
+    const uint32_t bga = (lerp2_(ga_(t01), ga_(t11), iwx, wx) >> 8) & 0x00FF00FFu;
+    const uint32_t crb = ((lerp2_(trb, brb, iwy, wy) + 0x00800080u) >> 8) & 0x00FF00FFu;
+    const uint32_t cga = ((lerp2_(tga, bga, iwy, wy) + 0x00800080u) >> 8) & 0x00FF00FFu;
+    if (opaque) return crb | (cga << 8) | 0xFF000000u;
+    const uint32_t a = cga >> 16;
+    return blend255_(crb & 0xFFu, a) | (blend255_(cga & 0xFFu, a) << 8) | (blend255_(crb >> 16, a) << 16) |
+           0xFF000000u;
 }
 
 constexpr uint32_t kBlackRGBA = 0xFF000000u;  // clear colour (0,0,0,1), renderer.rs:233-238

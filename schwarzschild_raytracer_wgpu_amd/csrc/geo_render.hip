@@ -35,8 +35,8 @@ struct RenderArgs {
     geo_frame frame;
     geo::PixelConsts k;  // frame constants, evaluated once on the host (IEEE f32, same bits)
     uint32_t width, height, row0, nrows;
-    uint32_t band_rows, band_stride;  // local row lr -> row0 + (lr/band_rows)*band_stride + lr%band_rows
-    uint32_t tiles_x;
+    uint32_t band_shift, band_stride;  // local row lr -> row0 + (lr>>shift)*band_stride + lr%(1<<shift)
+    uint32_t sky_opaque;
     float inv_w, inv_h, kt;
     const uint32_t* sky;
     uint32_t sky_w, sky_h;
@@ -70,15 +70,14 @@ __global__ __launch_bounds__(kBlock) void geo_render_kernel(const RenderArgs a) 
         for (uint32_t i = threadIdx.x; i < a.n_fan; i += kBlock) s_fan[i] = a.fan[i];
         __syncthreads();
     }
-    const uint32_t tx = blockIdx.x % a.tiles_x;
-    const uint32_t ty = blockIdx.x / a.tiles_x;
-    const uint32_t px = tx * kTileW + (threadIdx.x % kTileW);
-    const uint32_t ly = ty * kTileH + (threadIdx.x / kTileW);
-    // local row -> frame row.  band_rows % 8 == 0 (checked on the host) keeps
-    // each 8-row wave inside one band, so the division is wave-uniform (SALU).
+    const uint32_t px = blockIdx.x * kTileW + (threadIdx.x % kTileW);
+    const uint32_t ly = blockIdx.y * kTileH + (threadIdx.x / kTileW);
+    // local row -> frame row.  band_rows is a power of two >= 8 (checked on the
+    // host): each 8-row wave lies in one band and the mapping is wave-uniform.
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x) >> 6;
-    const uint32_t wl0 = ty * kTileH + wave * kWaveRows;
-    const uint32_t py = a.row0 + (wl0 / a.band_rows) * a.band_stride + (wl0 % a.band_rows) + (ly - wl0);
+    const uint32_t wl0 = blockIdx.y * kTileH + wave * kWaveRows;
+    const uint32_t py = a.row0 + (wl0 >> a.band_shift) * a.band_stride + (wl0 & ((1u << a.band_shift) - 1u)) +
+                        (ly - wl0);
     uint32_t steps = 0;
     if (px < a.width && ly < a.nrows && py < a.height) {
         float c2x, c2y, c2z;
@@ -99,7 +98,7 @@ __global__ __launch_bounds__(kBlock) void geo_render_kernel(const RenderArgs a) 
         const uint32_t* sky = a.sky;
         const uint32_t rgba = bh ? geo::kBlackRGBA
                                  : geo::sample_sky([sky](uint32_t i) { return sky[i]; },
-                                                   a.sky_w, a.sky_h, U, V);
+                                                   a.sky_w, a.sky_h, a.sky_opaque != 0, U, V);
         const size_t o = (size_t)ly * a.width + px;
         a.out_rgba[o] = rgba;
         if (a.out_mask) a.out_mask[o] = bh ? 1 : 0;
@@ -253,6 +252,7 @@ struct geo_ctx {
     int num_cus;
     uint32_t* sky;
     uint32_t sky_w, sky_h;
+    bool sky_opaque;
     float* fan;
     uint32_t fan_cap, n_fan;
     unsigned long long* step_slots;
@@ -344,6 +344,9 @@ int geo_set_sky(geo_ctx* c, const uint8_t* rgba8, uint32_t w, uint32_t h) {
     if (hipMemcpy(c->sky, rgba8, bytes, hipMemcpyHostToDevice) != hipSuccess) return GEO_EHIP;
     c->sky_w = w;
     c->sky_h = h;
+    bool opaque = true;
+    for (size_t i = 3; i < bytes && opaque; i += 4) opaque = rgba8[i] == 255;
+    c->sky_opaque = opaque;
     return GEO_OK;
 }
 
@@ -390,7 +393,7 @@ int geo_solve_ray_fan(geo_ctx* c, double sphere_r, double schwarz_r, uint32_t ma
 }
 
 static int render_impl(geo_ctx* c, const geo_frame* frame, const geo_scene* scene, uint32_t width,
-                       uint32_t height, uint32_t row0, uint32_t nrows, uint32_t band_rows,
+                       uint32_t height, uint32_t row0, uint32_t nrows, uint32_t band_shift,
                        uint32_t band_stride, uint8_t* out_rgba8, uint8_t* out_mask, float* out_uv,
                        uint32_t* out_steps, unsigned long long* steps_total, void* stream) {
     if (scene->mode != GEO_MODE_DIRECT && scene->mode != GEO_MODE_FAN) return GEO_EINVAL;
@@ -413,9 +416,10 @@ static int render_impl(geo_ctx* c, const geo_frame* frame, const geo_scene* scen
     a.height = height;
     a.row0 = row0;
     a.nrows = nrows;
-    a.band_rows = band_rows;
+    a.band_shift = band_shift;
     a.band_stride = band_stride;
-    a.tiles_x = (width + kTileW - 1) / kTileW;
+    a.sky_opaque = c->sky_opaque ? 1u : 0u;
+    const uint32_t tiles_x = (width + kTileW - 1) / kTileW;
     a.inv_w = 1.0f / (float)width;
     a.inv_h = 1.0f / (float)height;
     a.kt = geo::aberration_kt(frame->psi_factor_and_position[0]);
@@ -431,7 +435,7 @@ static int render_impl(geo_ctx* c, const geo_frame* frame, const geo_scene* scen
     a.out_steps = out_steps;
     a.step_slots = (steps_total || defer) ? c->step_slots : nullptr;
     hipStream_t s = (hipStream_t)stream;
-    const dim3 grid(a.tiles_x * tiles_y);
+    const dim3 grid(tiles_x, tiles_y);
     if (scene->mode == GEO_MODE_FAN) {
         hipLaunchKernelGGL((geo_render_kernel<GEO_MODE_FAN, geo::kCurvedOut>), grid, dim3(kBlock), 0, s, a);
     } else {
@@ -472,8 +476,8 @@ int geo_render_rows(geo_ctx* c, const geo_frame* frame, const geo_scene* scene, 
         return GEO_EINVAL;
     if ((uint64_t)row0 + nrows > height || width > (1u << 20) || height > (1u << 20))
         return GEO_EINVAL;
-    // one band covering every row (band_rows >= nrows, a multiple of 8)
-    return render_impl(c, frame, scene, width, height, row0, nrows, 1u << 21, 1u << 21, out_rgba8, out_mask,
+    // one band covering every row (2^21 >= nrows)
+    return render_impl(c, frame, scene, width, height, row0, nrows, 21u, 1u << 21, out_rgba8, out_mask,
                        out_uv, out_steps, steps_total, stream);
 }
 
@@ -482,16 +486,16 @@ int geo_render_bands(geo_ctx* c, const geo_frame* frame, const geo_scene* scene,
                      uint32_t nbands, uint8_t* out_rgba8, uint8_t* out_mask, float* out_uv,
                      uint32_t* out_steps, unsigned long long* steps_total, void* stream) {
     if (!c || !frame || !scene || !out_rgba8 || width == 0 || height == 0 || band_rows == 0 ||
-        nbands == 0 || band_step == 0 || band_rows % kWaveRows != 0)
+        nbands == 0 || band_step == 0 || band_rows < (uint32_t)kWaveRows || (band_rows & (band_rows - 1)) != 0)
         return GEO_EINVAL;
     if (width > (1u << 20) || height > (1u << 20)) return GEO_EINVAL;
     const uint64_t first = (uint64_t)band0 * band_rows;
     const uint64_t last = first + (uint64_t)(nbands - 1) * band_step * band_rows;
     const uint64_t nrows = (uint64_t)nbands * band_rows;
     if (first >= height || last >= height || nrows > (1u << 20)) return GEO_EINVAL;
-    return render_impl(c, frame, scene, width, height, (uint32_t)first, (uint32_t)nrows, band_rows,
-                       band_step * band_rows, out_rgba8, out_mask, out_uv, out_steps, steps_total,
-                       stream);
+    return render_impl(c, frame, scene, width, height, (uint32_t)first, (uint32_t)nrows,
+                       (uint32_t)__builtin_ctz(band_rows), band_step * band_rows, out_rgba8, out_mask, out_uv,
+                       out_steps, steps_total, stream);
 }
 
 }  // extern "C"

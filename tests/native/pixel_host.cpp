@@ -21,6 +21,8 @@ extern "C" int host_render(const geo_frame* f, const geo_scene* s, const float* 
                            uint32_t row0, uint32_t nrows, uint32_t* rgba, uint8_t* mask, float* uv,
                            uint32_t* steps, int variant) {
     const geo::PixelConsts k = geo::make_consts(s->rs, s->sphere_r, s->r_obs, s->step, s->max_steps);
+    bool opaque = true;
+    for (size_t i = 0; i < (size_t)sw * sh; ++i) opaque = opaque && (sky[i] >> 24) == 255u;
     const float inv_w = 1.0f / (float)width, inv_h = 1.0f / (float)height;
     for (uint32_t ly = 0; ly < nrows; ++ly) {
         const uint32_t py = row0 + ly;
@@ -40,7 +42,7 @@ extern "C" int host_render(const geo_frame* f, const geo_scene* s, const float* 
             float U, V;
             geo::sky_uv(f->central_to_uv, c2x, c2y, ct, lam, &U, &V);
             const size_t o = (size_t)ly * width + px;
-            rgba[o] = bh ? geo::kBlackRGBA : geo::sample_sky([sky](uint32_t i) { return sky[i]; }, sw, sh, U, V);
+            rgba[o] = bh ? geo::kBlackRGBA : geo::sample_sky([sky](uint32_t i) { return sky[i]; }, sw, sh, opaque, U, V);
             mask[o] = bh ? 1 : 0;
             uv[2 * o] = U;
             uv[2 * o + 1] = V;

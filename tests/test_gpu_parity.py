@@ -100,6 +100,7 @@ SCENES = [
      dict(rs=10.0, sphere_r=500.0, r_obs=math.sqrt(626.0), max_steps=1000), "equirect"),
     ("single_row", 97, 1, {}, dict(max_steps=512), "equirect"),
     ("single_col", 1, 77, {}, dict(max_steps=512), "equirect"),
+    ("translucent_sky", 120, 68, {}, dict(max_steps=512), "random_alpha"),
 ]
 
 
@@ -107,7 +108,10 @@ SCENES = [
 def test_direct_mode_matches_oracle_bitexact(geo, torch_mod, name, w, h, fk, sk, skykind):
     from schwarzschild_raytracer_wgpu_amd.scenes import make_sky
 
-    sky = make_sky(skykind, (1, 1) if skykind == "flat" else (512, 256))
+    if skykind == "random_alpha":
+        sky = np.random.default_rng(3).integers(0, 256, size=(128, 256, 4), dtype=np.uint8)
+    else:
+        sky = make_sky(skykind, (1, 1) if skykind == "flat" else (512, 256))
     frame = default_frame(w, h, **fk)
     scene = default_scene(**sk)
     ctx = make_ctx(geo, sky)

@@ -87,3 +87,15 @@ def test_host_header_fan_mode(host):
     for f in ("mask", "rgba"):
         assert np.array_equal(a[f], b[f])
     assert np.array_equal(a["uv"].view(np.uint32), b["uv"].view(np.uint32))
+
+
+def test_host_header_translucent_sky(host):
+    """Sky with alpha < 255: the alpha blend over the clear colour (rgb*a/255)."""
+    rng = np.random.default_rng(7)
+    sky = rng.integers(0, 256, size=(64, 128, 4), dtype=np.uint8)
+    w, h = 96, 54
+    frame, scene = default_frame(w, h), default_scene(512)
+    a = run_host(host, frame, scene, sky, w, h)
+    b = O.render_f32(frame, scene, sky, w, h, threads=4)
+    assert np.array_equal(a["rgba"], b["rgba"])
+    assert np.all(b["rgba"][..., 3] == 255)

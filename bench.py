@@ -28,6 +28,11 @@ sys.path.insert(0, ROOT)
 PEAK_FP32_TFLOPS = 157.3  # MI355X FP32 vector peak (MI355X_MICROARCH.md, spec)
 FLOPS_PER_EVAL = 40  # one RK4 evaluation of u'' = -u + 1.5 rs u^2
 NEWTON_EVALS = 3  # per sphere crossing (sphere_ray_tracer.rs:129)
+# adaptive mode (config 5): one Dormand-Prince RK5(4) attempt in Nystrom form
+# (geo_pixel.h dp5_step, counting an FMA as 2): 83 flops with the error
+# estimate, 72 for a Newton evaluation (no estimate)
+FLOPS_PER_ATTEMPT = 83
+FLOPS_PER_NEWTON_DP5 = 72
 
 
 def parse():
@@ -44,9 +49,11 @@ def parse():
     p.add_argument("--band-rows", type=int, default=8)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-threads", type=int, default=16)
-    p.add_argument("--cpu-row-step", type=int, default=1)
+    p.add_argument("--cpu-row-step", type=int, default=None,
+                   help="CPU baseline sample: every k-th row (default 1 up to 4K, 4 above)")
     p.add_argument("--cpu-seconds", type=float, default=1.0)
-    p.add_argument("--mode", default="direct", choices=["direct", "fan"])
+    p.add_argument("--mode", default=None, choices=["direct", "fan", "adaptive"],
+                   help="default: the config's mode (cfg1-4 direct, cfg5_8k_adaptive adaptive)")
     p.add_argument("--check-frame", action="store_true",
                    help="rank 0 checks the assembled frame against a single-launch full frame")
     p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
@@ -85,8 +92,10 @@ def main():
     obs.set_camera(*cfg.camera)
     obs.set_energy(cfg.energy)
     frame = obs.calc_transformation_pipeline()
-    mode = g.GEO_MODE_FAN if args.mode == "fan" else g.GEO_MODE_DIRECT
-    scene = g.make_scene(cfg.rs, cfg.sphere_r, obs.get_radial_position(), cfg.step, cfg.max_steps, mode)
+    args.mode = args.mode or cfg.mode
+    mode = {"direct": g.GEO_MODE_DIRECT, "fan": g.GEO_MODE_FAN, "adaptive": g.GEO_MODE_ADAPTIVE}[args.mode]
+    tol = cfg.tol if mode == g.GEO_MODE_ADAPTIVE else 0.0
+    scene = g.make_scene(cfg.rs, cfg.sphere_r, obs.get_radial_position(), cfg.step, cfg.max_steps, mode, tol=tol)
     sky = make_sky(cfg.sky, cfg.sky_size)
     ctx = g.Context(local)
     ctx.set_sky(sky)
@@ -115,6 +124,10 @@ def main():
     rows_mine = L.rows_mine()
     steps_diag = int(diag_ctr.item())
     evals_per_launch = steps_diag + NEWTON_EVALS * hits
+    if mode == g.GEO_MODE_ADAPTIVE:
+        flops_per_launch = FLOPS_PER_ATTEMPT * steps_diag + FLOPS_PER_NEWTON_DP5 * NEWTON_EVALS * hits
+    else:
+        flops_per_launch = FLOPS_PER_EVAL * evals_per_launch
 
     # GPU clock spin-up (untimed, not counted as warmup): from idle the first
     # frames run up to 5x slower while the clock ramps (tools/ubench/gap_probe2.py)
@@ -134,7 +147,7 @@ def main():
     from schwarzschild_raytracer_wgpu_amd.timing import HipEvent
 
     scene_defer = g.make_scene(cfg.rs, cfg.sphere_r, obs.get_radial_position(), cfg.step, cfg.max_steps, mode,
-                               flags=g._lib.GEO_FLAG_DEFER_STEPS)
+                               flags=g._lib.GEO_FLAG_DEFER_STEPS, tol=tol)
     timed = set(range(0, args.steps, max(1, args.event_every)))
     evs = {i: (HipEvent(), HipEvent()) for i in timed}
     steps_ctr.zero_()
@@ -181,11 +194,21 @@ def main():
 
     value = total_steps / elapsed_max
     # roofline for the dominant kernel, on this rank: algorithmic flops per launch / avg launch time
-    achieved_tflops = FLOPS_PER_EVAL * evals_per_launch / (kernel_ms_avg * 1e-3) / 1e12
+    achieved_tflops = flops_per_launch / (kernel_ms_avg * 1e-3) / 1e12
+    if mode == g.GEO_MODE_ADAPTIVE:
+        metric = (f"geodesic-step-attempts·pixels/sec at {W}x{H}, adaptive RK5(4) tol {cfg.tol:g} "
+                  f"(whole job; /GPU = value/n_gpus)")
+        unit = "geodesic-step-attempts·pixels/s"
+        stepping = f"adaptive Dormand-Prince RK5(4), tol {cfg.tol:g} in u, initial step pi/100, " \
+                   f"{cfg.max_steps} max attempts"
+    else:
+        metric = f"geodesic-steps·pixels/sec at {W}x{H}, {cfg.max_steps} max steps (whole job; /GPU = value/n_gpus)"
+        unit = "geodesic-steps·pixels/s"
+        stepping = f"step pi/100, {cfg.max_steps} max RK4 steps"
     out = {
-        "metric": "geodesic-steps·pixels/sec at 3840x2160, 2048 max steps (whole job; /GPU = value/n_gpus)",
+        "metric": metric,
         "value": value,
-        "unit": "geodesic-steps·pixels/s",
+        "unit": unit,
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
@@ -198,7 +221,7 @@ def main():
         "config": {
             "workload": f"{cfg.name}: {W}x{H}, rs={cfg.rs}, sphere_r={cfg.sphere_r}, observer {cfg.position} "
                         f"FrozenFall E={cfg.energy}, camera {tuple(round(c, 4) for c in cfg.camera)}, fov pi/2, "
-                        f"step pi/100, {cfg.max_steps} max RK4 steps, mode {args.mode}",
+                        f"{stepping}, mode {args.mode}",
             "width": W, "height": H, "max_steps": cfg.max_steps,
             "parallelism": f"rowbands{world}" if world > 1 else "single",
             "band_rows": args.band_rows,
@@ -219,12 +242,12 @@ def main():
             "unit": "TFLOP/s",
             "frac": achieved_tflops / PEAK_FP32_TFLOPS,
             "traffic": pmc_traffic(args.config, args.mode),
-            "kernel": "geo_render_kernel<0>",
-            "algorithmic_flops_per_launch": FLOPS_PER_EVAL * evals_per_launch,
+            "kernel": f"geo_render_kernel<{mode}>",
+            "algorithmic_flops_per_launch": flops_per_launch,
             "evals_per_launch": evals_per_launch,
         },
     }
-    if world == 1 and not args.no_cpu_baseline and mode == g.GEO_MODE_DIRECT:
+    if world == 1 and not args.no_cpu_baseline and mode != g.GEO_MODE_FAN:
         out["cpu_baseline"] = cpu_baseline(frame, scene, sky, W, H, args)
     print(json.dumps(out), flush=True)
     if world > 1:
@@ -237,7 +260,7 @@ def pmc_traffic(config, mode):
     tools/gpu_pmc.sh + tools/pmc_to_profile.py), or None."""
     import glob
 
-    if mode != "direct":
+    if mode == "fan":
         return None
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_{config}_pmc.json")))
     if not files:
@@ -253,7 +276,7 @@ def cpu_baseline(frame, scene, sky, W, H, args):
     import oracle as O
 
     threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
-    k = args.cpu_row_step
+    k = args.cpu_row_step or (1 if W * H <= 3840 * 2160 else 4)
     nrows = (H + k - 1) // k
     steps = 0
     frames = 0
@@ -269,10 +292,10 @@ def cpu_baseline(frame, scene, sky, W, H, args):
     what = "full" if k == 1 else f"every {k}th row of the"
     return {
         "value": steps / dt,
-        "unit": "geodesic-steps·pixels/s",
+        "unit": "geodesic-step-attempts·pixels/s" if scene.mode == 2 else "geodesic-steps·pixels/s",
         "cores": threads,
         "kind": "port",
-        "sample": f"{frames} x {what} {W}x{H} frame ({nrows * W} pixels, {steps // frames} RK4 steps each) "
+        "sample": f"{frames} x {what} {W}x{H} frame ({nrows * W} pixels, {steps // frames} steps each) "
                   f"in {dt:.2f} s wall on {threads} threads",
         "seconds": dt,
     }

@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define GEO_ABI_VERSION 1
+#define GEO_ABI_VERSION 2
 
 typedef enum geo_status {
     GEO_OK = 0,
@@ -54,6 +54,10 @@ typedef enum geo_status {
 /* Render modes (geo_scene.mode). */
 #define GEO_MODE_DIRECT 0u /* per-pixel RK4 of the null geodesic at the pixel's own angle */
 #define GEO_MODE_FAN 1u    /* reference-exact: lerp into the ray fan (shader.wgsl:77-84) */
+#define GEO_MODE_ADAPTIVE 2u /* per-pixel, error-controlled Dormand-Prince RK5(4) steps (config 5;
+                                a build extension, not in the reference): geo_scene.step is the
+                                initial step, max_steps the budget of step ATTEMPTS, tol the
+                                local error tolerance in u */
 
 /* geo_scene.flags */
 #define GEO_FLAG_DEFER_STEPS 1u /* executed steps accumulate in the context (no per-call
@@ -64,6 +68,10 @@ typedef enum geo_status {
 #define GEO_OBSERVER_UNMOVING 0
 #define GEO_OBSERVER_FROZEN_FALL 1
 #define GEO_OBSERVER_ORBITING 2
+
+/* GEO_MODE_ADAPTIVE step control (geo_pixel.h, geodesic_angle_adaptive). */
+#define GEO_ADAPTIVE_DEFAULT_TOL 1e-6f
+#define GEO_ADAPTIVE_MAX_GROWTH 16u /* largest step = 16 x geo_scene.step */
 
 /* Sentinel for a ray that never reaches the sphere, SphereRayTracer::NO_VALUE
  * (sphere_ray_tracer.rs:22).  Fan / traveled-angle space. */
@@ -84,11 +92,14 @@ typedef struct geo_scene {
     float rs;           /* Schwarzschild radius */
     float sphere_r;     /* radius of the textured sky sphere */
     float r_obs;        /* observer radial position |pos| (lib.rs:292) */
-    float step;         /* RK4 step in traveled angle (PI/100 in the reference) */
-    uint32_t max_steps; /* RK4 budget per ray (1000 in the reference), <= 2^24 */
+    float step;         /* RK4 step in traveled angle (PI/100 in the reference);
+                           GEO_MODE_ADAPTIVE: the initial step */
+    uint32_t max_steps; /* RK4 budget per ray (1000 in the reference), <= 2^24;
+                           GEO_MODE_ADAPTIVE: budget of step attempts */
     uint32_t mode;      /* GEO_MODE_* */
     uint32_t flags;     /* GEO_FLAG_* */
-    uint32_t reserved;  /* must be 0 */
+    float tol;          /* GEO_MODE_ADAPTIVE: local error tolerance in u (0 = 1e-6);
+                           must be 0 in the other modes */
 } geo_scene;
 
 typedef struct geo_ctx geo_ctx;

@@ -39,7 +39,7 @@ class GeoSceneC(ctypes.Structure):
         ("max_steps", ctypes.c_uint32),
         ("mode", ctypes.c_uint32),
         ("flags", ctypes.c_uint32),
-        ("reserved", ctypes.c_uint32),
+        ("tol", ctypes.c_float),
     ]
 
 
@@ -73,6 +73,7 @@ def _load() -> ctypes.CDLL:
         "geo_oracle_render_f32": (i, [vp, vp, vp, u32, vp, u32, u32, u32, u32, u32, u32, u32, i, vp, vp, vp,
                                       vp, vp]),
         "geo_oracle_observer_frame": (None, [f64, f64, f64, f64, vp, f64, f64, i, f64, vp]),
+        "geo_oracle_geodesic_f32": (ctypes.c_float, [vp, ctypes.c_float, ctypes.c_float, vp]),
         "geo_oracle_asinf": (ctypes.c_float, [ctypes.c_float]),
         "geo_oracle_atan2f": (ctypes.c_float, [ctypes.c_float, ctypes.c_float]),
         "geo_oracle_sincosf": (None, [ctypes.c_float, vp, vp]),
@@ -112,6 +113,14 @@ def solve_geodesic(sphere_r, schwarz_r, max_iter, step, r, energy, rotation, r_f
     steps = ctypes.c_uint32()
     a = lib.geo_oracle_solve_geodesic_f64(sphere_r, schwarz_r, max_iter, step, r, energy, rotation,
                                           int(bool(r_falling)), ctypes.byref(steps))
+    return a, steps.value
+
+
+def geodesic_f32(scene, st, ct):
+    """Traveled angle (f32 kernel order; scene.mode selects fixed or adaptive) and steps."""
+    steps = ctypes.c_uint32()
+    sc = as_scene(scene)
+    a = lib.geo_oracle_geodesic_f32(_addr(sc), st, ct, ctypes.byref(steps))
     return a, steps.value
 
 

@@ -202,6 +202,12 @@ void geo_oracle_pixel_f64(const geo_frame* f, const geo_scene* s, const float* f
         double w = t - fl;
         uint32_t i1 = i + 1u < n_fan ? i + 1u : n_fan - 1u;
         lam2 = (double)fan[i] * (1. - w) + (double)fan[i1] * w;
+    } else if (s->mode == GEO_MODE_ADAPTIVE) {
+        /* the adaptive mode has no reference counterpart: its f64 check is the
+         * fixed-step integration at step/32 */
+        lam2 = O_FRAC_PI_2 - geo_oracle_geodesic_at_theta_f64((double)s->sphere_r, (double)s->rs,
+                                                              GEO_ORACLE_FINE_BUDGET, (double)s->step / 32.,
+                                                              (double)s->r_obs, lam, &out->steps);
     } else {
         lam2 = O_FRAC_PI_2 - geo_oracle_geodesic_at_theta_f64((double)s->sphere_r, (double)s->rs, s->max_steps,
                                                               (double)s->step, (double)s->r_obs, lam, &out->steps);
@@ -295,6 +301,7 @@ typedef struct {
     float hh, h6, hh2, hhh, h2_6, r3_2, sphere_u, schwarz_u, u0, h_over_r2, bound, e_out, e_in, barrier;
     int r_inside_h, outside, sphere_outside, inside_sphere, diff_sides, rs_nonzero;
     float scale, U0, SU, BD, HU; /* scaled state U = scale*u */
+    float tolU, tolG, hmax;      /* GEO_MODE_ADAPTIVE step control */
 } fconsts;
 
 static fconsts make_fconsts(const geo_scene* s) {
@@ -331,6 +338,9 @@ static fconsts make_fconsts(const geo_scene* s) {
     k.SU = k.scale * k.sphere_u;
     k.BD = k.scale * k.bound;
     k.HU = k.scale * k.schwarz_u;
+    k.tolU = k.scale * (s->tol > 0.0f ? s->tol : GEO_ADAPTIVE_DEFAULT_TOL);
+    k.tolG = k.tolU * (1.0f / 64.0f);
+    k.hmax = k.step * (float)GEO_ADAPTIVE_MAX_GROWTH;
     return k;
 }
 
@@ -356,7 +366,97 @@ static inline void rk4f(float U, float UB, float h, float hh, float hh2, float h
     *NUB = fmaf(h6, fmaf(2.0f, fab, fu) + fc, UB);
 }
 
-static float geodesic_f32(const fconsts* k, float st, float ct, uint32_t* steps) {
+/* GEO_MODE_ADAPTIVE (config 5, a build extension): Dormand-Prince RK5(4)
+ * (J. Comput. Appl. Math. 6 (1980) 19-26) on the scaled state in Nystrom form,
+ *   U_i = U + c_i h V + h^2 sum_j (A^2)_ij G_j,  G_j = F(U_j),
+ *   NU = U + h V + h^2 sum_j (bA)_j G_j,  NV = V + h sum_j b_j G_j,
+ *   error estimate |sum_j ((b - b*)A)_j G_j| h^2  (in U),
+ * coefficients = the exact rationals rounded once to f32 (tools/dp5_coeffs.py
+ * prints this table).  Evaluation order: DESIGN.md §3a. */
+static const float DP_C2 = 0x1.99999ap-3f, DP_C3 = 0x1.333334p-2f, DP_C4 = 0x1.99999ap-1f,
+                   DP_C5 = 0x1.c71c72p-1f;
+static const float DP_A31 = 0x1.70a3d8p-5f, DP_A41 = -0x1.eb851ep-2f, DP_A42 = 0x1.99999ap-1f,
+                   DP_A51 = -0x1.dde5dcp+0f, DP_A52 = 0x1.a5de0ep+1f, DP_A53 = -0x1.08b37cp+0f,
+                   DP_A61 = -0x1.026c9cp+1f, DP_A62 = 0x1.08ba2ep+2f, DP_A63 = -0x1.b26c9cp+0f,
+                   DP_A64 = 0x1.45d174p-4f;
+static const float DP_Q[6] = {0x1.755556p-4f, 0.0f, 0x1.420338p-2f, 0x1.0aaaaap-3f, -0x1.256f18p-5f, 0.0f};
+static const float DP_B[6] = {0x1.755556p-4f, 0.0f, 0x1.cc049ap-2f, 0x1.4d5556p-1f, -0x1.4a1cfcp-2f,
+                              0x1.0c30c4p-3f};
+static const float DP_E[6] = {0x1.5b9754p-9f, 0.0f, -0x1.938a4p-8f, 0x1.4da74p-7f, -0x1.be0506p-9f,
+                              -0x1.ad1ad2p-9f};
+
+/* sum_j w_j G_j over the nonzero w_j, first term a product, then FMAs in j order */
+static float wsum(const float* w, const float* G, int n) {
+    float acc = 0.0f;
+    int first = 1;
+    for (int j = 0; j < n; ++j) {
+        if (w[j] == 0.0f) continue;
+        acc = first ? w[j] * G[j] : fmaf(w[j], G[j], acc);
+        first = 0;
+    }
+    return acc;
+}
+
+static void dp5f(float U, float V, float h, int flat, float* NU, float* NV, float* SE) {
+    float G[6], Ui;
+    const float A2[6][4] = {{0}, {0}, {DP_A31}, {DP_A41, DP_A42}, {DP_A51, DP_A52, DP_A53},
+                            {DP_A61, DP_A62, DP_A63, DP_A64}};
+    const float C[6] = {0.0f, DP_C2, DP_C3, DP_C4, DP_C5, 1.0f};
+    G[0] = Ff(U, flat);
+    for (int i = 1; i < 6; ++i) {
+        /* U_i = U + h (c_i V + h S_i); S_i over j < i-1 ((A^2)_{i,i-1} = 0); c6 = 1: V itself */
+        float cv = i == 5 ? V : C[i] * V;
+        if (i == 1)
+            Ui = fmaf(h, cv, U);
+        else
+            Ui = fmaf(h, fmaf(h, wsum(A2[i], G, i - 1), cv), U);
+        G[i] = Ff(Ui, flat);
+    }
+    *NU = fmaf(h, fmaf(h, wsum(DP_Q, G, 6), V), U);
+    *NV = fmaf(h, wsum(DP_B, G, 6), V);
+    *SE = wsum(DP_E, G, 6);
+}
+
+/* the literal adaptive loop: stop checks in the reference's order
+ * (crossing :150, escape :184, loop test :134-135) on accepted steps only */
+static float adaptive_f32(const fconsts* k, float U, float V, int flat, uint32_t* steps) {
+    float h = k->step, ang = 0.0f;
+    uint32_t it = 0;
+    while (it < k->max_steps) {
+        float NU, NV, SE;
+        ++it;
+        dp5f(U, V, h, flat, &NU, &NV, &SE);
+        float err = fabsf(SE) * (h * h);
+        if (err > k->tolU) {
+            h = h * 0.5f;
+            continue;
+        }
+        if ((NU > k->SU) != (U > k->SU)) {
+            float ns, wu, wv, se;
+            if (fabsf(V) > fabsf(NV)) {
+                ns = 0.0f; wu = U; wv = V;
+            } else {
+                ns = h; wu = NU; wv = NV;
+            }
+            for (int n = 0; n < 3; ++n) {
+                ns = ns - (wu - k->SU) / wv;
+                dp5f(U, V, ns, flat, &wu, &wv, &se);
+            }
+            *steps = it;
+            return ang + ns;
+        }
+        if (NU < k->BD) break;
+        U = NU;
+        V = NV;
+        ang = ang + h;
+        if (err < k->tolG) h = fminf(h + h, k->hmax);
+        if ((k->rs_nonzero && U > k->HU && V > 0.0f) || !(U > 0.0f)) break;
+    }
+    *steps = it;
+    return 15.0f;
+}
+
+static float geodesic_f32(const fconsts* k, float st, float ct, int adaptive, uint32_t* steps) {
     *steps = 0;
     float rotation = k->r * ct;
     int falling;
@@ -391,6 +491,7 @@ static float geodesic_f32(const fconsts* k, float st, float ct, uint32_t* steps)
     if ((k->rs_nonzero && k->u0 > k->schwarz_u && ub > 0.0f) || k->max_steps == 0u || !(k->u0 > 0.0f)) return 15.0f;
     int flat = !k->rs_nonzero;
     float U = k->U0, UB = k->scale * ub;
+    if (adaptive) return adaptive_f32(k, U, UB, flat, steps);
     uint32_t it = 0;
     for (;;) { /* :134-191, one step per iteration */
         float NU, NUB;
@@ -423,6 +524,14 @@ static float geodesic_f32(const fconsts* k, float st, float ct, uint32_t* steps)
     }
     *steps = it;
     return 15.0f;
+}
+
+float geo_oracle_geodesic_f32(const geo_scene* s, float st, float ct, uint32_t* steps) {
+    fconsts k = make_fconsts(s);
+    uint32_t n = 0;
+    float a = geodesic_f32(&k, st, ct, s->mode == GEO_MODE_ADAPTIVE, &n);
+    if (steps) *steps = n;
+    return a;
 }
 
 static inline void m3vf(const float* m, float x, float y, float z, float* o) {
@@ -462,7 +571,7 @@ static void pixel_f32(const geo_frame* f, const fconsts* k, int mode, const floa
         uint32_t i1 = (i + 1u < n_fan) ? i + 1u : n_fan - 1u;
         lam = fan[i] * (1.0f - w) + fan[i1] * w;
     } else {
-        lam = F_PI2 - geodesic_f32(k, st, rho2, steps);
+        lam = F_PI2 - geodesic_f32(k, st, rho2, mode == (int)GEO_MODE_ADAPTIVE, steps);
     }
     int bh = lam < -7.0f;
     /* sky_uv */

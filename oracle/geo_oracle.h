@@ -18,7 +18,9 @@
  *     geo_oracle_pixel_f64            shader.wgsl:57-106 (direct or fan mode)
  *     geo_oracle_observer_frame       observer.rs:197-262 + polar_transformations.rs
  *   f32 restatement of the kernel's fixed evaluation order (bit-exact checker):
- *     geo_oracle_pixel_f32 / geo_oracle_render_f32
+ *     geo_oracle_pixel_f32 / geo_oracle_render_f32 (all three modes; the
+ *     adaptive RK5(4) mode is a build extension without a reference
+ *     counterpart, checked in f64 against the fixed step/32 integration)
  */
 #ifndef GEO_ORACLE_H
 #define GEO_ORACLE_H
@@ -49,6 +51,9 @@ void geo_oracle_solve_ray_fan_f64(double sphere_r, double schwarz_r, uint32_t ma
 double geo_oracle_geodesic_at_theta_f64(double sphere_r, double schwarz_r, uint32_t max_iter,
                                         double step, double r, double theta, uint32_t* steps);
 
+/* GEO_MODE_ADAPTIVE in the f64 pixel: fixed RK4 at step/32 with this budget */
+#define GEO_ORACLE_FINE_BUDGET (1u << 22)
+
 void geo_oracle_pixel_f64(const geo_frame* f, const geo_scene* s, const float* fan, uint32_t n_fan,
                           uint32_t width, uint32_t height, uint32_t px, uint32_t py,
                           geo_oracle_px* out);
@@ -62,6 +67,10 @@ int geo_oracle_render_f32(const geo_frame* f, const geo_scene* s, const float* f
                           uint32_t height, uint32_t row0, uint32_t nrows, uint32_t row_step,
                           int threads, uint8_t* rgba, uint8_t* mask, float* uv, uint32_t* steps,
                           uint64_t* steps_total);
+
+/* Traveled angle of one ray in the f32 kernel order (direct or adaptive mode
+ * by s->mode) for (sin theta, cos theta) of the central-frame direction. */
+float geo_oracle_geodesic_f32(const geo_scene* s, float st, float ct, uint32_t* steps);
 
 /* Observer::calc_transformation_pipeline for a fixed pose (observer.rs:68-87,
  * 141-160, 197-262); state = GEO_OBSERVER_UNMOVING or GEO_OBSERVER_FROZEN_FALL. */

@@ -20,6 +20,9 @@ GEO_ESTATE = -5
 
 GEO_MODE_DIRECT = 0
 GEO_MODE_FAN = 1
+GEO_MODE_ADAPTIVE = 2
+GEO_ADAPTIVE_DEFAULT_TOL = 1e-6
+GEO_ADAPTIVE_MAX_GROWTH = 16
 GEO_FLAG_DEFER_STEPS = 1
 
 GEO_OBSERVER_UNMOVING = 0
@@ -49,7 +52,7 @@ class GeoScene(ctypes.Structure):
         ("max_steps", ctypes.c_uint32),
         ("mode", ctypes.c_uint32),
         ("flags", ctypes.c_uint32),
-        ("reserved", ctypes.c_uint32),
+        ("tol", ctypes.c_float),
     ]
 
 

@@ -175,8 +175,9 @@ class Context:
 
 
 def make_scene(rs: float, sphere_r: float, r_obs: float, step: float = math.pi / 100.0, max_steps: int = 1000,
-               mode: int = _lib.GEO_MODE_DIRECT, flags: int = 0) -> GeoScene:
-    return GeoScene(rs, sphere_r, r_obs, step, max_steps, mode, flags, 0)
+               mode: int = _lib.GEO_MODE_DIRECT, flags: int = 0, tol: float = 0.0) -> GeoScene:
+    """geo_scene; tol = GEO_MODE_ADAPTIVE's error tolerance in u (0 = 1e-6, must be 0 in other modes)."""
+    return GeoScene(rs, sphere_r, r_obs, step, max_steps, mode, flags, tol)
 
 
 class SphereRayTracer:

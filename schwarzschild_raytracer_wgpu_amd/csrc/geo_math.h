@@ -17,8 +17,10 @@
 
 #if defined(__HIPCC__) || defined(__HIP__)
 #define GEO_HD __host__ __device__ __forceinline__
+#define GEO_HDM __host__ __device__ __forceinline__  // member functions
 #else
 #define GEO_HD static inline
+#define GEO_HDM inline
 #endif
 
 // Makes the compiler forget what it knows about a VGPR value (no code).

@@ -24,6 +24,8 @@ constexpr float kNoValue = 15.0f;          // SphereRayTracer::NO_VALUE, sphere_
 constexpr float kBlackHoleLambda = -7.0f;  // hit_black_hole threshold, shader.wgsl:88
 constexpr int kNewtonIters = 3;            // final_newton_refinements, sphere_ray_tracer.rs:129
 constexpr float kSixth = 1.0f / 6.0f;
+constexpr float kAdaptiveDefaultTol = 1e-6f;  // GEO_ADAPTIVE_DEFAULT_TOL
+constexpr uint32_t kAdaptiveMaxGrowth = 16u;   // GEO_ADAPTIVE_MAX_GROWTH
 
 // Frame-constant scalars derived from the scene, evaluated identically on
 // every lane (and by the oracle).  Names follow sphere_ray_tracer.rs:60-132.
@@ -54,6 +56,10 @@ struct PixelConsts {
     // the integrator's scaled state U = scale*u (scale = 3 rs/2, or 1 for rs = 0)
     float scale, U0, SU, BD, HU;
     float SUp;  // next float above SU: (U > SU) == (U >= SUp) for every float U
+    // GEO_MODE_ADAPTIVE step control (geodesic_angle_adaptive), scaled like U
+    float tolU;  // scale * tol: reject a step whose error estimate exceeds it
+    float tolG;  // tolU / 64: double the step after one whose estimate is below it
+    float hmax;  // GEO_ADAPTIVE_MAX_GROWTH * step
 };
 
 // Integration kinds (frame-uniform, chosen on the host):
@@ -81,7 +87,9 @@ GEO_HD float med3_(float x, float lo, float hi) {
 #endif
 }
 
-GEO_HD PixelConsts make_consts(float rs, float sphere_r, float r, float step, uint32_t max_steps) {
+// tol: GEO_MODE_ADAPTIVE local error tolerance in u (<= 0: the default 1e-6).
+GEO_HD PixelConsts make_consts(float rs, float sphere_r, float r, float step, uint32_t max_steps,
+                               float tol = 0.0f) {
     PixelConsts k;
     k.rs = rs;
     k.sphere_r = sphere_r;
@@ -138,6 +146,9 @@ GEO_HD PixelConsts make_consts(float rs, float sphere_r, float r, float step, ui
     k.BD = k.scale * k.bound;
     k.HU = k.scale * k.schwarz_u;
     k.SUp = next_up_(k.SU);
+    k.tolU = k.scale * (tol > 0.0f ? tol : kAdaptiveDefaultTol);
+    k.tolG = k.tolU * (1.0f / 64.0f);
+    k.hmax = step * (float)kAdaptiveMaxGrowth;
     return k;
 }
 
@@ -264,6 +275,33 @@ GEO_HD bool geodesic_init(const PixelConsts& k, float st, float ct, float* early
     return true;
 }
 
+// Stop flag of one accepted step (reference order: crossing :150, escape
+// :184, loop test :134-135).  The integration ends at the first crossing, so
+// "above the sphere" (U > SU) is fixed for the whole integration and frame-
+// uniform (U0 vs SU).  Outside the horizon the flag is then ONE interval test
+// (v_med3_f32 + compare):
+//   inside the sphere (U0 > SU): stop <=> NU not in [SU+, HU]
+//       (crossing outward | horizon; escape NU < BD < SU is a crossing too)
+//   outside (U0 <= SU):          stop <=> NU not in [BD, SU]
+//       (crossing inward | escape; the horizon HU > SU is a crossing too)
+// `!(NU >= BD)` is (NU < BD) or NaN and, with BD > 0, also covers the `u > 0`
+// test.  NaN always stops.  Inside the horizon the general test is kept.
+template <int KIND>
+struct StopTest {
+    float SU, BD, HU, lo, hi;
+    bool above0;
+    GEO_HDM explicit StopTest(const PixelConsts& k) : SU(k.SU), BD(k.BD), HU(k.HU), above0(k.U0 > k.SU) {
+        lo = above0 ? k.SUp : BD;
+        hi = above0 ? HU : SU;
+    }
+    GEO_HDM bool operator()(float NU, float NUB) const {
+        if constexpr (KIND == kCurvedIn)
+            return ((NU > SU) != above0) | !(NU >= BD) | ((NU > HU) & (NUB > 0.0f));
+        else
+            return med3_(NU, lo, hi) != NU;
+    }
+};
+
 // Traveled angle of the ray at angle theta to the black hole, or kNoValue.
 // *steps = executed main-loop RK4 steps.  LOOP = RK4 steps per exit test
 // (tools/ubench/loop_ab.hip), KIND the integration kind (geodesic_kind).
@@ -272,32 +310,12 @@ GEO_HD float geodesic_angle_v(const PixelConsts& k, float st, float ct, uint32_t
     *steps = 0;
     float U, UB, early;
     if (!geodesic_init(k, st, ct, &early, &U, &UB)) return early;
-    const float SU = k.SU, BD = k.BD, HU = k.HU;
+    const float SU = k.SU;
     const float h = k.step, hh = k.hh, hh2 = k.hh2, hhh = k.hhh, h6 = k.h6, h2_6 = k.h2_6;
-    // Main loop (:134-191), restructured for the wave64 VALU.  Per step the
-    // lane-exit flag is crossing (:150) | escape (:184) | horizon (:134);
-    // `!(NU >= BD)` is (NU < BD) or NaN and, with BD > 0, also covers the
-    // `u > 0` test; the budget (:135) is wave-uniform.  Results equal the
-    // literal loop's (the oracle keeps that form; tests require bit equality).
-    // Stop flag of one step (reference order: crossing :150, escape :184,
-    // loop test :134-135).  The loop ends at the first crossing, so "above
-    // the sphere" (U > SU) is fixed for the whole integration and frame-
-    // uniform (U0 vs SU).  Outside the horizon the flag is then ONE interval
-    // test (v_med3_f32 + compare):
-    //   inside the sphere (U0 > SU): stop <=> NU not in [SU+, HU]
-    //       (crossing outward | horizon; escape NU < BD < SU is a crossing too)
-    //   outside (U0 <= SU):          stop <=> NU not in [BD, SU]
-    //       (crossing inward | escape; the horizon HU > SU is a crossing too)
-    // NaN always stops.  Inside the horizon the general test is kept.
-    const bool above0 = k.U0 > SU;
-    const float lo = above0 ? k.SUp : BD;
-    const float hi = above0 ? HU : SU;
-    auto stop_at = [&](float NU, float NUB) -> bool {
-        if constexpr (KIND == kCurvedIn)
-            return ((NU > SU) != above0) | !(NU >= BD) | ((NU > HU) & (NUB > 0.0f));
-        else
-            return med3_(NU, lo, hi) != NU;
-    };
+    // Main loop (:134-191), restructured for the wave64 VALU: per step the
+    // lane-exit flag is StopTest (crossing | escape | horizon); the budget
+    // (:135) is wave-uniform.
+    const StopTest<KIND> stop_at(k);
     // LOOP = G: G RK4 steps per exit test (the budget in whole groups is a
     // wave-uniform bound); a lane that stops inside a group discards the rest
     // of it.  Results equal the literal loop's (the oracle keeps that form;
@@ -379,6 +397,108 @@ GEO_HD float geodesic_angle(const PixelConsts& k, float st, float ct, uint32_t* 
         case kCurvedIn: return geodesic_angle_v<GEO_LOOP_VARIANT, kCurvedIn>(k, st, ct, steps);
         default: return geodesic_angle_v<GEO_LOOP_VARIANT, kFlat>(k, st, ct, steps);
     }
+}
+
+// ---- GEO_MODE_ADAPTIVE (config 5; a build extension, not in the reference) ----
+//
+// Dormand-Prince RK5(4) (J. Comput. Appl. Math. 6 (1980) 19-26, RK5(4)7M) on
+// the scaled state, in Nystrom form: for (U, V)' = (V, F(U)) the stage values
+// are U_i = U + c_i h V + h^2 sum_j (A^2)_ij G_j with G_j = F(U_j), so no stage
+// V is formed; the 5th-order solution is
+//   NU = U + h V + h^2 sum_j (bA)_j G_j,   NV = V + h sum_j b_j G_j,
+// and the embedded error estimate in U is h^2 sum_j ((b - b*)A)_j G_j (stage 7,
+// the FSAL stage, does not enter it).  Coefficients: exact rationals rounded
+// once to f32 (tools/dp5_coeffs.py); zeros dropped ((A^2)_{i,i-1} = b2 =
+// (bA)_2 = (bA)_6 = (eA)_2 = 0, c6 = 1).  49 VALU ops per attempt.
+namespace dp5 {
+constexpr float c2 = 0x1.99999ap-3f, c3 = 0x1.333334p-2f, c4 = 0x1.99999ap-1f, c5 = 0x1.c71c72p-1f;
+constexpr float a31 = 0x1.70a3d8p-5f;
+constexpr float a41 = -0x1.eb851ep-2f, a42 = 0x1.99999ap-1f;
+constexpr float a51 = -0x1.dde5dcp+0f, a52 = 0x1.a5de0ep+1f, a53 = -0x1.08b37cp+0f;
+constexpr float a61 = -0x1.026c9cp+1f, a62 = 0x1.08ba2ep+2f, a63 = -0x1.b26c9cp+0f, a64 = 0x1.45d174p-4f;
+constexpr float q1 = 0x1.755556p-4f, q3 = 0x1.420338p-2f, q4 = 0x1.0aaaaap-3f, q5 = -0x1.256f18p-5f;
+constexpr float b1 = 0x1.755556p-4f, b3 = 0x1.cc049ap-2f, b4 = 0x1.4d5556p-1f, b5 = -0x1.4a1cfcp-2f,
+                b6 = 0x1.0c30c4p-3f;
+constexpr float e1 = 0x1.5b9754p-9f, e3 = -0x1.938a4p-8f, e4 = 0x1.4da74p-7f, e5 = -0x1.be0506p-9f,
+                e6 = -0x1.ad1ad2p-9f;
+}  // namespace dp5
+
+// One attempt: 5th-order (NU, NV) and the error sum SE (error = |SE| h^2).
+template <int KIND>
+GEO_HD void dp5_step(float U, float V, float h, float* NU, float* NV, float* SE) {
+    using namespace dp5;
+    const float g1 = F_<KIND>(U);
+    const float u2 = fmaf_(h, c2 * V, U);
+    const float g2 = F_<KIND>(u2);
+    const float u3 = fmaf_(h, fmaf_(h, a31 * g1, c3 * V), U);
+    const float g3 = F_<KIND>(u3);
+    const float u4 = fmaf_(h, fmaf_(h, fmaf_(a42, g2, a41 * g1), c4 * V), U);
+    const float g4 = F_<KIND>(u4);
+    const float u5 = fmaf_(h, fmaf_(h, fmaf_(a53, g3, fmaf_(a52, g2, a51 * g1)), c5 * V), U);
+    const float g5 = F_<KIND>(u5);
+    const float u6 = fmaf_(h, fmaf_(h, fmaf_(a64, g4, fmaf_(a63, g3, fmaf_(a62, g2, a61 * g1))), V), U);
+    const float g6 = F_<KIND>(u6);
+    *NU = fmaf_(h, fmaf_(h, fmaf_(q5, g5, fmaf_(q4, g4, fmaf_(q3, g3, q1 * g1))), V), U);
+    *NV = fmaf_(h, fmaf_(b6, g6, fmaf_(b5, g5, fmaf_(b4, g4, fmaf_(b3, g3, b1 * g1)))), V);
+    *SE = fmaf_(e6, g6, fmaf_(e5, g5, fmaf_(e4, g4, fmaf_(e3, g3, e1 * g1))));
+}
+
+// Traveled angle with error-controlled steps, or kNoValue; *steps = step
+// attempts (accepted + rejected).  Same ray set-up, stop order and Newton
+// sphere crossing as the fixed-step path (sphere_ray_tracer.rs:60-193), with
+// the RK5 map in place of RK4.  Step control is power-of-two so every step
+// is an exact multiple of the initial one:
+//   |SE| h^2 > tolU           reject, h /= 2
+//   |SE| h^2 < tolU/64        accept, then h = min(2h, hmax)  (5th order: x32)
+//   otherwise                 accept, keep h
+template <int KIND>
+GEO_HD float geodesic_angle_adaptive(const PixelConsts& k, float st, float ct, uint32_t* steps) {
+    *steps = 0;
+    float U, V, early;
+    if (!geodesic_init(k, st, ct, &early, &U, &V)) return early;
+    const StopTest<KIND> stop_at(k);
+    const uint32_t ms = k.max_steps;
+    float h = k.step, ang = 0.0f;
+    float ou = U, ov = V, nu = U, nv = V, hc = h;
+    bool stopped = false;
+    uint32_t it = 0;
+    while (it < ms) {
+        ++it;
+        float NU, NV, SE;
+        dp5_step<KIND>(U, V, h, &NU, &NV, &SE);
+        const float err = __builtin_fabsf(SE) * (h * h);
+        if (err > k.tolU) {
+            h = h * 0.5f;
+            continue;
+        }
+        if (stop_at(NU, NV)) {
+            ou = U; ov = V; nu = NU; nv = NV; hc = h;
+            stopped = true;
+            break;
+        }
+        U = NU;
+        V = NV;
+        ang = ang + h;
+        if (err < k.tolG) {
+            const float h2 = h + h;
+            h = h2 < k.hmax ? h2 : k.hmax;
+        }
+    }
+    *steps = it;
+    if (!stopped || (nu > k.SU) == (ou > k.SU)) return kNoValue;
+    // Newton on the step length from the steeper end (:150-182)
+    float ns, wu, wv;
+    if (__builtin_fabsf(ov) > __builtin_fabsf(nv)) {
+        ns = 0.0f; wu = ou; wv = ov;
+    } else {
+        ns = hc; wu = nu; wv = nv;
+    }
+    for (int n = 0; n < kNewtonIters; ++n) {
+        ns = ns - (wu - k.SU) / wv;
+        float se;
+        dp5_step<KIND>(ou, ov, ns, &wu, &wv, &se);
+    }
+    return ang + ns;
 }
 
 // 3x3 part of a column-major mat4 times v (w = 0).

@@ -1,6 +1,7 @@
 // geo_render.hip — gfx950 kernels and the device half of the libgeo C-ABI.
 //
-//   geo_render_kernel<MODE>  per-pixel fs_main + solve_geodesic
+//   geo_render_kernel<MODE>  per-pixel fs_main + solve_geodesic (fixed RK4, fan lerp,
+//                            or error-controlled RK5(4): GEO_MODE_ADAPTIVE)
 //                            (SR/schwarzschild_sphere_shader/shader.wgsl:57-106,
 //                             SR/simulation/sphere_ray_tracer.rs:35-193)
 //   geo_fan_kernel           SphereRayTracer::solve_ray_fan in f64, one lane per node
@@ -49,7 +50,7 @@ struct RenderArgs {
     unsigned long long* step_slots;
 };
 
-// MODE: GEO_MODE_DIRECT / GEO_MODE_FAN; KIND: geo::kCurvedOut/kCurvedIn/kFlat
+// MODE: GEO_MODE_DIRECT / GEO_MODE_FAN / GEO_MODE_ADAPTIVE; KIND: geo::kCurvedOut/kCurvedIn/kFlat
 // (frame-uniform integration kind, geo::geodesic_kind; ignored in fan mode).
 // Sum of v over the 64 lanes of a fully active wave (DPP inclusive scan:
 // row_shr 1/2/4/8 within rows of 16, then row_bcast 15/31; lane 63 holds it).
@@ -89,6 +90,8 @@ __global__ __launch_bounds__(kBlock) void geo_render_kernel(const RenderArgs a) 
         float lam;
         if constexpr (MODE == GEO_MODE_FAN) {
             lam = geo::fan_lerp(s_fan, a.n_fan, st);
+        } else if constexpr (MODE == GEO_MODE_ADAPTIVE) {
+            lam = geo::kPi2 - geo::geodesic_angle_adaptive<KIND>(a.k, st, ct, &steps);
         } else {
             lam = geo::kPi2 - geo::geodesic_angle_v<GEO_LOOP_VARIANT, KIND>(a.k, st, ct, &steps);
         }
@@ -105,7 +108,7 @@ __global__ __launch_bounds__(kBlock) void geo_render_kernel(const RenderArgs a) 
         if (a.out_uv) a.out_uv[o] = make_float2(U, V);
         if (a.out_steps) a.out_steps[o] = steps;
     }
-    if constexpr (MODE == GEO_MODE_DIRECT) {
+    if constexpr (MODE != GEO_MODE_FAN) {
         if (a.step_slots) {
             // One atomic per wave (all 64 lanes active here; a wave's sum fits
             // u32: 64 x 2^20 steps at most) into one of kStepSlots sharded
@@ -396,22 +399,26 @@ static int render_impl(geo_ctx* c, const geo_frame* frame, const geo_scene* scen
                        uint32_t height, uint32_t row0, uint32_t nrows, uint32_t band_shift,
                        uint32_t band_stride, uint8_t* out_rgba8, uint8_t* out_mask, float* out_uv,
                        uint32_t* out_steps, unsigned long long* steps_total, void* stream) {
-    if (scene->mode != GEO_MODE_DIRECT && scene->mode != GEO_MODE_FAN) return GEO_EINVAL;
-    if ((scene->flags & ~GEO_FLAG_DEFER_STEPS) != 0 || scene->reserved != 0) return GEO_EINVAL;
+    if (scene->mode != GEO_MODE_DIRECT && scene->mode != GEO_MODE_FAN && scene->mode != GEO_MODE_ADAPTIVE)
+        return GEO_EINVAL;
+    if ((scene->flags & ~GEO_FLAG_DEFER_STEPS) != 0) return GEO_EINVAL;
+    const bool adaptive = scene->mode == GEO_MODE_ADAPTIVE;
+    // tol: 0 (default) or a positive finite tolerance in the adaptive mode, 0 otherwise
+    if (adaptive ? !(scene->tol >= 0.0f && scene->tol <= 3.0e38f) : scene->tol != 0.0f) return GEO_EINVAL;
     const bool defer = (scene->flags & GEO_FLAG_DEFER_STEPS) != 0;
     if (scene->max_steps > (1u << 24)) return GEO_EINVAL;  // a wave's step sum must fit u32
     if (defer && steps_total) return GEO_EINVAL;
     if (!c->sky) return GEO_ESTATE;
     if (scene->mode == GEO_MODE_FAN && (!c->fan || c->n_fan < 2)) return GEO_ESTATE;
     // bound > 0 (escape test folding, geo_pixel.h) needs r_obs > 0 and sphere_r > 0
-    if (scene->mode == GEO_MODE_DIRECT &&
+    if (scene->mode != GEO_MODE_FAN &&
         (!(scene->step > 0.0f) || !(scene->r_obs > 0.0f) || !(scene->sphere_r > 0.0f) || !(scene->rs >= 0.0f)))
         return GEO_EINVAL;
     DeviceGuard g(c->device);
     if (!g.ok) return GEO_EHIP;
     RenderArgs a;
     std::memcpy(&a.frame, frame, sizeof(geo_frame));
-    a.k = geo::make_consts(scene->rs, scene->sphere_r, scene->r_obs, scene->step, scene->max_steps);
+    a.k = geo::make_consts(scene->rs, scene->sphere_r, scene->r_obs, scene->step, scene->max_steps, scene->tol);
     a.width = width;
     a.height = height;
     a.row0 = row0;
@@ -438,6 +445,17 @@ static int render_impl(geo_ctx* c, const geo_frame* frame, const geo_scene* scen
     const dim3 grid(tiles_x, tiles_y);
     if (scene->mode == GEO_MODE_FAN) {
         hipLaunchKernelGGL((geo_render_kernel<GEO_MODE_FAN, geo::kCurvedOut>), grid, dim3(kBlock), 0, s, a);
+    } else if (adaptive) {
+        switch (geo::geodesic_kind(a.k)) {
+            case geo::kCurvedOut:
+                hipLaunchKernelGGL((geo_render_kernel<GEO_MODE_ADAPTIVE, geo::kCurvedOut>), grid, dim3(kBlock), 0, s, a);
+                break;
+            case geo::kCurvedIn:
+                hipLaunchKernelGGL((geo_render_kernel<GEO_MODE_ADAPTIVE, geo::kCurvedIn>), grid, dim3(kBlock), 0, s, a);
+                break;
+            default:
+                hipLaunchKernelGGL((geo_render_kernel<GEO_MODE_ADAPTIVE, geo::kFlat>), grid, dim3(kBlock), 0, s, a);
+        }
     } else {
         switch (geo::geodesic_kind(a.k)) {
             case geo::kCurvedOut:
@@ -451,7 +469,7 @@ static int render_impl(geo_ctx* c, const geo_frame* frame, const geo_scene* scen
         }
     }
     if (hipGetLastError() != hipSuccess) return GEO_EHIP;
-    if (steps_total && scene->mode == GEO_MODE_DIRECT) {
+    if (steps_total && scene->mode != GEO_MODE_FAN) {
         hipLaunchKernelGGL(geo_steps_finalize, dim3(1), dim3(kStepSlots), 0, s, c->step_slots,
                            steps_total);
         if (hipGetLastError() != hipSuccess) return GEO_EHIP;

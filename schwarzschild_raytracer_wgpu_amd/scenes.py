@@ -5,7 +5,7 @@ camera (PI, 0), fov PI/2, FrozenFall with E = 1: renderer.rs:83-85,
 lib.rs:72, observer.rs:70-81) is scale-invariant in rs (the RK4 step is an
 angle), so the configs use it divided by 10: rs = 1, sphere 50, observer
 (2.5, 0, 0.1).  The sky textures of the reference (.MISSING_LARGE_BLOBS) are
-absent; configs 2-4 use a synthetic equirect checkerboard with xorshift noise.
+absent; configs 2-5 use a synthetic equirect checkerboard with xorshift noise.
 """
 from __future__ import annotations
 
@@ -31,6 +31,8 @@ class SceneConfig:
     step: float = math.pi / 100.0
     sky: str = "equirect"  # or "flat"
     sky_size: tuple = (4096, 2048)
+    mode: str = "direct"  # "direct" (per-pixel fixed RK4), "fan" (reference-exact), "adaptive" (RK5(4))
+    tol: float = 0.0      # adaptive mode: local error tolerance in u (0 = 1e-6)
     extra: dict = field(default_factory=dict)
 
 
@@ -39,6 +41,12 @@ CONFIGS = {
     "cfg2_1080p": SceneConfig("cfg2_1080p", 1920, 1080, 512),
     "cfg3_4k": SceneConfig("cfg3_4k", 3840, 2160, 2048),
     "cfg4_4k_8gpu": SceneConfig("cfg4_4k_8gpu", 3840, 2160, 2048),
+    # config 5 (a build extension): 8K, error-controlled Dormand-Prince RK5(4)
+    # steps (tol 1e-6 in u, budget 2048 attempts), observer off-axis at
+    # r = 1.3 rs (inside the photon sphere; (1.2, 0.5, 0) has |pos| = 1.3
+    # exactly), camera (PI + 0.6, 0.3)
+    "cfg5_8k_adaptive": SceneConfig("cfg5_8k_adaptive", 7680, 4320, 2048, position=(1.2, 0.5, 0.0),
+                                    camera=(math.pi + 0.6, 0.3), mode="adaptive", tol=1e-6),
 }
 
 FLAT_COLOUR = (64, 128, 255, 255)

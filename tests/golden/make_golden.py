@@ -18,7 +18,8 @@ sys.path.insert(0, os.path.dirname(HERE))
 
 import oracle as O  # noqa: E402
 from helpers import default_scene  # noqa: E402
-from schwarzschild_raytracer_wgpu_amd._lib import GEO_MODE_FAN  # noqa: E402
+from schwarzschild_raytracer_wgpu_amd import make_scene  # noqa: E402
+from schwarzschild_raytracer_wgpu_amd._lib import GEO_MODE_ADAPTIVE, GEO_MODE_FAN  # noqa: E402
 from schwarzschild_raytracer_wgpu_amd.scenes import make_sky  # noqa: E402
 
 STEP = math.pi / 100
@@ -57,7 +58,23 @@ def main():
              f64_mask=p64["mask"], f64_uv=p64["uv"], f64_steps=p64["steps"], f64_lam=p64["lam"],
              f32_rgba=p32["rgba"], f32_mask=p32["mask"], f32_uv=p32["uv"], f32_steps=p32["steps"],
              fan=fan, fan_rgba=f32fan["rgba"], fan_mask=f32fan["mask"], fan_uv=f32fan["uv"])
+    adaptive()
     print("wrote", os.listdir(HERE))
+
+
+def adaptive():
+    """Config 5 at 64x36: GEO_MODE_ADAPTIVE (f32 kernel order) and its f64
+    check (fixed RK4 at step/32)."""
+    w, h = 64, 36
+    frame = oracle_frame(w, h, pos=(1.2, 0.5, 0.0), cam=(math.pi + 0.6, 0.3))
+    sc = make_scene(1.0, 50.0, 1.3, STEP, 2048, GEO_MODE_ADAPTIVE, tol=1e-6)
+    sky = make_sky("equirect", (64, 32))
+    p32 = O.render_f32(frame, sc, sky, w, h, threads=4)
+    p64 = O.render_f64(frame, sc, w, h, threads=4)
+    np.savez(os.path.join(HERE, "adaptive_64x36.npz"),
+             frame=np.frombuffer(bytes(frame), dtype=np.float32), sky=sky,
+             f32_rgba=p32["rgba"], f32_mask=p32["mask"], f32_uv=p32["uv"], f32_steps=p32["steps"],
+             f64_mask=p64["mask"], f64_uv=p64["uv"])
 
 
 if __name__ == "__main__":

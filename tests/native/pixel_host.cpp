@@ -16,11 +16,19 @@ static float geo_v(const geo::PixelConsts& k, float st, float ct, uint32_t* n) {
     }
 }
 
+static float geo_adaptive(const geo::PixelConsts& k, float st, float ct, uint32_t* n) {
+    switch (geo::geodesic_kind(k)) {
+        case geo::kCurvedOut: return geo::geodesic_angle_adaptive<geo::kCurvedOut>(k, st, ct, n);
+        case geo::kCurvedIn: return geo::geodesic_angle_adaptive<geo::kCurvedIn>(k, st, ct, n);
+        default: return geo::geodesic_angle_adaptive<geo::kFlat>(k, st, ct, n);
+    }
+}
+
 extern "C" int host_render(const geo_frame* f, const geo_scene* s, const float* fan, uint32_t n_fan,
                            const uint32_t* sky, uint32_t sw, uint32_t sh, uint32_t width, uint32_t height,
                            uint32_t row0, uint32_t nrows, uint32_t* rgba, uint8_t* mask, float* uv,
                            uint32_t* steps, int variant) {
-    const geo::PixelConsts k = geo::make_consts(s->rs, s->sphere_r, s->r_obs, s->step, s->max_steps);
+    const geo::PixelConsts k = geo::make_consts(s->rs, s->sphere_r, s->r_obs, s->step, s->max_steps, s->tol);
     bool opaque = true;
     for (size_t i = 0; i < (size_t)sw * sh; ++i) opaque = opaque && (sky[i] >> 24) == 255u;
     const float inv_w = 1.0f / (float)width, inv_h = 1.0f / (float)height;
@@ -36,6 +44,8 @@ extern "C" int host_render(const geo_frame* f, const geo_scene* s, const float* 
             float lam;
             if (s->mode == GEO_MODE_FAN)
                 lam = geo::fan_lerp(fan, n_fan, st);
+            else if (s->mode == GEO_MODE_ADAPTIVE)
+                lam = geo::kPi2 - geo_adaptive(k, st, ct, &n);
             else
                 lam = geo::kPi2 - (variant == 1 ? geo_v<1>(k, st, ct, &n) : variant == 2 ? geo_v<2>(k, st, ct, &n) : variant == 3 ? geo_v<3>(k, st, ct, &n) : geo_v<4>(k, st, ct, &n));
             const bool bh = lam < geo::kBlackHoleLambda;

@@ -249,6 +249,70 @@ def test_4k_2048_properties(geo, torch_mod):
     assert_same(sub, ref)
 
 
+def test_adaptive_golden_fixture_bitexact(geo, torch_mod):
+    z = np.load(os.path.join(GOLD, "adaptive_64x36.npz"))
+    frame = geo.GeoFrame.from_buffer_copy(z["frame"].tobytes())
+    ctx = make_ctx(geo, z["sky"])
+    scene = geo.make_scene(1.0, 50.0, 1.3, math.pi / 100, 2048, geo.GEO_MODE_ADAPTIVE, tol=1e-6)
+    hip = render(geo, torch_mod, ctx, frame, scene, 64, 36)
+    assert_same(hip, dict(rgba=z["f32_rgba"], mask=z["f32_mask"], uv=z["f32_uv"], steps=z["f32_steps"]))
+    assert np.array_equal(hip["mask"], z["f64_mask"])
+
+
+ADAPTIVE_SCENES = [
+    # name, w, h, frame kwargs, (r_obs, max_steps, tol, rs)
+    ("cfg5_small", 384, 216, dict(pos=(1.2, 0.5, 0.0), camera=(math.pi + 0.6, 0.3)), (1.3, 2048, 1e-6, 1.0)),
+    ("default_scene", 320, 180, {}, (R_OBS, 2048, 0.0, 1.0)),
+    ("tight_tol", 160, 90, {}, (R_OBS, 2048, 1e-9, 1.0)),
+    ("budget_7", 160, 90, {}, (R_OBS, 7, 1e-6, 1.0)),
+    ("inside_horizon", 128, 128, dict(pos=(0.8, 0.0, 0.05)), (math.sqrt(0.64 + 0.0025), 2048, 1e-6, 1.0)),
+    ("flat_space", 128, 72, dict(rs=0.0, state=0), (R_OBS, 2048, 1e-6, 0.0)),
+]
+
+
+@pytest.mark.parametrize("name,w,h,fk,sp", ADAPTIVE_SCENES, ids=[s[0] for s in ADAPTIVE_SCENES])
+def test_adaptive_mode_matches_oracle_bitexact(geo, torch_mod, name, w, h, fk, sp):
+    """GEO_MODE_ADAPTIVE (config 5): the kernel's RK5(4) loop == the oracle's literal adaptive loop."""
+    from schwarzschild_raytracer_wgpu_amd.scenes import make_sky
+
+    r_obs, ms, tol, rs = sp
+    sky = make_sky("equirect", (512, 256))
+    frame = default_frame(w, h, **{"rs": rs, **fk})
+    scene = geo.make_scene(rs, 50.0, r_obs, math.pi / 100, ms, geo.GEO_MODE_ADAPTIVE, tol=tol)
+    ctx = make_ctx(geo, sky)
+    hip = render(geo, torch_mod, ctx, frame, scene, w, h)
+    ref = O.render_f32(frame, scene, sky, w, h, threads=8)
+    assert_same(hip, ref)
+    assert hip["total"] == ref["steps_total"]
+
+
+def test_cfg5_8k_adaptive_properties(geo, torch_mod):
+    """Full config-5 frame (7680x4320, adaptive): deterministic, step counter
+    == sum of per-pixel attempts, sampled rows bit-exact against the oracle,
+    and the frame agrees with the fixed-step RK4 frame on the BH mask almost
+    everywhere (the two integrators differ only at the photon-ring edge)."""
+    from schwarzschild_raytracer_wgpu_amd.scenes import CONFIGS, make_sky
+
+    cfg = CONFIGS["cfg5_8k_adaptive"]
+    w, h = cfg.width, cfg.height
+    sky = make_sky("equirect", (4096, 2048))
+    frame = default_frame(w, h, pos=cfg.position, camera=cfg.camera)
+    scene = geo.make_scene(1.0, 50.0, 1.3, math.pi / 100, cfg.max_steps, geo.GEO_MODE_ADAPTIVE, tol=cfg.tol)
+    ctx = make_ctx(geo, sky)
+    a = render(geo, torch_mod, ctx, frame, scene, w, h)
+    assert a["total"] == int(a["steps"].astype(np.uint64).sum())
+    assert a["steps"].max() < cfg.max_steps
+    ref = O.render_f32(frame, scene, sky, w, h, row0=21, nrows=h // 211, row_step=211, threads=16)
+    sub = {k: a[k][21::211][: h // 211] for k in ("rgba", "mask", "uv", "steps")}
+    assert_same(sub, ref)
+    fixed = render(geo, torch_mod, ctx, frame, default_scene(2048, r_obs=1.3), w, h)
+    assert np.mean(fixed["mask"] == a["mask"]) > 0.999
+    both = (a["mask"] == 0) & (fixed["mask"] == 0)
+    assert np.percentile(wrap_du(a["uv"], fixed["uv"])[both], 99) < 1e-4
+    # ~5x fewer attempts than fixed steps
+    assert a["total"] < 0.3 * fixed["total"]
+
+
 def test_invalid_arguments(geo, torch_mod):
     from schwarzschild_raytracer_wgpu_amd import _lib
 
@@ -272,5 +336,14 @@ def test_invalid_arguments(geo, torch_mod):
     assert st == _lib.GEO_ESTATE
     with pytest.raises(geo.GeoError):
         ctx.set_fan(np.zeros(1, np.float32))
+    # tol: only in the adaptive mode, and finite >= 0 there
+    for sc in (geo.make_scene(1.0, 50.0, 2.5, math.pi / 100, 16, geo.GEO_MODE_DIRECT, tol=1e-6),
+               geo.make_scene(1.0, 50.0, 2.5, math.pi / 100, 16, geo.GEO_MODE_ADAPTIVE, tol=-1e-6),
+               geo.make_scene(1.0, 50.0, 2.5, math.pi / 100, 16, geo.GEO_MODE_ADAPTIVE, tol=float("nan")),
+               geo.make_scene(1.0, 50.0, 2.5, math.pi / 100, 16, geo.GEO_MODE_ADAPTIVE, tol=float("inf")),
+               geo.make_scene(1.0, 50.0, 2.5, math.pi / 100, 16, 3)):
+        st = _lib.lib.geo_render_rows(ctx._h, ctypes.byref(frame), ctypes.byref(sc), 8, 8, 0, 8, out.data_ptr(),
+                                      None, None, None, None, None)
+        assert st == _lib.GEO_EINVAL
     with pytest.raises(geo.GeoError):
         geo.Context(99)

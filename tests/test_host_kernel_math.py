@@ -99,3 +99,35 @@ def test_host_header_translucent_sky(host):
     b = O.render_f32(frame, scene, sky, w, h, threads=4)
     assert np.array_equal(a["rgba"], b["rgba"])
     assert np.all(b["rgba"][..., 3] == 255)
+
+
+ADAPTIVE_CASES = [
+    ("default", 160, 90, {}, dict(max_steps=2048)),
+    ("cfg5_inside_photon_sphere", 160, 90, dict(pos=(1.2, 0.5, 0.0), camera=(math.pi + 0.6, 0.3)),
+     dict(r_obs=1.3)),
+    ("budget_5", 96, 54, {}, dict(max_steps=5)),
+    ("budget_0", 32, 18, {}, dict(max_steps=0)),
+    ("tol_1e-9", 96, 54, {}, dict(tol=1e-9)),
+    ("tol_1e-3", 96, 54, {}, dict(tol=1e-3)),
+    ("inside_horizon", 64, 64, dict(pos=(0.8, 0.0, 0.05)), dict(r_obs=math.sqrt(0.64 + 0.0025))),
+    ("flat_space", 64, 36, dict(rs=0.0, state=0), dict(rs=0.0)),
+    ("outside_sphere", 64, 36, dict(pos=(60.0, 0.0, 1.0)), dict(r_obs=math.sqrt(3601.0))),
+]
+
+
+@pytest.mark.parametrize("name,w,h,fk,sk", ADAPTIVE_CASES, ids=[c[0] for c in ADAPTIVE_CASES])
+def test_host_header_adaptive_equals_oracle(host, name, w, h, fk, sk):
+    """GEO_MODE_ADAPTIVE: the header's DP5(4) loop equals the oracle's literal adaptive loop."""
+    from schwarzschild_raytracer_wgpu_amd import make_scene
+    from schwarzschild_raytracer_wgpu_amd._lib import GEO_MODE_ADAPTIVE
+
+    sky = make_sky("equirect", (128, 64))
+    p = dict(rs=1.0, r_obs=math.sqrt(2.5 ** 2 + 0.01), max_steps=2048, tol=0.0)
+    p.update(sk)
+    frame = default_frame(w, h, **fk)
+    scene = make_scene(p["rs"], 50.0, p["r_obs"], math.pi / 100, p["max_steps"], GEO_MODE_ADAPTIVE, tol=p["tol"])
+    a = run_host(host, frame, scene, sky, w, h)
+    b = O.render_f32(frame, scene, sky, w, h, threads=4)
+    for f in ("mask", "steps", "rgba"):
+        assert np.array_equal(a[f], b[f]), (f, np.argwhere(a[f] != b[f])[:5])
+    assert np.array_equal(a["uv"].view(np.uint32), b["uv"].view(np.uint32))

@@ -23,8 +23,22 @@ timeout -k 10 300 python bench.py > "$OUT/bench_$TAG.json" 2> "$OUT/bench_$TAG.e
 rc=$?; echo "bench rc=$rc"; cat "$OUT/bench_$TAG.json"; tail -3 "$OUT/bench_$TAG.err"
 if [ $rc -ne 0 ]; then exit $rc; fi
 
+# further configs (e.g. EXTRA_CONFIGS="cfg5_8k_adaptive"): bench line each
+for C in ${EXTRA_CONFIGS:-}; do
+    timeout -k 10 300 python bench.py --config "$C" > "$OUT/bench_${TAG}_$C.json" 2> "$OUT/bench_${TAG}_$C.err"
+    rc=$?; echo "bench $C rc=$rc"; cat "$OUT/bench_${TAG}_$C.json"; tail -3 "$OUT/bench_${TAG}_$C.err"
+    if [ $rc -ne 0 ]; then exit $rc; fi
+done
+
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$TAG" -o run \
     -- python3 "$ROOT/bench.py" --no-cpu-baseline > "$OUT/prof_$TAG.log" 2>&1
 rc=$?; echo "rocprof rc=$rc"; tail -3 "$OUT/prof_$TAG.log"
-exit $rc
+if [ $rc -ne 0 ]; then exit $rc; fi
+for C in ${EXTRA_CONFIGS:-}; do
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_${TAG}_$C" -o run \
+        -- python3 "$ROOT/bench.py" --no-cpu-baseline --config "$C" > "$OUT/prof_${TAG}_$C.log" 2>&1
+    rc=$?; echo "rocprof $C rc=$rc"; tail -3 "$OUT/prof_${TAG}_$C.log"
+    if [ $rc -ne 0 ]; then exit $rc; fi
+done
+exit 0

@@ -459,44 +459,42 @@ GEO_HD float geodesic_angle_adaptive(const PixelConsts& k, float st, float ct, u
     const StopTest<KIND> stop_at(k);
     const uint32_t ms = k.max_steps;
     float h = k.step, ang = 0.0f;
-    float ou = U, ov = V, nu = U, nv = V, hc = h;
+    float NU = U, NV = V;
     bool stopped = false;
     uint32_t it = 0;
+    // One exit per attempt (the stop of an accepted step); accept/reject is
+    // branch-free selects, so the wave runs one straight-line attempt per
+    // iteration.  On the stop, (U, V, h) still hold the step's start and size.
     while (it < ms) {
         ++it;
-        float NU, NV, SE;
+        float SE;
         dp5_step<KIND>(U, V, h, &NU, &NV, &SE);
         const float err = __builtin_fabsf(SE) * (h * h);
-        if (err > k.tolU) {
-            h = h * 0.5f;
-            continue;
-        }
-        if (stop_at(NU, NV)) {
-            ou = U; ov = V; nu = NU; nv = NV; hc = h;
+        const bool acc = !(err > k.tolU);
+        if (acc && stop_at(NU, NV)) {
             stopped = true;
             break;
         }
-        U = NU;
-        V = NV;
-        ang = ang + h;
-        if (err < k.tolG) {
-            const float h2 = h + h;
-            h = h2 < k.hmax ? h2 : k.hmax;
-        }
+        const float h2 = h + h;
+        const float hg = err < k.tolG ? (h2 < k.hmax ? h2 : k.hmax) : h;
+        U = acc ? NU : U;
+        V = acc ? NV : V;
+        ang = acc ? ang + h : ang;
+        h = acc ? hg : h * 0.5f;
     }
     *steps = it;
-    if (!stopped || (nu > k.SU) == (ou > k.SU)) return kNoValue;
+    if (!stopped || (NU > k.SU) == (U > k.SU)) return kNoValue;
     // Newton on the step length from the steeper end (:150-182)
     float ns, wu, wv;
-    if (__builtin_fabsf(ov) > __builtin_fabsf(nv)) {
-        ns = 0.0f; wu = ou; wv = ov;
+    if (__builtin_fabsf(V) > __builtin_fabsf(NV)) {
+        ns = 0.0f; wu = U; wv = V;
     } else {
-        ns = hc; wu = nu; wv = nv;
+        ns = h; wu = NU; wv = NV;
     }
     for (int n = 0; n < kNewtonIters; ++n) {
         ns = ns - (wu - k.SU) / wv;
         float se;
-        dp5_step<KIND>(ou, ov, ns, &wu, &wv, &se);
+        dp5_step<KIND>(U, V, ns, &wu, &wv, &se);
     }
     return ang + ns;
 }

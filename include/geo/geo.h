@@ -20,6 +20,9 @@
  *                                                                SR/simulation/sphere_ray_tracer.rs:35-56,
  *                                                                .../basic_sphere_buffer.rs:85-88
  *   geo_set_fan                RayFanTexture::update             SR/schwarzschild_sphere_shader/ray_fan_texture.rs:65-90
+ *   geo_rays_* / geo_points_*  RayConnector / PointCloud      SR/simulation/ray_connector.rs:6-157,
+ *                                                                SR/schwarzschild_point_shader/point_cloud.rs:7-156
+ *   geo_draw_points            point pipeline vs_main + fs_main  SR/schwarzschild_point_shader/shader.wgsl:36-74
  *   geo_render_rows            SchwarzschildSphereShaderDraw::draw + fs_main
  *                                                                SR/schwarzschild_sphere_shader/schwarzschild_sphere_shader_draw.rs:3-6,
  *                                                                .../basic_sphere_buffer.rs:92-100,
@@ -161,6 +164,65 @@ int geo_render_bands(geo_ctx* ctx, const geo_frame* frame, const geo_scene* scen
 /* Adds the steps accumulated under GEO_FLAG_DEFER_STEPS to *steps_total
  * (device u64) and clears the context's counter.  Asynchronous on `stream`. */
 int geo_steps_flush(geo_ctx* ctx, unsigned long long* steps_total, void* stream);
+
+/* ---- accretion-disk points ------------------------- */
+/* A batch of RayConnectors (SR/simulation/ray_connector.rs:6-25) on n points:
+ * per point a near-side connector (less_than_180 = true) and/or a far-side one
+ * (false).  Connector order: the n near-side ones, then the n far-side ones.
+ * State (48 node values per connector, needs_reset) stays on the device. */
+#define GEO_RAYS_NEAR 1u
+#define GEO_RAYS_FAR 2u
+typedef struct geo_rays geo_rays;
+typedef struct geo_points geo_points;
+
+/* RayConnector::new for every (point, side); pos_xyz: host, 3 floats per point. */
+int geo_rays_create(geo_ctx* ctx, float schwarz_r, uint32_t n_points, uint32_t sides, const float* pos_xyz,
+                    geo_rays** out);
+void geo_rays_destroy(geo_rays* rays);
+/* number of connectors */
+int geo_rays_count(const geo_rays* rays);
+/* RayConnector::set_position (:134-136) for every point (host, 3 floats per point). */
+int geo_rays_set_positions(geo_rays* rays, const float* pos_xyz);
+/* update_ray(other, iterations) (ray_connector.rs:48-132) for every connector,
+ * or reset_ray(other) (:27-44) when reset != 0.  other_xyz (host): 3 floats
+ * (one other end for all) or 3 per point when per_point != 0 (then the call
+ * synchronises `stream` after uploading them).  out_vertices: device, 4 floats
+ * per connector [x, y, z, incoming angle], or NULL for the batch's own buffer
+ * (geo_rays_vertices).  Asynchronous on `stream`. */
+int geo_rays_update(geo_rays* rays, const float* other_xyz, int per_point, uint32_t iterations, int reset,
+                    float* out_vertices, void* stream);
+const float* geo_rays_vertices(const geo_rays* rays);
+
+/* PointCloud::new (SR/schwarzschild_point_shader/point_cloud.rs:20-65): one
+ * near-side RayConnector per model vertex (host, 3 floats each), plus a
+ * far-side one when farside != 0, all reset against observer_xyz; with
+ * orbits != 0 every vertex also becomes a particle on an Orbit (f64,
+ * orbit.rs) with direction (-y, x, 0) and rotation 18 + 2 rand.  seed: the
+ * per-point random streams (wyrand) for those rotations and for respawns.
+ * Synchronous. */
+int geo_points_create(geo_ctx* ctx, float schwarz_r, const float* model_xyz, uint32_t n,
+                      const float* observer_xyz, int farside, int orbits, unsigned long long seed,
+                      geo_points** out);
+void geo_points_destroy(geo_points* pts);
+int geo_points_count(const geo_points* pts);
+/* PointCloud::update (point_cloud.rs:117-148): orbit step by dt seconds and
+ * respawn (orbits), then update_ray(observer, 1) for every connector.
+ * Asynchronous on `stream`. */
+int geo_points_update(geo_points* pts, const float* observer_xyz, double dt, void* stream);
+/* get_vertices / get_vertices_farside: device pointer, 4 floats per point
+ * (NULL for the far side of a cloud without one). */
+const float* geo_points_vertices(const geo_points* pts, int farside);
+/* current point positions (host, 3 floats per point); synchronises `stream`. */
+int geo_points_positions(const geo_points* pts, float* out_xyz, void* stream);
+
+/* The point pipeline (SR/schwarzschild_point_shader/shader.wgsl:36-74,
+ * pipeline.rs:55-74: PointList, colour (1,0,0,1), REPLACE) drawn over rows
+ * [row0, row0+nrows) of an RGBA8 frame (device, laid out as geo_render_rows'
+ * out_rgba8).  vertices: device, 4 floats each.  out_xy (device, optional):
+ * the pixel (x, y) of every vertex, (-1, -1) when clipped.  Async on `stream`. */
+int geo_draw_points(geo_ctx* ctx, const geo_frame* frame, const float* vertices, uint32_t n, uint32_t width,
+                    uint32_t height, uint32_t row0, uint32_t nrows, uint8_t* out_rgba8, int* out_xy,
+                    void* stream);
 
 /* ---- observer (host, f64; SR/simulation/observer.rs) ----------------- */
 /* Observer::new (observer.rs:68-87): pos (25,0,1), camera (PI,0), FrozenFall,

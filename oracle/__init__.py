@@ -74,6 +74,11 @@ def _load() -> ctypes.CDLL:
                                       vp, vp]),
         "geo_oracle_observer_frame": (None, [f64, f64, f64, f64, vp, f64, f64, i, f64, vp]),
         "geo_oracle_geodesic_f32": (ctypes.c_float, [vp, ctypes.c_float, ctypes.c_float, vp]),
+        "geo_oracle_rays_update": (i, [ctypes.c_float, u32, u32, vp, vp, vp, vp, i, i, i, vp, i]),
+        "geo_oracle_points_run": (i, [ctypes.c_float, vp, u32, i, i, ctypes.c_uint64, u32, vp, vp, vp, vp, vp, i]),
+        "geo_oracle_project_point": (i, [vp, vp, u32, u32, vp, vp]),
+        "geo_oracle_draw_points": (i, [vp, vp, u32, u32, u32, u32, u32, vp, vp]),
+        "geo_oracle_acosf": (ctypes.c_float, [ctypes.c_float]),
         "geo_oracle_asinf": (ctypes.c_float, [ctypes.c_float]),
         "geo_oracle_atan2f": (ctypes.c_float, [ctypes.c_float, ctypes.c_float]),
         "geo_oracle_sincosf": (None, [ctypes.c_float, vp, vp]),
@@ -199,3 +204,62 @@ def sincosf(x: float):
     s, c = ctypes.c_float(), ctypes.c_float()
     lib.geo_oracle_sincosf(x, _addr(s), _addr(c))
     return s.value, c.value
+
+
+# ---- accretion-disk points (geo_oracle_points.c) ----------------------------
+
+NR_NODES = 48
+
+
+class Rays:
+    """Host mirror of a geo_rays batch (ray_connector.rs): n points x sides
+    connectors (near side first), state u[c, 48] and needs_reset[c]."""
+
+    def __init__(self, rs, pos, sides=1, libm=True):
+        self.rs = float(rs)
+        self.pos = np.ascontiguousarray(pos, dtype=np.float32).reshape(-1, 3)
+        self.n = self.pos.shape[0]
+        self.sides = sides
+        nside = (sides & 1) + ((sides >> 1) & 1)
+        self.u = np.ones((self.n * nside, NR_NODES), np.float32)   # RayConnector::new: u_ray = 1
+        self.needs = np.ones(self.n * nside, np.uint8)             # needs_reset = true
+        self.libm = int(bool(libm))
+
+    def update(self, other, iterations=1, reset=False):
+        other = np.ascontiguousarray(other, dtype=np.float32)
+        per_point = int(other.size != 3)
+        out = np.empty((self.u.shape[0], 4), np.float32)
+        lib.geo_oracle_rays_update(self.rs, self.n, self.sides, _np(self.pos), _np(self.u), _np(self.needs),
+                                   _np(other), per_point, int(iterations), int(bool(reset)), _np(out), self.libm)
+        return out
+
+
+def points_run(rs, model, observers, dts, farside=True, orbits=True, seed=0, libm=False):
+    """PointCloud::new(model, observers[0]) then len(dts) updates; returns
+    (near (n,4), far (n,4) or None, positions (n,3))."""
+    model = np.ascontiguousarray(model, dtype=np.float32).reshape(-1, 3)
+    n = model.shape[0]
+    obs = np.ascontiguousarray(observers, dtype=np.float32).reshape(-1, 3)
+    dts = np.ascontiguousarray(dts, dtype=np.float64)
+    assert obs.shape[0] == dts.size + 1
+    near = np.empty((n, 4), np.float32)
+    far = np.empty((n, 4), np.float32) if farside else None
+    pos = np.empty((n, 3), np.float32)
+    r = lib.geo_oracle_points_run(float(rs), _np(model), n, int(farside), int(orbits), ctypes.c_uint64(seed),
+                                  dts.size, _np(obs), _np(dts), _np(near), _np(far), _np(pos), int(bool(libm)))
+    if r != 0:
+        raise RuntimeError(f"geo_oracle_points_run: {r}")
+    return near, far, pos
+
+
+def draw_points(frame, verts, width, height, rgba=None, row0=0, nrows=None):
+    """vs_main + PointList raster over an RGBA frame (rows [row0, row0+nrows));
+    returns (rgba, xy (n, 2) int32, -1 when clipped)."""
+    verts = np.ascontiguousarray(verts, dtype=np.float32).reshape(-1, 4)
+    nrows = height - row0 if nrows is None else nrows
+    if rgba is None:
+        rgba = np.zeros((nrows, width, 4), np.uint8)
+    xy = np.empty((verts.shape[0], 2), np.int32)
+    fr = as_frame(frame)
+    lib.geo_oracle_draw_points(_addr(fr), _np(verts), verts.shape[0], width, height, row0, nrows, _np(rgba), _np(xy))
+    return rgba, xy

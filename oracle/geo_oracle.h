@@ -78,7 +78,26 @@ void geo_oracle_observer_frame(double schwarz_r, double fov, double width, doubl
                                const double pos[3], double cam_phi, double cam_theta, int state,
                                double energy, geo_frame* out);
 
+/* ---- accretion-disk points (geo_oracle_points.c) ----------------------
+ * libm = 1: the C library's acosf/atanf where the reference calls
+ * f32::acos/atan (reference-faithful); 0: the kernel's polynomials (the
+ * bit-exact checker of the HIP path). */
+/* RayConnector batch, as geo_rays_update: connectors near side first; state
+ * u[c*48 + i] and needs[c] in/out; other: 3 floats or 3 per point. */
+int geo_oracle_rays_update(float rs, uint32_t n_points, uint32_t sides, const float* pos, float* u, uint8_t* needs,
+                           const float* other, int per_point, int iterations, int reset, float* out, int libm);
+/* PointCloud::new, then nframes PointCloud::update calls (observers: 3 floats
+ * for new + 3 per frame; dts per frame). */
+int geo_oracle_points_run(float rs, const float* model, uint32_t n, int farside, int orbits, uint64_t seed,
+                          uint32_t nframes, const float* observers, const double* dts, float* out_near,
+                          float* out_far, float* out_pos, int libm);
+/* vs_main + raster of one vertex / a vertex list (kernel f32 order) */
+int geo_oracle_project_point(const geo_frame* f, const float* v, uint32_t width, uint32_t height, int* ix, int* iy);
+int geo_oracle_draw_points(const geo_frame* f, const float* verts, uint32_t n, uint32_t width, uint32_t height,
+                           uint32_t row0, uint32_t nrows, uint8_t* rgba, int* out_xy);
+
 /* f32 math kernels, exported for accuracy tests */
+float geo_oracle_acosf(float x);
 float geo_oracle_asinf(float x);
 float geo_oracle_atan2f(float y, float x);
 void geo_oracle_sincosf(float x, float* s, float* c);

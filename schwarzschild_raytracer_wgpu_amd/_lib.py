@@ -25,6 +25,9 @@ GEO_ADAPTIVE_DEFAULT_TOL = 1e-6
 GEO_ADAPTIVE_MAX_GROWTH = 16
 GEO_FLAG_DEFER_STEPS = 1
 
+GEO_RAYS_NEAR = 1
+GEO_RAYS_FAR = 2
+
 GEO_OBSERVER_UNMOVING = 0
 GEO_OBSERVER_FROZEN_FALL = 1
 GEO_OBSERVER_ORBITING = 2
@@ -84,6 +87,20 @@ SIGNATURES = {
          _vp, _vp, _vp, _vp, _vp],
     ),
     "geo_steps_flush": (_int, [_vp, _vp, _vp]),
+    "geo_rays_create": (_int, [_vp, ctypes.c_float, _u32, _u32, _vp, ctypes.POINTER(_vp)]),
+    "geo_rays_destroy": (None, [_vp]),
+    "geo_rays_count": (_int, [_vp]),
+    "geo_rays_set_positions": (_int, [_vp, _vp]),
+    "geo_rays_update": (_int, [_vp, _vp, _int, _u32, _int, _vp, _vp]),
+    "geo_rays_vertices": (_vp, [_vp]),
+    "geo_points_create": (_int, [_vp, ctypes.c_float, _vp, _u32, _vp, _int, _int, ctypes.c_ulonglong,
+                                 ctypes.POINTER(_vp)]),
+    "geo_points_destroy": (None, [_vp]),
+    "geo_points_count": (_int, [_vp]),
+    "geo_points_update": (_int, [_vp, _vp, _f64, _vp]),
+    "geo_points_vertices": (_vp, [_vp, _int]),
+    "geo_points_positions": (_int, [_vp, _vp, _vp]),
+    "geo_draw_points": (_int, [_vp, ctypes.POINTER(GeoFrame), _vp, _u32, _u32, _u32, _u32, _u32, _vp, _vp, _vp]),
     "geo_observer_create": (_int, [_f64, _f64, _f64, _f64, ctypes.POINTER(_vp)]),
     "geo_observer_destroy": (None, [_vp]),
     "geo_observer_set_position": (_int, [_vp, _f64, _f64, _f64]),

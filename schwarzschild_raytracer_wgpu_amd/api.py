@@ -4,7 +4,9 @@ over the libgeo C-ABI.  Names and argument meaning follow the Rust sources:
   Observer            SR/simulation/observer.rs:42-297
   SphereRayTracer     SR/simulation/sphere_ray_tracer.rs:12-56
   BasicSphereBuffer   SR/schwarzschild_sphere_shader/sphere_buffer/basic_sphere_buffer.rs:12-101
-  Renderer.render     SR/renderer/renderer.rs:208-283 (sphere pass only)
+  RayConnectors       SR/simulation/ray_connector.rs:6-157 (a device batch)
+  PointCloud          SR/schwarzschild_point_shader/point_cloud.rs:7-156
+  Renderer.render     SR/renderer/renderer.rs:208-283 (sphere pass + point pass)
 
 Device buffers are torch tensors (PyTorch is plumbing here: device memory and
 streams); every compute call goes to the HIP kernels in libgeo.so.
@@ -256,15 +258,183 @@ class BasicSphereBuffer:
                              target.mask, target.uv, target.steps, target.steps_total, stream)
 
 
+def _hip():
+    """The HIP runtime torch loaded (the libamdhip64.so.7 soname), for raw
+    device copies of library-owned buffers."""
+    global _HIP
+    if _HIP is None:
+        import torch  # noqa: F401
+
+        h = ctypes.CDLL("libamdhip64.so.7")
+        h.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+        _HIP = h
+    return _HIP
+
+
+_HIP = None
+
+
+def _f32x3(v) -> ctypes.Array:
+    a = np.ascontiguousarray(v, dtype=np.float32).reshape(-1)
+    if a.size != 3:
+        raise ValueError("expected 3 floats")
+    return (ctypes.c_float * 3)(*a.tolist())
+
+
+class RayConnectors:
+    """A device batch of RayConnector (ray_connector.rs:6-157) on n points: a
+    near-side connector (less_than_180 = true) per point and/or a far-side
+    one.  RayConnector::new(schwarz_r, pos, less_than_180) for every
+    (point, side); `update_ray` / `reset_ray` run the HIP kernel over all
+    connectors (near side first) into `self.vertices` (device, (count, 4):
+    [x, y, z, incoming angle])."""
+
+    def __init__(self, ctx: Context, schwarz_r: float, positions, sides: int = _lib.GEO_RAYS_NEAR):
+        import torch
+
+        pos = np.ascontiguousarray(positions, dtype=np.float32).reshape(-1, 3)
+        self.ctx, self.n_points = ctx, pos.shape[0]
+        h = ctypes.c_void_p()
+        check("geo_rays_create", lib.geo_rays_create(ctx._h, schwarz_r, self.n_points, sides, pos.ctypes.data,
+                                                     ctypes.byref(h)))
+        self._h = h
+        self.count = lib.geo_rays_count(h)
+        self.vertices = torch.empty((self.count, 4), dtype=torch.float32, device=f"cuda:{ctx.device}")
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            lib.geo_rays_destroy(h)
+            self._h = None
+
+    def set_positions(self, positions) -> None:
+        pos = np.ascontiguousarray(positions, dtype=np.float32).reshape(-1, 3)
+        assert pos.shape[0] == self.n_points
+        check("geo_rays_set_positions", lib.geo_rays_set_positions(self._h, pos.ctypes.data))
+
+    def _call(self, other, iterations: int, reset: bool, stream):
+        o = np.ascontiguousarray(other, dtype=np.float32).reshape(-1)
+        per_point = o.size != 3
+        if per_point and o.size != 3 * self.n_points:
+            raise ValueError("other: 3 floats or 3 per point")
+        check("geo_rays_update", lib.geo_rays_update(self._h, o.ctypes.data, int(per_point), iterations,
+                                                     int(reset), _ptr(self.vertices), _stream_handle(stream)))
+        return self.vertices
+
+    def update_ray(self, other_position, iterations: int = 1, stream=None):
+        """update_ray(other, iterations) for every connector (one other end for
+        all, or one per point)."""
+        return self._call(other_position, iterations, False, stream)
+
+    def reset_ray(self, other_position, stream=None):
+        return self._call(other_position, 0, True, stream)
+
+
+class PointCloud:
+    """PointCloud (point_cloud.rs:7-156) on the device: RayConnectors for the
+    near (and far) side of every model vertex, optionally driven by f64
+    orbits with respawn.  Randomness: per-point wyrand streams from `seed`."""
+
+    def __init__(self, ctx: Context, model_vertices, schwarz_r: float, observer_pos, activate_farside: bool,
+                 activate_orbits: bool, seed: int = 0):
+        model = np.ascontiguousarray(model_vertices, dtype=np.float32).reshape(-1, 3)
+        self.ctx, self.n = ctx, model.shape[0]
+        self.has_farside = bool(activate_farside)
+        h = ctypes.c_void_p()
+        check("geo_points_create", lib.geo_points_create(ctx._h, schwarz_r, model.ctypes.data, self.n,
+                                                         _f32x3(observer_pos), int(activate_farside),
+                                                         int(activate_orbits), seed, ctypes.byref(h)))
+        self._h = h
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            lib.geo_points_destroy(h)
+            self._h = None
+
+    # model generators (point_cloud.rs:67-115)
+    @classmethod
+    def new_spiral(cls, ctx: Context, schwarz_r: float, observer_pos, activate_farside: bool) -> "PointCloud":
+        n = 10000
+        t = np.arange(n, dtype=np.float32) / np.float32(n) * np.float32(2 * math.pi + 0.05)
+        r = np.float32(16) + np.float32(2) * t
+        pts = np.stack([-r * np.cos(np.float32(10) * t), -r * np.sin(np.float32(10) * t),
+                        np.full(n, 0.001, np.float32)], 1)
+        return cls(ctx, pts, schwarz_r, observer_pos, activate_farside, False)
+
+    @classmethod
+    def new_accretion_disk(cls, ctx: Context, schwarz_r: float, observer_pos, activate_farside: bool,
+                           seed: int = 0, n: int = 5000) -> "PointCloud":
+        rng = np.random.default_rng(seed)
+        r = 16.0 + 10.0 * rng.random(n)
+        phi = rng.random(n) * 2 * math.pi
+        theta = 0.2 * (rng.random(n) - 0.5)
+        pts = np.stack([r * np.cos(phi) * np.cos(theta), r * np.sin(phi) * np.cos(theta), r * np.sin(theta)], 1)
+        return cls(ctx, pts.astype(np.float32), schwarz_r, observer_pos, activate_farside, True, seed)
+
+    @classmethod
+    def new_heart(cls, ctx: Context, schwarz_r: float, observer_pos, activate_farside: bool) -> "PointCloud":
+        n = 4000
+        t = np.arange(n, dtype=np.float32) / np.float32(n) * np.float32(2 * math.pi)
+        pts = np.stack([np.full(n, 11.0, np.float32), np.float32(16) * np.sin(t) ** 3,
+                        np.float32(13) * np.cos(t) - np.float32(5) * np.cos(2 * t) - np.float32(2) * np.cos(3 * t)
+                        - np.cos(4 * t)], 1)
+        return cls(ctx, pts.astype(np.float32), schwarz_r, observer_pos, activate_farside, False)
+
+    def update(self, observer_pos, dt: float, stream=None) -> None:
+        """PointCloud::update (:117-148): orbits step + respawn, update_ray(observer, 1)."""
+        check("geo_points_update", lib.geo_points_update(self._h, _f32x3(observer_pos), dt,
+                                                         _stream_handle(stream)))
+
+    def vertices_ptr(self, farside: bool = False) -> int:
+        p = lib.geo_points_vertices(self._h, int(farside))
+        if not p:
+            raise ValueError("no far side")
+        return p
+
+    def get_vertices(self, farside: bool = False) -> np.ndarray:
+        """Host copy of get_vertices / get_vertices_farside ((n, 4) f32); synchronises."""
+        import torch
+
+        torch.cuda.synchronize()
+        out = np.empty((self.n, 4), np.float32)
+        if _hip().hipMemcpy(out.ctypes.data, self.vertices_ptr(farside), out.nbytes, 2) != 0:  # DeviceToHost
+            raise RuntimeError("hipMemcpy")
+        return out
+
+    def positions(self, stream=None) -> np.ndarray:
+        out = np.empty((self.n, 3), np.float32)
+        check("geo_points_positions", lib.geo_points_positions(self._h, out.ctypes.data, _stream_handle(stream)))
+        return out
+
+    def draw(self, frame: GeoFrame, target: "RenderTarget", out_xy=None, stream=None) -> None:
+        """The point pipeline over the target (both vertex buffers)."""
+        for far in ((False, True) if self.has_farside else (False,)):
+            draw_points(self.ctx, frame, self.vertices_ptr(far), self.n, target, out_xy=out_xy, stream=stream)
+
+
+def draw_points(ctx: Context, frame: GeoFrame, vertices, n: int, target: "RenderTarget", row0: int = 0,
+                nrows: int | None = None, out_xy=None, stream=None) -> None:
+    """geo_draw_points: vs_main + PointList raster (shader.wgsl:36-74) of n
+    vertices (device pointer or tensor, 4 floats each) over target rows."""
+    nrows = target.height - row0 if nrows is None else nrows
+    vp = vertices if isinstance(vertices, int) else _ptr(vertices)
+    check("geo_draw_points", lib.geo_draw_points(ctx._h, ctypes.byref(frame), vp, n, target.width, target.height,
+                                                 row0, nrows, _ptr(target.rgba), _ptr(out_xy),
+                                                 _stream_handle(stream)))
+
+
 class Renderer:
-    """The sphere pass of Renderer::render (renderer.rs:208-258): clear to
-    (0,0,0,1), then draw each sphere over the whole target."""
+    """Renderer::render (renderer.rs:208-258): the spheres, then the point
+    meshes (near and far vertex buffers of each PointCloud) over the target."""
 
     def __init__(self, observer: Observer):
         self.observer = observer
 
-    def render(self, spheres, target: RenderTarget, stream=None) -> GeoFrame:
+    def render(self, spheres, target: RenderTarget, point_clouds=(), stream=None) -> GeoFrame:
         frame = self.observer.calc_transformation_pipeline()
         for s in spheres:
             s.draw(frame, target, stream=stream)
+        for pc in point_clouds:
+            pc.draw(frame, target, stream=stream)
         return frame

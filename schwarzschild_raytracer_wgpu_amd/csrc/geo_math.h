@@ -15,7 +15,8 @@
 // tests/test_math.py (<= 3 ulp / 2e-7 abs on the ranges used).
 #pragma once
 
-#if defined(__HIPCC__) || defined(__HIP__)
+#if defined(__HIP__)  // HIP language mode (hipcc compiles .cpp as HIP too)
+#include <hip/hip_runtime.h>
 #define GEO_HD __host__ __device__ __forceinline__
 #define GEO_HDM __host__ __device__ __forceinline__  // member functions
 #else
@@ -95,5 +96,22 @@ GEO_HD float atan2f_(float y, float x) {
     r = (x < 0.0f) ? kPi - r : r;
     return __builtin_copysignf(r, y);
 }
+
+// acos(x) for x in [-1, 1] (clamped), from the asin kernel:
+// |x| <= 1/2: pi/2 - asin(x); else 2 asin(sqrt((1 - |x|)/2)) (reflected for x < 0).
+GEO_HD float acosf_(float x) {
+    x = clampf_(x, -1.0f, 1.0f);
+    const float a = __builtin_fabsf(x);
+    if (a <= 0.5f) return kPi2 - asinf_(x);
+    const float z = 0.5f * (1.0f - a);
+    const float s = __builtin_sqrtf(z);
+    const float p = fmaf_(fmaf_(fmaf_(fmaf_(4.2163199048e-2f, z, 2.4181311049e-2f), z,
+                                      4.5470025998e-2f), z, 7.4953002686e-2f), z,
+                          1.6666752422e-1f);
+    const float r = 2.0f * fmaf_(p * z, s, s);
+    return x > 0.0f ? r : kPi - r;
+}
+
+GEO_HD float atanf_(float x) { return atan2f_(x, 1.0f); }
 
 }  // namespace geo

@@ -20,6 +20,7 @@
 #include <new>
 
 #include "../../include/geo/geo.h"
+#include "geo_ctx.h"
 #include "geo_pixel.h"
 
 namespace {
@@ -250,32 +251,6 @@ __global__ void geo_fan_kernel(double sphere_r, double schwarz_r, uint32_t max_i
 
 }  // namespace
 
-struct geo_ctx {
-    int device;
-    int num_cus;
-    uint32_t* sky;
-    uint32_t sky_w, sky_h;
-    bool sky_opaque;
-    float* fan;
-    uint32_t fan_cap, n_fan;
-    unsigned long long* step_slots;
-};
-
-namespace {
-
-struct DeviceGuard {
-    int prev = -1;
-    bool ok = false;
-    explicit DeviceGuard(int dev) {
-        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
-        ok = hipSetDevice(dev) == hipSuccess;
-    }
-    ~DeviceGuard() {
-        if (prev >= 0) (void)hipSetDevice(prev);
-    }
-};
-
-}  // namespace
 
 extern "C" {
 

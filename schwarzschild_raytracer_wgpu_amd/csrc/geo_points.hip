@@ -71,13 +71,19 @@ struct RaysArgs {
     float ox, oy, oz;            // the other end, when `other` is null
     const float* other;          // per-point other ends (x,y,z interleaved) or null
     const float* pos;            // SoA x[n] y[n] z[n]
-    const uint8_t* respawn;      // per point: reset at respawn_pos first (PointCloud::update), or null
+    const uint8_t* respawn;      // per point: respawned this frame (RESPAWN pass only)
     const float* respawn_pos;    // SoA
     float* u;                    // [48][n_conn]
     uint8_t* needs_reset;        // [n_conn]
     float4* out;                 // [n_conn]
 };
 
+// RESPAWN = false: one RayConnector call per connector (update_ray / reset_ray).
+// RESPAWN = true: the respawn pre-pass of PointCloud::update with orbits
+// (point_cloud.rs:129-134) — only the connectors of respawned points run, a
+// reset_ray at the new position; the regular pass follows.  Two launches keep
+// one solve per lane (VGPR budget: 48 nodes + 46 + 46 Thomas values).
+template <bool RESPAWN>
 __global__ __launch_bounds__(kRaysBlock) void geo_rays_kernel(const RaysArgs a) {
     const uint32_t c = blockIdx.x * kRaysBlock + threadIdx.x;
     if (c >= a.n_conn) return;
@@ -85,9 +91,10 @@ __global__ __launch_bounds__(kRaysBlock) void geo_rays_kernel(const RaysArgs a) 
     const bool far = a.sides == GEO_RAYS_FAR ? true : c >= a.n_points;
     const uint32_t p = c >= a.n_points ? c - a.n_points : c;
     const uint32_t n = a.n_points;
+    if (RESPAWN && !a.respawn[p]) return;
+    float* const ug = a.u + c;
+    const size_t stride = a.n_conn;
     float u[geo::kRayNodes];
-#pragma unroll
-    for (int i = 0; i < geo::kRayNodes; ++i) u[i] = a.u[(size_t)i * a.n_conn + c];
     bool needs = a.needs_reset[c] != 0;
     float ox = a.ox, oy = a.oy, oz = a.oz;
     if (a.other) {
@@ -95,15 +102,14 @@ __global__ __launch_bounds__(kRaysBlock) void geo_rays_kernel(const RaysArgs a) 
         oy = a.other[3 * (size_t)p + 1];
         oz = a.other[3 * (size_t)p + 2];
     }
-    if (a.respawn && a.respawn[p])
-        (void)geo::ray_connect(a.rs, !far, a.respawn_pos[p], a.respawn_pos[n + p], a.respawn_pos[2 * n + p], ox, oy,
-                               oz, true, 0u, &needs, u);
-    const float px = a.pos[p], py = a.pos[n + p], pz = a.pos[2 * n + p];
-    const float angle = geo::ray_connect(a.rs, !far, px, py, pz, ox, oy, oz, a.reset != 0, a.iterations, &needs, u);
+    const float* src = RESPAWN ? a.respawn_pos : a.pos;
+    const float px = src[p], py = src[n + p], pz = src[2 * n + p];
+    const float angle = geo::ray_connect(a.rs, !far, px, py, pz, ox, oy, oz, RESPAWN || a.reset != 0,
+                                         a.iterations, &needs, [=](int i) { return ug[(size_t)i * stride]; }, u);
 #pragma unroll
-    for (int i = 0; i < geo::kRayNodes; ++i) a.u[(size_t)i * a.n_conn + c] = u[i];
+    for (int i = 0; i < geo::kRayNodes; ++i) ug[(size_t)i * stride] = u[i];
     a.needs_reset[c] = needs ? 1 : 0;
-    if (a.out) a.out[c] = make_float4(px, py, pz, angle);
+    if (!RESPAWN && a.out) a.out[c] = make_float4(px, py, pz, angle);
 }
 
 // PointCloud::update, orbit half (point_cloud.rs:119-141): step, then respawn
@@ -240,7 +246,12 @@ int rays_launch(geo_rays* r, float ox, float oy, float oz, const float* other_de
     a.needs_reset = r->needs_reset;
     a.out = out ? reinterpret_cast<float4*>(out) : r->verts;
     if (r->n_conn == 0) return GEO_OK;
-    hipLaunchKernelGGL(geo_rays_kernel, dim3((r->n_conn + kRaysBlock - 1) / kRaysBlock), dim3(kRaysBlock), 0, s, a);
+    const dim3 grid((r->n_conn + kRaysBlock - 1) / kRaysBlock);
+    if (with_respawn) {
+        hipLaunchKernelGGL(geo_rays_kernel<true>, grid, dim3(kRaysBlock), 0, s, a);
+        if (hipGetLastError() != hipSuccess) return GEO_EHIP;
+    }
+    hipLaunchKernelGGL(geo_rays_kernel<false>, grid, dim3(kRaysBlock), 0, s, a);
     return hipGetLastError() == hipSuccess ? GEO_OK : GEO_EHIP;
 }
 

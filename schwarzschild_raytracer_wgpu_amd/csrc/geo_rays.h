@@ -71,17 +71,20 @@ GEO_HD float calc_ray_angle(float rs, bool lt180, float u_bar, float r) {
 // One RayConnector call for a connector at (px,py,pz) and the other end
 // (ox,oy,oz): reset_ray(other) when `reset`, else update_ray(other, iterations)
 // (which resets by itself when needs_reset is set or the other end jumped by
-// more than 0.5).  u: the connector's 48 node values (in/out).  Returns the
+// more than 0.5).  load(i): the connector's stored node value i, read only
+// when no reset replaces it (so the stored and the reset values are never
+// live together); u: the 48 node values after the call.  Returns the
 // incoming angle (vertex w).
+template <typename Load>
 GEO_HD float ray_connect(float rs, bool lt180, float px, float py, float pz, float ox, float oy, float oz,
-                         bool reset, uint32_t iterations, bool* needs_reset, float* u) {
+                         bool reset, uint32_t iterations, bool* needs_reset, Load load, float* u) {
     float phi = angle_between_(px, py, pz, ox, oy, oz);  // last_phi (:31-34, :53-56)
     if (!lt180) phi = kTauF - phi;
     bool do_reset = reset || *needs_reset;
     if (!do_reset && !(phi < kSmallestAngle)) {
         // the jump test of update_ray (:82-84)
         const float u0 = 1.0f / len3_(ox, oy, oz);
-        if (__builtin_fabsf(1.0f / u0 - 1.0f / u[0]) > 0.5f) do_reset = true;
+        if (__builtin_fabsf(1.0f / u0 - 1.0f / load(0)) > 0.5f) do_reset = true;
     }
     if (do_reset) {
         // reset_ray (:28-40): linear initial guess between the two ends
@@ -93,6 +96,9 @@ GEO_HD float ray_connect(float rs, bool lt180, float px, float py, float pz, flo
             const float w = (float)i / (float)(kRayNodes - 1);
             u[i] = u0 * (1.0f - w) + u1 * w;
         }
+    } else {
+#pragma unroll
+        for (int i = 0; i < kRayNodes; ++i) u[i] = load(i);
     }
     if (phi < kSmallestAngle) {
         // nearly straight ray (:61-76): no solve; reset on the next call

@@ -66,6 +66,12 @@ typedef enum geo_status {
 #define GEO_FLAG_DEFER_STEPS 1u /* executed steps accumulate in the context (no per-call
                                    fold); read them with geo_steps_flush.  steps_total
                                    must then be NULL. */
+#define GEO_FLAG_COMPOSITE 2u   /* draw OVER the current contents of out_rgba8 with the
+                                   reference's alpha blending (BlendState::ALPHA_BLENDING,
+                                   pipeline.rs:49) and leave discarded (black-hole / no-hit)
+                                   pixels untouched: the 2nd, 3rd... sphere of a frame
+                                   (lib.rs:67-89).  Without it a sphere is drawn over the
+                                   cleared target (0,0,0,1). */
 
 /* Observer motion states, ObserverState (SR/simulation/observer.rs:12-16). */
 #define GEO_OBSERVER_UNMOVING 0

@@ -174,12 +174,14 @@ def render_f64(frame, scene, width, height, row0=0, nrows=None, fan=None, thread
 
 
 def render_f32(frame, scene, sky, width, height, row0=0, nrows=None, row_step=1, fan=None, threads=8,
-               want_uv=True, want_steps=True):
+               want_uv=True, want_steps=True, target=None):
+    """target: the (nrows, width, 4) image a GEO_FLAG_COMPOSITE scene draws over (copied)."""
     nrows = height - row0 if nrows is None else nrows
     fr, sc = as_frame(frame), as_scene(scene)
     sky_a = np.ascontiguousarray(sky, dtype=np.uint8)
     fan_a = None if fan is None else np.ascontiguousarray(fan, dtype=np.float32)
-    rgba = np.empty((nrows, width, 4), np.uint8)
+    rgba = np.zeros((nrows, width, 4), np.uint8) if target is None else np.array(target, np.uint8).reshape(
+        nrows, width, 4)
     mask = np.empty((nrows, width), np.uint8)
     uv = np.empty((nrows, width, 2), np.float32) if want_uv else None
     steps = np.empty((nrows, width), np.uint32) if want_steps else None

@@ -542,8 +542,9 @@ static inline void m3vf(const float* m, float x, float y, float z, float* o) {
 
 
 static void pixel_f32(const geo_frame* f, const fconsts* k, int mode, const float* fan, uint32_t n_fan,
-                      const uint32_t* sky, uint32_t sw, uint32_t sh, int opaque, uint32_t width, uint32_t height,
-                      uint32_t px, uint32_t py, uint32_t* rgba, uint8_t* bh_out, float* uv, uint32_t* steps) {
+                      const uint32_t* sky, uint32_t sw, uint32_t sh, int opaque, int composite, uint32_t width,
+                      uint32_t height, uint32_t px, uint32_t py, uint32_t* rgba, uint8_t* bh_out, float* uv,
+                      uint32_t* steps) {
     const float* m0 = f->display_to_movement;
     float nx = ((float)(2u * px + 1u) - (float)width) * (1.0f / (float)width);
     float ny = ((float)height - (float)(2u * py + 1u)) * (1.0f / (float)height);
@@ -596,7 +597,7 @@ static void pixel_f32(const geo_frame* f, const fconsts* k, int mode, const floa
     uv[1] = V;
     *bh_out = (uint8_t)bh;
     if (bh) {
-        *rgba = 0xFF000000u;
+        if (!composite) *rgba = 0xFF000000u; /* composite: a discarded fragment keeps the target */
         return;
     }
     /* bilinear LOD-0, U wraps, V clamps, 8-bit sub-texel weights; per
@@ -625,13 +626,19 @@ static void pixel_f32(const geo_frame* f, const fconsts* k, int mode, const floa
         uint32_t bot = (v01 * (256u - wx) + v11 * wx) >> 8;
         c[ch] = (top * (256u - wy) + bot * wy + 128u) >> 8;
     }
-    if (!opaque) {
-        for (int ch = 0; ch < 3; ++ch) {
-            uint32_t p = c[ch] * c[3] + 128u;
-            c[ch] = (p + (p >> 8)) >> 8;
-        }
+    /* BlendState::ALPHA_BLENDING (pipeline.rs:49) over the target d, 8-bit
+     * fixed point: rgb = round((s a + d (255 - a))/255), alpha = round((255 a
+     * + d_a (255 - a))/255); without GEO_FLAG_COMPOSITE d = the clear colour
+     * (0,0,0,255). */
+    uint32_t dst = composite ? *rgba : 0xFF000000u;
+    uint32_t a = c[3], out[4];
+    for (int ch = 0; ch < 4; ++ch) {
+        uint32_t sv = ch < 3 ? c[ch] : 255u;
+        uint32_t p = sv * a + ((dst >> (8 * ch)) & 255u) * (255u - a) + 128u;
+        out[ch] = (p + (p >> 8)) >> 8;
     }
-    *rgba = c[0] | (c[1] << 8) | (c[2] << 16) | (255u << 24);
+    (void)opaque; /* all-opaque skies take the same formula (a = 255: out = s) */
+    *rgba = out[0] | (out[1] << 8) | (out[2] << 16) | (out[3] << 24);
 }
 
 typedef struct {
@@ -662,8 +669,9 @@ static void* job_f32(void* arg) {
             uint32_t rgba, st;
             uint8_t bh;
             float uv[2];
-            pixel_f32(j->f, &j->k, (int)j->s->mode, j->fan, j->n_fan, j->sky, j->sw, j->sh, j->opaque, j->width, j->height,
-                      px, py, &rgba, &bh, uv, &st);
+            memcpy(&rgba, j->rgba + 4 * o, 4); /* the target, for GEO_FLAG_COMPOSITE */
+            pixel_f32(j->f, &j->k, (int)j->s->mode, j->fan, j->n_fan, j->sky, j->sw, j->sh, j->opaque,
+                      (j->s->flags & GEO_FLAG_COMPOSITE) != 0, j->width, j->height, px, py, &rgba, &bh, uv, &st);
             memcpy(j->rgba + 4 * o, &rgba, 4);
             if (j->mask) j->mask[o] = bh;
             if (j->uv) {

@@ -219,14 +219,18 @@ class RenderTarget:
 
 class BasicSphereBuffer:
     """BasicSphereBuffer::new(..., sphere_radius, schwarz_radius, texture_image)
-    (basic_sphere_buffer.rs:21-60): N = 400 fan nodes, max_iter 1000, step PI/100."""
+    (basic_sphere_buffer.rs:21-60): N = 400 fan nodes, max_iter 1000, step PI/100.
+    A sphere owns its Context (its texture and ray fan live there, as the
+    reference's per-sphere bind groups do): pass a device index, or a Context
+    no other sphere uses."""
 
     NR_NODES_HALF = 200
     MAX_ITER = 1000
     STEP = math.pi / 100.0
 
-    def __init__(self, ctx: Context, sphere_radius: float, schwarz_radius: float, texture_rgba: np.ndarray,
+    def __init__(self, ctx: Context | int, sphere_radius: float, schwarz_radius: float, texture_rgba: np.ndarray,
                  max_iter: int = MAX_ITER, step: float = STEP, mode: int = _lib.GEO_MODE_DIRECT):
+        ctx = Context(ctx) if isinstance(ctx, int) else ctx
         self.ctx = ctx
         self.sphere_radius = sphere_radius
         self.schwarz_radius = schwarz_radius
@@ -251,10 +255,14 @@ class BasicSphereBuffer:
                           self.mode)
 
     def draw(self, frame: GeoFrame, target: RenderTarget, row0: int = 0, nrows: int | None = None,
-             stream=None) -> None:
-        """SchwarzschildSphereShaderDraw::draw + fs_main over rows [row0, row0+nrows)."""
+             stream=None, composite: bool = False) -> None:
+        """SchwarzschildSphereShaderDraw::draw + fs_main over rows [row0, row0+nrows);
+        composite: alpha-blend over the target's contents (a 2nd/3rd sphere)."""
         nrows = target.height - row0 if nrows is None else nrows
-        self.ctx.render_rows(frame, self.scene(), target.width, target.height, row0, nrows, target.rgba,
+        scene = self.scene()
+        if composite:
+            scene.flags |= _lib.GEO_FLAG_COMPOSITE
+        self.ctx.render_rows(frame, scene, target.width, target.height, row0, nrows, target.rgba,
                              target.mask, target.uv, target.steps, target.steps_total, stream)
 
 
@@ -425,16 +433,18 @@ def draw_points(ctx: Context, frame: GeoFrame, vertices, n: int, target: "Render
 
 
 class Renderer:
-    """Renderer::render (renderer.rs:208-258): the spheres, then the point
-    meshes (near and far vertex buffers of each PointCloud) over the target."""
+    """Renderer::render (renderer.rs:208-258): clear to (0,0,0,1), the spheres
+    in order with alpha blending (the first over the cleared target, the rest
+    GEO_FLAG_COMPOSITE over the previous ones), then the point meshes (near and
+    far vertex buffers of each PointCloud) over the target."""
 
     def __init__(self, observer: Observer):
         self.observer = observer
 
     def render(self, spheres, target: RenderTarget, point_clouds=(), stream=None) -> GeoFrame:
         frame = self.observer.calc_transformation_pipeline()
-        for s in spheres:
-            s.draw(frame, target, stream=stream)
+        for i, s in enumerate(spheres):
+            s.draw(frame, target, stream=stream, composite=i > 0)
         for pc in point_clouds:
             pc.draw(frame, target, stream=stream)
         return frame

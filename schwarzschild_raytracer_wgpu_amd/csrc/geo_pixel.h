@@ -573,20 +573,18 @@ GEO_HD void sky_uv(const float* m2, float c2x, float c2y, float rho, float lam, 
 
 // LOD-0 bilinear sample of an RGBA8 equirect (U wraps, V clamps) with 8-bit
 // sub-texel weights, as texture units do, on packed channel pairs
-// (R|B and G|A in the two 16-bit halves of a u32; no field overflows), then
-// the reference's alpha blend over the clear colour (0,0,0,1): rgb*a/255,
-// alpha 1 (pipeline.rs:49, renderer.rs:233-238).  `opaque` (every texel
-// alpha 255, checked on upload) skips the blend, which is exact there.
+// (R|B and G|A in the two 16-bit halves of a u32; no field overflows).
 GEO_HD uint32_t rb_(uint32_t t) { return t & 0x00FF00FFu; }
 GEO_HD uint32_t ga_(uint32_t t) { return (t >> 8) & 0x00FF00FFu; }
 GEO_HD uint32_t lerp2_(uint32_t a, uint32_t b, uint32_t ia, uint32_t wb) { return a * ia + b * wb; }
-GEO_HD uint32_t blend255_(uint32_t c, uint32_t a) {  // round(c*a/255) for c, a <= 255
-    const uint32_t p = c * a + 128u;
+GEO_HD uint32_t div255_(uint32_t v) {  // round(v / 255) for v <= 255 * 255
+    const uint32_t p = v + 128u;
     return (p + (p >> 8)) >> 8;
 }
+GEO_HD uint32_t blend255_(uint32_t c, uint32_t a) { return div255_(c * a); }  // round(c*a/255)
 
 template <typename Fetch>
-GEO_HD uint32_t sample_sky(Fetch fetch, uint32_t tw, uint32_t th, bool opaque, float U, float V) {
+GEO_HD uint32_t sample_sky_raw(Fetch fetch, uint32_t tw, uint32_t th, float U, float V) {
     const float x = fmaf_(U, (float)tw, -0.5f);
     const float y = fmaf_(V, (float)th, -0.5f);
     const float fx0 = __builtin_floorf(x);
@@ -615,10 +613,31 @@ GEO_HD uint32_t sample_sky(Fetch fetch, uint32_t tw, uint32_t th, bool opaque, f
     const uint32_t bga = (lerp2_(ga_(t01), ga_(t11), iwx, wx) >> 8) & 0x00FF00FFu;
     const uint32_t crb = ((lerp2_(trb, brb, iwy, wy) + 0x00800080u) >> 8) & 0x00FF00FFu;
     const uint32_t cga = ((lerp2_(tga, bga, iwy, wy) + 0x00800080u) >> 8) & 0x00FF00FFu;
-    if (opaque) return crb | (cga << 8) | 0xFF000000u;
-    const uint32_t a = cga >> 16;
-    return blend255_(crb & 0xFFu, a) | (blend255_(cga & 0xFFu, a) << 8) | (blend255_(crb >> 16, a) << 16) |
-           0xFF000000u;
+    return crb | (cga << 8);
+}
+
+// The reference's alpha blend (BlendState::ALPHA_BLENDING, pipeline.rs:49) in
+// 8-bit fixed point of a sample s over the target pixel d:
+//   rgb = round((s.rgb a + d.rgb (255 - a)) / 255),  alpha = round(a + d.a (255 - a) / 255).
+GEO_HD uint32_t composite_(uint32_t s, uint32_t d) {
+    const uint32_t a = s >> 24, ia = 255u - a;
+    const uint32_t r = div255_((s & 0xFFu) * a + (d & 0xFFu) * ia);
+    const uint32_t g = div255_(((s >> 8) & 0xFFu) * a + ((d >> 8) & 0xFFu) * ia);
+    const uint32_t b = div255_(((s >> 16) & 0xFFu) * a + ((d >> 16) & 0xFFu) * ia);
+    const uint32_t al = div255_(a * 255u + (d >> 24) * ia);
+    return r | (g << 8) | (b << 16) | (al << 24);
+}
+
+// A sample over the cleared target (0,0,0,1) (renderer.rs:233-238): rgb*a/255,
+// alpha 1.  `opaque` (every texel alpha 255, checked on upload) skips the
+// blend, which is exact there.
+template <typename Fetch>
+GEO_HD uint32_t sample_sky(Fetch fetch, uint32_t tw, uint32_t th, bool opaque, float U, float V) {
+    const uint32_t s = sample_sky_raw(fetch, tw, th, U, V);
+    if (opaque) return s | 0xFF000000u;
+    const uint32_t a = s >> 24;
+    return blend255_(s & 0xFFu, a) | (blend255_((s >> 8) & 0xFFu, a) << 8) |
+           (blend255_((s >> 16) & 0xFFu, a) << 16) | 0xFF000000u;
 }
 
 constexpr uint32_t kBlackRGBA = 0xFF000000u;  // clear colour (0,0,0,1), renderer.rs:233-238

@@ -39,6 +39,7 @@ struct RenderArgs {
     uint32_t width, height, row0, nrows;
     uint32_t band_shift, band_stride;  // local row lr -> row0 + (lr>>shift)*band_stride + lr%(1<<shift)
     uint32_t sky_opaque;
+    uint32_t composite;  // GEO_FLAG_COMPOSITE
     float inv_w, inv_h, kt;
     const uint32_t* sky;
     uint32_t sky_w, sky_h;
@@ -100,11 +101,17 @@ __global__ __launch_bounds__(kBlock) void geo_render_kernel(const RenderArgs a) 
         float U, V;
         geo::sky_uv(a.frame.central_to_uv, c2x, c2y, ct, lam, &U, &V);
         const uint32_t* sky = a.sky;
-        const uint32_t rgba = bh ? geo::kBlackRGBA
-                                 : geo::sample_sky([sky](uint32_t i) { return sky[i]; },
-                                                   a.sky_w, a.sky_h, a.sky_opaque != 0, U, V);
+        auto fetch = [sky](uint32_t i) { return sky[i]; };
         const size_t o = (size_t)ly * a.width + px;
-        a.out_rgba[o] = rgba;
+        if (a.composite) {
+            // over the previous spheres; a discarded pixel keeps the target
+            if (!bh) {
+                const uint32_t s = geo::sample_sky_raw(fetch, a.sky_w, a.sky_h, U, V);
+                a.out_rgba[o] = a.sky_opaque ? s : geo::composite_(s, a.out_rgba[o]);
+            }
+        } else {
+            a.out_rgba[o] = bh ? geo::kBlackRGBA : geo::sample_sky(fetch, a.sky_w, a.sky_h, a.sky_opaque != 0, U, V);
+        }
         if (a.out_mask) a.out_mask[o] = bh ? 1 : 0;
         if (a.out_uv) a.out_uv[o] = make_float2(U, V);
         if (a.out_steps) a.out_steps[o] = steps;
@@ -376,7 +383,7 @@ static int render_impl(geo_ctx* c, const geo_frame* frame, const geo_scene* scen
                        uint32_t* out_steps, unsigned long long* steps_total, void* stream) {
     if (scene->mode != GEO_MODE_DIRECT && scene->mode != GEO_MODE_FAN && scene->mode != GEO_MODE_ADAPTIVE)
         return GEO_EINVAL;
-    if ((scene->flags & ~GEO_FLAG_DEFER_STEPS) != 0) return GEO_EINVAL;
+    if ((scene->flags & ~(GEO_FLAG_DEFER_STEPS | GEO_FLAG_COMPOSITE)) != 0) return GEO_EINVAL;
     const bool adaptive = scene->mode == GEO_MODE_ADAPTIVE;
     // tol: 0 (default) or a positive finite tolerance in the adaptive mode, 0 otherwise
     if (adaptive ? !(scene->tol >= 0.0f && scene->tol <= 3.0e38f) : scene->tol != 0.0f) return GEO_EINVAL;
@@ -401,6 +408,7 @@ static int render_impl(geo_ctx* c, const geo_frame* frame, const geo_scene* scen
     a.band_shift = band_shift;
     a.band_stride = band_stride;
     a.sky_opaque = c->sky_opaque ? 1u : 0u;
+    a.composite = (scene->flags & GEO_FLAG_COMPOSITE) ? 1u : 0u;
     const uint32_t tiles_x = (width + kTileW - 1) / kTileW;
     a.inv_w = 1.0f / (float)width;
     a.inv_h = 1.0f / (float)height;

@@ -52,7 +52,15 @@ extern "C" int host_render(const geo_frame* f, const geo_scene* s, const float* 
             float U, V;
             geo::sky_uv(f->central_to_uv, c2x, c2y, ct, lam, &U, &V);
             const size_t o = (size_t)ly * width + px;
-            rgba[o] = bh ? geo::kBlackRGBA : geo::sample_sky([sky](uint32_t i) { return sky[i]; }, sw, sh, opaque, U, V);
+            auto fetch = [sky](uint32_t i) { return sky[i]; };
+            if (s->flags & GEO_FLAG_COMPOSITE) {
+                if (!bh) {
+                    const uint32_t sm = geo::sample_sky_raw(fetch, sw, sh, U, V);
+                    rgba[o] = opaque ? sm : geo::composite_(sm, rgba[o]);
+                }
+            } else {
+                rgba[o] = bh ? geo::kBlackRGBA : geo::sample_sky(fetch, sw, sh, opaque, U, V);
+            }
             mask[o] = bh ? 1 : 0;
             uv[2 * o] = U;
             uv[2 * o + 1] = V;

@@ -347,3 +347,50 @@ def test_invalid_arguments(geo, torch_mod):
         assert st == _lib.GEO_EINVAL
     with pytest.raises(geo.GeoError):
         geo.Context(99)
+
+
+def test_three_sphere_composite_bitexact(geo, torch_mod):
+    """The reference's three-sphere frame (lib.rs:62-89) drawn pass by pass with
+    GEO_FLAG_COMPOSITE into one device target: equal to the oracle's passes."""
+    from test_host_kernel_math import three_spheres
+
+    w, h = 320, 180
+    frame, passes = three_spheres(w, h)
+    ctx = geo.Context(0)
+    dev = torch_mod.device("cuda:0")
+    rgba = torch_mod.empty(w * h * 4, dtype=torch_mod.uint8, device=dev)
+    ref = None
+    for scene, sky in passes:
+        ctx.set_sky(sky)
+        ctx.render_rows(frame, scene, w, h, 0, h, rgba)
+        torch_mod.cuda.synchronize()
+        ref = O.render_f32(frame, scene, sky, w, h, threads=8, target=None if ref is None else ref["rgba"])
+        assert np.array_equal(rgba.cpu().numpy().reshape(h, w, 4), ref["rgba"])
+
+
+def test_renderer_three_spheres_and_points(geo, torch_mod):
+    """Renderer.render over three BasicSphereBuffers (each with its own
+    context) + an accretion-disk PointCloud == the oracle's passes + raster."""
+    from test_host_kernel_math import three_spheres
+
+    w, h = 256, 144
+    frame, passes = three_spheres(w, h)
+    obs = geo.Observer(1.0, math.pi / 2, w, h)
+    obs.set_position(2.5, 0.0, 0.1)
+    spheres = [geo.BasicSphereBuffer(0, sc.sphere_r, 1.0, sky, max_iter=2048) for sc, sky in passes]
+    for sp in spheres:
+        sp.update_ray_fan(obs.get_radial_position())
+    dev = torch_mod.device("cuda:0")
+    tgt = geo.RenderTarget(w, h, torch_mod.empty(w * h * 4, dtype=torch_mod.uint8, device=dev))
+    from test_points import accretion_disk
+
+    disk = geo.PointCloud(spheres[0].ctx, accretion_disk(1000, seed=2), 1.0, obs.get_position(), True, False)
+    fr = geo.Renderer(obs).render(spheres, tgt, point_clouds=[disk])
+    torch_mod.cuda.synchronize()
+    assert bytes(fr) == bytes(frame)
+    ref = None
+    for sc, sky in passes:
+        ref = O.render_f32(frame, sc, sky, w, h, threads=8, target=None if ref is None else ref["rgba"])
+    img, _ = O.draw_points(frame, disk.get_vertices(False), w, h, rgba=ref["rgba"])
+    img, _ = O.draw_points(frame, disk.get_vertices(True), w, h, rgba=img)
+    assert np.array_equal(tgt.rgba.cpu().numpy().reshape(h, w, 4), img)

@@ -32,11 +32,11 @@ def host():
     return lib
 
 
-def run_host(lib, frame, scene, sky, w, h, fan=None, variant=2):
+def run_host(lib, frame, scene, sky, w, h, fan=None, variant=2, target=None):
     fr, sc = O.as_frame(frame), O.as_scene(scene)
     sky = np.ascontiguousarray(sky)
     fan_a = np.ascontiguousarray(fan, np.float32) if fan is not None else None
-    rgba = np.empty((h, w, 4), np.uint8)
+    rgba = np.zeros((h, w, 4), np.uint8) if target is None else np.array(target, np.uint8)
     mask = np.empty((h, w), np.uint8)
     uv = np.empty((h, w, 2), np.float32)
     steps = np.empty((h, w), np.uint32)
@@ -131,3 +131,53 @@ def test_host_header_adaptive_equals_oracle(host, name, w, h, fk, sk):
     for f in ("mask", "steps", "rgba"):
         assert np.array_equal(a[f], b[f]), (f, np.argwhere(a[f] != b[f])[:5])
     assert np.array_equal(a["uv"].view(np.uint32), b["uv"].view(np.uint32))
+
+
+def three_spheres(w, h):
+    """The reference's frame (lib.rs:62-89): sky sphere r = 50 (opaque), a
+    planet sphere r = 1.1 (opaque) and a cloud sphere r = 1.2 (translucent),
+    drawn in that order with alpha blending (rs = 1 units)."""
+    from schwarzschild_raytracer_wgpu_amd import make_scene
+    from schwarzschild_raytracer_wgpu_amd._lib import GEO_FLAG_COMPOSITE
+
+    rng = np.random.default_rng(12)
+    planet = make_sky("equirect", (96, 48), seed=0x1234)
+    clouds = rng.integers(0, 256, size=(40, 80, 4), dtype=np.uint8)
+    clouds[..., 3] = (clouds[..., 3] // 2)  # alpha <= 127
+    frame = default_frame(w, h, pos=(2.5, 0.0, 0.1))
+    r = math.sqrt(2.5 ** 2 + 0.01)
+    passes = [(make_scene(1.0, 50.0, r, math.pi / 100, 2048), make_sky("equirect", (128, 64))),
+              (make_scene(1.0, 1.1, r, math.pi / 100, 2048, flags=GEO_FLAG_COMPOSITE), planet),
+              (make_scene(1.0, 1.2, r, math.pi / 100, 2048, flags=GEO_FLAG_COMPOSITE), clouds)]
+    return frame, passes
+
+
+def test_host_header_composite_three_spheres(host):
+    """GEO_FLAG_COMPOSITE: the reference's three-sphere frame; every pass equals the oracle's."""
+    w, h = 128, 72
+    frame, passes = three_spheres(w, h)
+    a = b = None
+    for scene, sky in passes:
+        a = run_host(host, frame, scene, sky, w, h, target=None if a is None else a["rgba"])
+        b = O.render_f32(frame, scene, sky, w, h, threads=4, target=None if b is None else b["rgba"])
+        assert np.array_equal(a["rgba"], b["rgba"])
+    # the cloud pass changed pixels where the cloud sphere is hit, and only there
+    assert 0 < (b["mask"] == 0).sum() < w * h
+
+
+def test_composite_over_clear_equals_plain_draw():
+    """A sphere composited over the cleared target (0,0,0,255) equals the plain draw."""
+    from schwarzschild_raytracer_wgpu_amd import make_scene
+    from schwarzschild_raytracer_wgpu_amd._lib import GEO_FLAG_COMPOSITE
+
+    w, h = 96, 54
+    rng = np.random.default_rng(3)
+    sky = rng.integers(0, 256, size=(64, 128, 4), dtype=np.uint8)
+    frame = default_frame(w, h)
+    r = math.sqrt(2.5 ** 2 + 0.01)
+    plain = O.render_f32(frame, make_scene(1.0, 50.0, r, math.pi / 100, 512), sky, w, h)
+    clear = np.zeros((h, w, 4), np.uint8)
+    clear[..., 3] = 255
+    comp = O.render_f32(frame, make_scene(1.0, 50.0, r, math.pi / 100, 512, flags=GEO_FLAG_COMPOSITE), sky, w, h,
+                        target=clear)
+    assert np.array_equal(plain["rgba"], comp["rgba"])

@@ -79,6 +79,7 @@ def _load() -> ctypes.CDLL:
         "geo_oracle_project_point": (i, [vp, vp, u32, u32, vp, vp]),
         "geo_oracle_draw_points": (i, [vp, vp, u32, u32, u32, u32, u32, vp, vp]),
         "geo_oracle_acosf": (ctypes.c_float, [ctypes.c_float]),
+        "geo_oracle_orbit_frames": (i, [f64, f64, f64, f64, vp, f64, f64, f64, u32, f64, vp, vp]),
         "geo_oracle_asinf": (ctypes.c_float, [ctypes.c_float]),
         "geo_oracle_atan2f": (ctypes.c_float, [ctypes.c_float, ctypes.c_float]),
         "geo_oracle_sincosf": (None, [ctypes.c_float, vp, vp]),
@@ -265,3 +266,15 @@ def draw_points(frame, verts, width, height, rgba=None, row0=0, nrows=None):
     fr = as_frame(frame)
     lib.geo_oracle_draw_points(_addr(fr), _np(verts), verts.shape[0], width, height, row0, nrows, _np(rgba), _np(xy))
     return rgba, xy
+
+
+def orbit_frames(rs, fov, width, height, pos, camera, rotation, nframes, dt):
+    """Orbiting observer replay: (frames: list of GeoFrameC, positions (n, 3)) or None."""
+    frames = (GeoFrameC * nframes)()
+    positions = np.empty((nframes, 3), np.float64)
+    p = (ctypes.c_double * 3)(*pos)
+    r = lib.geo_oracle_orbit_frames(rs, fov, width, height, ctypes.cast(p, ctypes.c_void_p), camera[0], camera[1],
+                                    rotation, nframes, dt, ctypes.cast(frames, ctypes.c_void_p), _np(positions))
+    if r != 0:
+        return None
+    return list(frames), positions

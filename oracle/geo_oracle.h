@@ -91,6 +91,12 @@ int geo_oracle_rays_update(float rs, uint32_t n_points, uint32_t sides, const fl
 int geo_oracle_points_run(float rs, const float* model, uint32_t n, int farside, int orbits, uint64_t seed,
                           uint32_t nframes, const float* observers, const double* dts, float* out_near,
                           float* out_far, float* out_pos, int libm);
+/* Orbiting observer replay (observer.rs:104-124, 162-169, 197-262):
+ * start_orbit(rotation) at pos, then nframes x (update_position(dt),
+ * calc_transformation_pipeline).  -1 when no orbit can start. */
+int geo_oracle_orbit_frames(double rs, double fov, double width, double height, const double pos[3], double cam_phi,
+                            double cam_theta, double rotation, uint32_t nframes, double dt, geo_frame* frames,
+                            double* positions);
 /* vs_main + raster of one vertex / a vertex list (kernel f32 order) */
 int geo_oracle_project_point(const geo_frame* f, const float* v, uint32_t width, uint32_t height, int* ix, int* iy);
 int geo_oracle_draw_points(const geo_frame* f, const float* verts, uint32_t n, uint32_t width, uint32_t height,

@@ -507,3 +507,111 @@ int geo_oracle_draw_points(const geo_frame* f, const float* verts, uint32_t n, u
     }
     return 0;
 }
+
+/* ------------------------------------------------------------------ */
+/* Orbiting observer (observer.rs:104-124, 162-169, 197-262): start_orbit,  */
+/* then per frame update_position + calc_transformation_pipeline            */
+/* ------------------------------------------------------------------ */
+
+static dm3 dm_cols(dv3 x, dv3 y, dv3 z) { dm3 m; m.c[0] = x; m.c[1] = y; m.c[2] = z; return m; }
+static dm3 dmm(const dm3* a, const dm3* b) { return dm_cols(dmv(a, b->c[0]), dmv(a, b->c[1]), dmv(a, b->c[2])); }
+static dm3 dtr(const dm3* m) {
+    return dm_cols(d3(m->c[0].x, m->c[1].x, m->c[2].x), d3(m->c[0].y, m->c[1].y, m->c[2].y),
+                   d3(m->c[0].z, m->c[1].z, m->c[2].z));
+}
+static dm3 drot_x(double a) { double s = sin(a), c = cos(a); return dm_cols(d3(1, 0, 0), d3(0, c, s), d3(0, -s, c)); }
+static dm3 drot_z(double a) { double s = sin(a), c = cos(a); return dm_cols(d3(c, s, 0), d3(-s, c, 0), d3(0, 0, 1)); }
+static dm3 dlook(dv3 t) { /* polar_transformations.rs:43-51 */
+    double inv = 1. / dlen(t);
+    dv3 z = d3(t.x * inv, t.y * inv, t.z * inv);
+    dv3 xp = carthesic_to_polar(z);
+    xp.z -= 1.57079632679489661923;
+    dv3 x = polar_to_carthesic(xp);
+    return dm_cols(x, dcross(z, x), z);
+}
+static double dsignum(double x) { return signbit(x) ? -1. : 1.; }
+
+/* orbit.rs:185-208 */
+static dv3 orbit_get_velocity(const orbit* o) {
+    double hr = 1. - o->schwarz_r / o->r;
+    double falling = o->rotation == 0. ? -dsignum(o->r - o->last_r) : dsignum(o->u_bar);
+    return d3(o->energy / hr,
+              -falling * sqrt(o->energy * o->energy - hr * (1. + o->rotation * o->rotation / (o->r * o->r))),
+              o->rotation / (o->r * o->r));
+}
+static double orbit_current_tilt_angle(const orbit* o) {
+    dv3 p = carthesic_to_polar(dmv(&o->plane_tilt_mat, polar_to_carthesic(d3(o->r, o->orbit_angle, 0.))));
+    return o->tilt_angle * cos(p.y);
+}
+
+/* Replays an orbiting observer: start_orbit(rotation) at pos, then nframes x
+ * (update_position(_, dt), calc_transformation_pipeline).  Returns -1 when the
+ * orbit cannot start (Orbit::new is None). */
+int geo_oracle_orbit_frames(double rs, double fov, double width, double height, const double pos[3], double cam_phi,
+                            double cam_theta, double rotation, uint32_t nframes, double dt, geo_frame* frames,
+                            double* positions) {
+    dv3 p = d3(pos[0], pos[1], pos[2]);
+    orbit o;
+    if (!orbit_new(rs, p, d3(-p.y, p.x, 0.), rotation, &o)) return -1;
+    double psi = 1.;
+    dm3 std_to_mov = dm_cols(d3(1, 0, 0), d3(0, 1, 0), d3(0, 0, 1));
+    dm3 mov_to_central = std_to_mov, central_to_uv = std_to_mov;
+    double t = tan(fov / 2.);
+    double fov_scaling[4] = {t, t * (width / height), 1., 1.};
+    for (uint32_t f = 0; f < nframes; ++f) {
+        orbit_do_step(&o, 1. * dt); /* time_speedup 1 */
+        p = orbit_get_position(&o);
+        double r = dlen(p);
+        int singular = fabs(r - rs) < 1e-10 || o.has_hit_singularity;
+        if (!singular) {
+            dv3 vel = orbit_get_velocity(&o);
+            double hr = 1. - rs / dlen(p);
+            psi = r > rs ? vel.x * vel.x * hr : -vel.y * vel.y / hr;
+            if (psi - 1. < 1e-10) psi = 1.;
+            dm3 l = dlook(d3(-p.x, -p.y, -p.z));
+            dm3 standard_to_central = dtr(&l);
+            if (o.rotation != 0.) {
+                double tilt_angle = orbit_current_tilt_angle(&o);
+                double plane_angle1 = acos(-vel.x * vel.y * dsignum(r - rs) /
+                                           sqrt((1. + r * r * vel.z * vel.z) * psi * (psi - 1.)));
+                double plane_angle2 = r > rs ? acos(-vel.y / sqrt(hr * (psi - 1.)))
+                                             : acos(-vel.x * sqrt(-hr / (psi - 1.)));
+                dm3 opt = drot_z(-tilt_angle), tc1 = drot_x(-plane_angle1), m2 = drot_x(plane_angle2);
+                dm3 a = dmm(&tc1, &opt);
+                std_to_mov = dmm(&a, &standard_to_central);
+                dm3 optt = dtr(&opt);
+                mov_to_central = dmm(&optt, &m2);
+            } else {
+                std_to_mov = standard_to_central;
+                mov_to_central = dm_cols(d3(1, 0, 0), d3(0, 1, 0), d3(0, 0, 1));
+            }
+            dm3 lu = dlook(p), flip = dm_cols(d3(1, 0, 0), d3(0, -1, 0), d3(0, 0, 1));
+            central_to_uv = dmm(&lu, &flip);
+        }
+        dm3 cam_to_std = dlook(d3(cos(cam_phi) * cos(cam_theta), sin(cam_phi) * cos(cam_theta), sin(cam_theta)));
+        dm3 cam = dmm(&std_to_mov, &cam_to_std);
+        geo_frame* out = &frames[f];
+        memset(out, 0, sizeof(*out));
+        const dm3* src[3] = {&cam, &mov_to_central, &central_to_uv};
+        float* dst[3] = {out->display_to_movement, out->movement_to_central, out->central_to_uv};
+        for (int k = 0; k < 3; ++k)
+            for (int c = 0; c < 3; ++c) {
+                dst[k][c * 4 + 0] = (float)src[k]->c[c].x;
+                dst[k][c * 4 + 1] = (float)src[k]->c[c].y;
+                dst[k][c * 4 + 2] = (float)src[k]->c[c].z;
+            }
+        for (int i = 0; i < 4; ++i) out->display_to_movement[12 + i] = (float)fov_scaling[i];
+        out->movement_to_central[15] = 1.f;
+        out->central_to_uv[15] = 1.f;
+        out->psi_factor_and_position[0] = (float)sqrt((psi - 1.) / psi);
+        out->psi_factor_and_position[1] = (float)p.x;
+        out->psi_factor_and_position[2] = (float)p.y;
+        out->psi_factor_and_position[3] = (float)p.z;
+        if (positions) {
+            positions[3 * f] = p.x;
+            positions[3 * f + 1] = p.y;
+            positions[3 * f + 2] = p.z;
+        }
+    }
+    return 0;
+}

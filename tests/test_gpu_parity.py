@@ -394,3 +394,27 @@ def test_renderer_three_spheres_and_points(geo, torch_mod):
     img, _ = O.draw_points(frame, disk.get_vertices(False), w, h, rgba=ref["rgba"])
     img, _ = O.draw_points(frame, disk.get_vertices(True), w, h, rgba=img)
     assert np.array_equal(tgt.rgba.cpu().numpy().reshape(h, w, 4), img)
+
+
+@pytest.mark.parametrize("rotation,nframes", [(3.2, 120), (2.0, 200)])
+def test_orbit_replay_render_bitexact(geo, torch_mod, rotation, nframes):
+    """N2 scenario replay: an orbiting observer (non-identity movement_to_central,
+    observer.rs:215-242) after n frames; the rendered frame == the oracle's."""
+    from schwarzschild_raytracer_wgpu_amd.scenes import make_sky
+
+    w, h = 320, 180
+    obs = geo.Observer(1.0, math.pi / 2, w, h)
+    obs.set_position(2.5, 0.0, 0.1)
+    obs.set_camera(math.pi + 0.3, 0.1)
+    assert obs.start_orbit(rotation)
+    for _ in range(nframes):
+        obs.update_position((0.0, 0.0, 0.0), 1 / 60)
+    frame = obs.calc_transformation_pipeline()
+    m1 = np.array(frame.movement_to_central[:])
+    assert not np.allclose(m1, np.eye(4).reshape(-1))
+    scene = default_scene(2048, r_obs=obs.get_radial_position())
+    sky = make_sky("equirect", (512, 256))
+    ctx = make_ctx(geo, sky)
+    hip = render(geo, torch_mod, ctx, frame, scene, w, h)
+    ref = O.render_f32(frame, scene, sky, w, h, threads=8)
+    assert_same(hip, ref)

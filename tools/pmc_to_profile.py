@@ -17,14 +17,14 @@ import glob  # noqa: E402
 tag, out, workload = sys.argv[1], sys.argv[2], sys.argv[3]
 c = {}
 dur = {}
-for p in sorted(glob.glob(f"gpurun_out/{tag}_*/run_counter_collection.csv")):
+for p in sorted(sum((glob.glob(f"gpurun_out/{t}_*/run_counter_collection.csv") for t in tag.split(",")), [])):
     cc, d = load(p)
     c.update(cc)
     dur.update(d)
 dur_ns = sum(dur.values()) / len(dur)
 xcd_cycles = c["GRBM_GUI_ACTIVE"] / 8.0
 res = {
-    "kernel": "geo_render_kernel<GEO_MODE_DIRECT, kCurvedOut>",
+    "kernel": sys.argv[4] if len(sys.argv) > 4 else "geo_render_kernel<GEO_MODE_DIRECT, kCurvedOut>",
     "workload": workload,
     "source": f"rocprofv3 --kernel-trace --pmc (separate passes), gpurun_out/{tag}_*",
     "counters_per_dispatch": c,

@@ -5,9 +5,9 @@ over N GPUs with an RCCL gather to rank 0).
 
 One "step" = one frame: every rank renders its interleaved row bands of the
 4K frame with the HIP kernel (geo_render_bands), then (N > 1) rank 0 gathers
-the bands over RCCL and reassembles the frame for present.  Gathers run on
-RCCL's stream, double-buffered, so frame n's gather overlaps frame n+1's
-compute.  value = executed RK4 main-loop steps of all ranks / max-over-ranks
+the bands over RCCL and reassembles the frame for present (geo_assemble_bands).
+Gathers run on RCCL's stream in batches of --frames-per-gather frames,
+double-buffered, so a batch's gather overlaps the next batch's compute.  value = executed RK4 main-loop steps of all ranks / max-over-ranks
 wall time of the K timed frames (inputs resident in HBM, sky uploaded once).
 
   python bench.py [--gpus N] [--steps K] [--warmup W]
@@ -47,6 +47,9 @@ def parse():
                    help="time every k-th timed frame's kernel with a fence-free HIP event pair")
     p.add_argument("--config", default="cfg3_4k")
     p.add_argument("--band-rows", type=int, default=8)
+    p.add_argument("--frames-per-gather", type=int, default=4,
+                   help="N > 1: frames per RCCL gather to rank 0 (amortises the ~34 us host cost of a gather; "
+                        "rank 0 reassembles each batch with one geo_assemble_bands launch)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-threads", type=int, default=16)
     p.add_argument("--cpu-row-step", type=int, default=None,
@@ -107,7 +110,7 @@ def main():
     from schwarzschild_raytracer_wgpu_amd.dist import ShardedFrame
 
     sf = ShardedFrame(ctx, frame, scene, W, H, args.band_rows, rank, world, dev, dist if world > 1 else None,
-                      host_gather=args.dist_backend == "gloo")
+                      host_gather=args.dist_backend == "gloo", frames_per_gather=args.frames_per_gather)
     L = sf.layout
     steps_ctr = torch.zeros(1, dtype=torch.int64, device=dev)
 
@@ -225,6 +228,7 @@ def main():
             "width": W, "height": H, "max_steps": cfg.max_steps,
             "parallelism": f"rowbands{world}" if world > 1 else "single",
             "band_rows": args.band_rows,
+            "frames_per_gather": sf.K,
         },
         "per_gpu": value / world,
         "pixels_per_s": total_pixels / elapsed_max,

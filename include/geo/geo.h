@@ -167,6 +167,16 @@ int geo_render_bands(geo_ctx* ctx, const geo_frame* frame, const geo_scene* scen
                      float* out_uv, uint32_t* out_steps, unsigned long long* steps_total,
                      void* stream);
 
+/* Rank 0's reassembly after gathering every rank's geo_render_bands output
+ * (multi-GPU present): `src` (device) holds `world` rank blocks
+ * of rank_stride bytes, rank r's block being its packed bands (bands r,
+ * r+world, r+2*world, ... of band_rows rows) for nframes frames at
+ * frame_stride bytes apart.  Writes nframes width x height RGBA8 frames
+ * back to back to `dst` (device).  Asynchronous on `stream`. */
+int geo_assemble_bands(geo_ctx* ctx, const uint8_t* src, size_t rank_stride, size_t frame_stride, uint32_t world,
+                       uint32_t band_rows, uint32_t width, uint32_t height, uint32_t nframes, uint8_t* dst,
+                       void* stream);
+
 /* Adds the steps accumulated under GEO_FLAG_DEFER_STEPS to *steps_total
  * (device u64) and clears the context's counter.  Asynchronous on `stream`. */
 int geo_steps_flush(geo_ctx* ctx, unsigned long long* steps_total, void* stream);

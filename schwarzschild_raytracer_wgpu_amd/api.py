@@ -148,6 +148,13 @@ class Context:
         """geo_steps_flush: add the GEO_FLAG_DEFER_STEPS accumulator to steps_total (device u64)."""
         check("geo_steps_flush", lib.geo_steps_flush(self._h, _ptr(steps_total), _stream_handle(stream)))
 
+    def assemble_bands(self, src, rank_stride: int, frame_stride: int, world: int, band_rows: int, width: int,
+                       height: int, nframes: int, dst, stream=None) -> None:
+        """geo_assemble_bands: rank-packed bands (device) -> nframes frames (device)."""
+        check("geo_assemble_bands", lib.geo_assemble_bands(self._h, _ptr(src), rank_stride, frame_stride, world,
+                                                           band_rows, width, height, nframes, _ptr(dst),
+                                                           _stream_handle(stream)))
+
     def render_rows(self, frame: GeoFrame, scene: GeoScene, width: int, height: int, row0: int, nrows: int,
                     out_rgba, out_mask=None, out_uv=None, out_steps=None, steps_total=None, stream=None) -> None:
         """geo_render_rows; outputs are device tensors (rgba: nrows*width*4 u8)."""

@@ -130,6 +130,28 @@ __global__ __launch_bounds__(kBlock) void geo_render_kernel(const RenderArgs a) 
     }
 }
 
+// Frame row y of frame f comes from rank r = (y / band_rows) % world, local
+// row ((y / band_rows) / world) * band_rows + y % band_rows of that rank's
+// packed bands (geo_render_bands' layout).  One thread per 16 B (W % 4 == 0)
+// or per pixel.
+template <typename T>
+__global__ __launch_bounds__(256) void geo_assemble_kernel(const uint8_t* __restrict__ src, size_t rank_stride,
+                                                           size_t frame_stride, uint32_t world, uint32_t band_rows,
+                                                           uint32_t row_units, uint32_t height,
+                                                           uint8_t* __restrict__ dst) {
+    const uint32_t x = blockIdx.x * 256u + threadIdx.x;
+    const uint32_t y = blockIdx.y;
+    const uint32_t f = blockIdx.z;
+    if (x >= row_units) return;
+    const uint32_t b = y / band_rows;
+    const uint32_t r = b % world;
+    const size_t lrow = (size_t)(b / world) * band_rows + y % band_rows;
+    const size_t row_bytes = (size_t)row_units * sizeof(T);
+    const T* s = reinterpret_cast<const T*>(src + r * rank_stride + f * frame_stride + lrow * row_bytes);
+    T* d = reinterpret_cast<T*>(dst + ((size_t)f * height + y) * row_bytes);
+    d[x] = s[x];
+}
+
 __global__ __launch_bounds__(kStepSlots) void geo_steps_finalize(unsigned long long* slots,
                                                                   unsigned long long* total) {
     __shared__ unsigned long long s[kStepSlots / 64];
@@ -458,6 +480,32 @@ static int render_impl(geo_ctx* c, const geo_frame* frame, const geo_scene* scen
         if (hipGetLastError() != hipSuccess) return GEO_EHIP;
     }
     return GEO_OK;
+}
+
+int geo_assemble_bands(geo_ctx* c, const uint8_t* src, size_t rank_stride, size_t frame_stride, uint32_t world,
+                       uint32_t band_rows, uint32_t width, uint32_t height, uint32_t nframes, uint8_t* dst,
+                       void* stream) {
+    if (!c || !src || !dst || world == 0 || band_rows == 0 || width == 0 || height == 0 || nframes == 0 ||
+        height > 65535u || nframes > 65535u)
+        return GEO_EINVAL;
+    const size_t row_bytes = (size_t)width * 4;
+    const size_t nb_max = ((size_t)(height + band_rows - 1) / band_rows + world - 1) / world;
+    if (frame_stride < nb_max * band_rows * row_bytes || rank_stride < (size_t)nframes * frame_stride)
+        return GEO_EINVAL;
+    DeviceGuard g(c->device);
+    if (!g.ok) return GEO_EHIP;
+    hipStream_t s = (hipStream_t)stream;
+    const bool wide = (width % 4u) == 0 && (rank_stride % 16u) == 0 && (frame_stride % 16u) == 0 &&
+                      ((uintptr_t)src % 16u) == 0 && ((uintptr_t)dst % 16u) == 0;
+    const uint32_t units = wide ? width / 4u : width;
+    const dim3 grid((units + 255u) / 256u, height, nframes);
+    if (wide)
+        hipLaunchKernelGGL(geo_assemble_kernel<uint4>, grid, dim3(256), 0, s, src, rank_stride, frame_stride, world,
+                           band_rows, units, height, dst);
+    else
+        hipLaunchKernelGGL(geo_assemble_kernel<uint32_t>, grid, dim3(256), 0, s, src, rank_stride, frame_stride,
+                           world, band_rows, units, height, dst);
+    return hipGetLastError() == hipSuccess ? GEO_OK : GEO_EHIP;
 }
 
 int geo_steps_flush(geo_ctx* c, unsigned long long* steps_total, void* stream) {

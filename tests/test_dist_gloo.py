@@ -80,3 +80,58 @@ def test_band_layout_balance_4k_8ranks():
 def test_band_layout_single_rank_is_identity():
     L = BandLayout(1080, 8, 1, 0)
     assert L.local_to_frame_rows() == list(range(1080))
+
+
+def _worker_batched(rank, world, port, W, H, B, K, nframes, q):
+    """Several frames per gather (frames_per_gather = K): rank r's buffer holds K
+    packed frames back to back; rank 0 reassembles every frame of the batch."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import math
+
+        import oracle as O
+        from helpers import default_frame, default_scene
+        from schwarzschild_raytracer_wgpu_amd.scenes import make_sky
+
+        sky = make_sky("equirect", (64, 32))
+        scene = default_scene(256)
+        L = BandLayout(H, B, world, rank)
+        row_bytes = W * 4
+        sl = L.nb_max * B * row_bytes
+        frames = [default_frame(W, H, camera=(math.pi + 0.1 * f, 0.05 * f)) for f in range(nframes)]
+        local = torch.zeros(K * sl, dtype=torch.uint8)
+        for f in range(nframes):
+            lv = local[f * sl:(f + 1) * sl].view(L.nb_max * B, row_bytes)
+            for i, fr in enumerate(L.local_to_frame_rows()):
+                if fr >= 0:
+                    r = O.render_f32(frames[f], scene, sky, W, H, row0=fr, nrows=1, threads=1)
+                    lv[i] = torch.from_numpy(r["rgba"].reshape(-1).copy())
+        recv = torch.empty(world * K * sl, dtype=torch.uint8) if rank == 0 else None
+        dist.gather(local, gather_list=list(recv.chunk(world)) if rank == 0 else None, dst=0)
+        if rank == 0:
+            ok = True
+            gl = list(recv.chunk(world))
+            for f in range(nframes):
+                full = torch.zeros(L.nb_total * B * row_bytes, dtype=torch.uint8)
+                assemble(full, gl, L, row_bytes, frame=f, frame_stride=sl)
+                ref = O.render_f32(frames[f], scene, sky, W, H, threads=2)["rgba"].reshape(-1)
+                ok = ok and bool(np.array_equal(full[: H * row_bytes].numpy(), ref))
+            q.put(ok)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,W,H,B,K,nframes", [(2, 40, 36, 8, 3, 3), (3, 24, 40, 8, 4, 2)])
+def test_gloo_batched_gather_reassembles_frames(world, W, H, B, K, nframes):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_batched, args=(r, world, port, W, H, B, K, nframes, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=240)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    assert q.get(timeout=10) is True

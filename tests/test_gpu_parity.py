@@ -418,3 +418,27 @@ def test_orbit_replay_render_bitexact(geo, torch_mod, rotation, nframes):
     hip = render(geo, torch_mod, ctx, frame, scene, w, h)
     ref = O.render_f32(frame, scene, sky, w, h, threads=8)
     assert_same(hip, ref)
+
+
+@pytest.mark.parametrize("world,W,H,B,K", [(3, 40, 37, 8, 2), (8, 64, 2160 // 8, 8, 3), (2, 33, 20, 16, 1)])
+def test_assemble_bands_matches_host_assembly(geo, torch_mod, world, W, H, B, K):
+    """geo_assemble_bands == the host (torch) reassembly of dist.assemble, for
+    every frame of a K-frame batch (16-B and 4-B copy paths)."""
+    from schwarzschild_raytracer_wgpu_amd.dist import BandLayout, assemble
+
+    ctx = geo.Context(0)
+    L = BandLayout(H, B, world, 0)
+    row_bytes = W * 4
+    sl = L.nb_max * B * row_bytes
+    rng = np.random.default_rng(world * 100 + K)
+    src = rng.integers(0, 256, size=world * K * sl, dtype=np.uint8)
+    dev = torch_mod.device("cuda:0")
+    frame_bytes = L.nb_total * B * row_bytes
+    out = torch_mod.zeros(K * H * row_bytes, dtype=torch_mod.uint8, device=dev)
+    ctx.assemble_bands(torch_mod.from_numpy(src).to(dev), K * sl, sl, world, B, W, H, K, out)
+    got = out.cpu().numpy()
+    gl = list(torch_mod.from_numpy(src).chunk(world))
+    for f in range(K):
+        full = torch_mod.zeros(frame_bytes, dtype=torch_mod.uint8)
+        assemble(full, gl, L, row_bytes, frame=f, frame_stride=sl)
+        assert np.array_equal(got[f * H * row_bytes:(f + 1) * H * row_bytes], full[:H * row_bytes].numpy()), f

@@ -47,6 +47,9 @@ def parse():
                    help="time every k-th timed frame's kernel with a fence-free HIP event pair")
     p.add_argument("--config", default="cfg3_4k")
     p.add_argument("--band-rows", type=int, default=8)
+    p.add_argument("--render-streams", type=int, default=None,
+                   help="render streams (1 or 2; default 1 at N = 1, 2 at N > 1: the next frame's waves fill "
+                        "the tail of a rank's small share)")
     p.add_argument("--frames-per-gather", type=int, default=4,
                    help="N > 1: frames per RCCL gather to rank 0 (amortises the ~34 us host cost of a gather; "
                         "rank 0 reassembles each batch with one geo_assemble_bands launch)")
@@ -110,7 +113,8 @@ def main():
     from schwarzschild_raytracer_wgpu_amd.dist import ShardedFrame
 
     sf = ShardedFrame(ctx, frame, scene, W, H, args.band_rows, rank, world, dev, dist if world > 1 else None,
-                      host_gather=args.dist_backend == "gloo", frames_per_gather=args.frames_per_gather)
+                      host_gather=args.dist_backend == "gloo", frames_per_gather=args.frames_per_gather,
+                      render_streams=args.render_streams or (1 if world == 1 else 2))
     L = sf.layout
     steps_ctr = torch.zeros(1, dtype=torch.int64, device=dev)
 
@@ -160,8 +164,8 @@ def main():
     t0 = time.perf_counter()
     for i in range(args.steps):
         sf.step(i, events=evs.get(i), scene=scene_defer)
+    sf.drain()  # joins the render streams into the current one
     ctx.steps_flush(steps_ctr)
-    sf.drain()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -229,6 +233,7 @@ def main():
             "parallelism": f"rowbands{world}" if world > 1 else "single",
             "band_rows": args.band_rows,
             "frames_per_gather": sf.K,
+            "render_streams": sf.S,
         },
         "per_gpu": value / world,
         "pixels_per_s": total_pixels / elapsed_max,
@@ -253,6 +258,7 @@ def main():
     }
     if world == 1 and not args.no_cpu_baseline and mode != g.GEO_MODE_FAN:
         out["cpu_baseline"] = cpu_baseline(frame, scene, sky, W, H, args)
+        out["reference_equivalent"] = reference_fan_cost(ctx, cfg, obs.get_radial_position())
     print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
@@ -271,6 +277,39 @@ def pmc_traffic(config, mode):
         return None
     with open(files[-1]) as f:
         return json.load(f)["derived"]["traffic_bytes"]
+
+
+def reference_fan_cost(ctx, cfg, r):
+    """What the reference actually computes per frame on its CPU: the 400-node
+    f64 ray fan of each of its 3 spheres (SphereRayTracer::solve_ray_fan,
+    sphere_ray_tracer.rs:35-56; lib.rs:292-295), single-threaded — timed on
+    the oracle's literal f64 restatement; beside it the same fans on the GPU
+    (geo_solve_ray_fan, f64, one lane per node).  Display semantics differ
+    (fan lerp vs per-pixel geodesics), so this is context, not
+    the metric."""
+    import oracle as O
+
+    n = 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < 0.5:
+        for sphere_r in (cfg.sphere_r, 1.1, 1.2):  # the reference's 3 spheres (lib.rs:67-89), rs = 1 units
+            O.solve_ray_fan(sphere_r, cfg.rs, 1000, math.pi / 100, 400, r)
+        n += 1
+    cpu_ms = (time.perf_counter() - t0) / n * 1e3
+    import torch
+
+    for _ in range(3):
+        ctx.solve_ray_fan(cfg.sphere_r, cfg.rs, 1000, math.pi / 100, 400, r)
+    torch.cuda.synchronize()
+    m = 20
+    t0 = time.perf_counter()
+    for _ in range(m):
+        for sphere_r in (cfg.sphere_r, 1.1, 1.2):
+            ctx.solve_ray_fan(sphere_r, cfg.rs, 1000, math.pi / 100, 400, r)
+    gpu_ms = (time.perf_counter() - t0) / m * 1e3
+    return {"what": "3 spheres x 400-node f64 ray fan per frame (the reference's per-frame CPU work)",
+            "cpu_ms_per_frame_1core": cpu_ms, "gpu_ms_per_frame_geo_solve_ray_fan": gpu_ms,
+            "note": "gpu figure includes the synchronous host copy of each fan"}
 
 
 def cpu_baseline(frame, scene, sky, W, H, args):

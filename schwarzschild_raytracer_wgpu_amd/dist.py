@@ -69,34 +69,50 @@ class ShardedFrame:
     """Render-then-gather pipeline for one rank, K frames per gather.
 
     step(i) renders this rank's bands of frame i into slot i % K of batch
-    buffer (i // K) % 2 on the current stream; after the K-th frame of a batch
-    one async gather (RCCL, on its own stream, ordered after the renders)
-    sends the K packed frames to rank 0, so a batch's gather overlaps the next
-    batch's renders.  Rank 0 reassembles all K frames of a batch with one
-    geo_assemble_bands launch when the batch retires.  K amortises the host
-    cost of a gather (~34 us, tools/host_overhead.py) over K frames: at N = 8
-    a 4K frame is ~31 us of GPU work per rank.
+    buffer (i // K) % 2, on render stream i % S; after the K-th frame of a
+    batch one async gather (RCCL, launched from its own stream once the
+    batch's renders are done) sends the K packed frames to rank 0, so a
+    batch's gather overlaps the next batch's renders.  Rank 0 reassembles all
+    K frames of a batch with one geo_assemble_bands launch on a side stream
+    when the batch retires.
+
+    K amortises the host cost of a gather (~26-34 us, tools/host_overhead.py)
+    over K frames; S = 2 render streams let frame i+1's waves fill frame i's
+    tail (at N = 8 a rank's share of a 4K frame is only ~2 waves per slot:
+    0.0417 -> 0.0309 ms/frame back to back, tools/scale_probe.py).  All
+    cross-stream hazards are ordered with events: a batch buffer is
+    re-rendered only after its gather completed, rank 0's receive buffer is
+    re-filled only after its reassembly completed.
     """
 
     def __init__(self, ctx, frame, scene, width: int, height: int, band_rows: int, rank: int, world: int, device,
-                 dist=None, host_gather: bool = False, frames_per_gather: int = 1):
+                 dist=None, host_gather: bool = False, frames_per_gather: int = 1, render_streams: int = 1):
         """host_gather: stage through host memory (gloo backend; rehearsals only)."""
         import torch
 
+        self.torch = torch
         self.host_gather = host_gather
         self.ctx, self.frame, self.scene = ctx, frame, scene
         self.width, self.height = width, height
         self.layout = BandLayout(height, band_rows, world, rank)
         self.rank, self.world, self.dist = rank, world, dist
         self.K = max(1, int(frames_per_gather)) if world > 1 else 1
+        self.S = min(2, max(1, int(render_streams)))
         L = self.layout
         self.row_bytes = width * 4
         self.slice = L.nb_max * band_rows * self.row_bytes  # one frame's packed bands
         self.bufs = [torch.empty(self.K * self.slice, dtype=torch.uint8, device=device) for _ in range(2)]
         self.frame_bytes = height * self.row_bytes  # assembled frames, back to back
+        self.extra = [torch.cuda.Stream(device) for _ in range(self.S - 1)]
         self.recv = None
         self.frames = None
         self.side = None
+        self.gstream = None
+        self.ev_free = [None, None]       # batch buffer b may be re-rendered after this event
+        self.ev_assembled = [None, None]  # rank 0: recv[b] may be re-filled after this event
+        self.ev_rendered = [[None] * self.S for _ in range(2)]  # last render per stream into batch b
+        if world > 1 and not host_gather:
+            self.gstream = torch.cuda.Stream(device)
         if world > 1 and rank == 0:
             rdev = "cpu" if host_gather else device
             self.recv = [torch.empty(world * self.K * self.slice, dtype=torch.uint8, device=rdev) for _ in range(2)]
@@ -104,8 +120,6 @@ class ShardedFrame:
             if not host_gather:
                 # reassembly (HBM-bound) on its own stream, overlapping the next renders (VALU-bound)
                 self.side = torch.cuda.Stream(device)
-                self.ev_gathered = [torch.cuda.Event() for _ in range(2)]
-                self.ev_assembled = [None, None]
         self.pending = [None, None]  # (work, nframes, batch number) per batch buffer
         self.rendered = 0            # frames rendered into the open batch
         self.open = 0                # batch buffer being filled
@@ -122,66 +136,90 @@ class ShardedFrame:
         self.ctx.render_bands(self.frame, self.scene if scene is None else scene, self.width, self.height,
                               L.band_rows, self.rank, self.world, L.nb_mine, buf, **outs)
 
+    def _render_stream(self, i: int):
+        k = i % self.S
+        return self.torch.cuda.current_stream() if k == 0 else self.extra[k - 1]
+
+    def _join(self) -> None:
+        """The current stream waits for every render stream."""
+        cur = self.torch.cuda.current_stream()
+        for st in self.extra:
+            ev = self.torch.cuda.Event()
+            ev.record(st)
+            cur.wait_event(ev)
+
     def _launch(self, b: int, n: int) -> None:
         self.batches += 1
         if self.world == 1:
             self.pending[b] = (None, n, self.batches)
             return
-        src = self.bufs[b].cpu() if self.host_gather else self.bufs[b]
+        torch = self.torch
         gl = list(self.recv[b].chunk(self.world)) if self.rank == 0 else None
-        if self.side is not None and self.ev_assembled[b] is not None:
-            import torch
-
-            # recv[b] is read by the reassembly of the batch two back
-            torch.cuda.current_stream().wait_event(self.ev_assembled[b])
-        work = self.dist.gather(src, gather_list=gl, dst=0, async_op=True)
+        if self.host_gather:
+            self._join()
+            work = self.dist.gather(self.bufs[b].cpu(), gather_list=gl, dst=0, async_op=True)
+        else:
+            with torch.cuda.stream(self.gstream):
+                for ev in self.ev_rendered[b]:
+                    if ev is not None:
+                        self.gstream.wait_event(ev)
+                if self.ev_assembled[b] is not None:
+                    self.gstream.wait_event(self.ev_assembled[b])  # recv[b] is still being reassembled
+                work = self.dist.gather(self.bufs[b], gather_list=gl, dst=0, async_op=True)
+        self.ev_rendered[b] = [None] * self.S
         self.pending[b] = (work, n, self.batches)
 
     def _retire(self, b: int) -> None:
         p = self.pending[b]
         if p is None:
             return
+        torch = self.torch
         work, n, seq = p
         self.pending[b] = None
-        if work is not None:
-            if self.side is not None:
-                import torch
-
-                with torch.cuda.stream(self.side):
-                    work.wait()  # the side stream waits for the gather
-                    self.ev_gathered[b].record(self.side)
+        if work is not None and not self.host_gather:
+            st = self.side if self.side is not None else self.gstream
+            with torch.cuda.stream(st):
+                work.wait()  # this stream waits for the gather
+                ev = torch.cuda.Event()
+                ev.record(st)
+                self.ev_free[b] = ev
+                if self.side is not None:
                     self.ctx.assemble_bands(self.recv[b], self.K * self.slice, self.slice, self.world,
                                             self.layout.band_rows, self.width, self.height, n, self.frames)
-                    ev = torch.cuda.Event()
-                    ev.record(self.side)
-                    self.ev_assembled[b] = ev
-                # bufs[b] (this rank's send buffer) is re-rendered next: after the gather
-                torch.cuda.current_stream().wait_event(self.ev_gathered[b])
-            else:
-                work.wait()
-                if self.rank == 0:
-                    src = self.recv[b]
-                    if self.host_gather:
-                        src = src.to(self.frames.device)
-                    self.ctx.assemble_bands(src, self.K * self.slice, self.slice, self.world, self.layout.band_rows,
-                                            self.width, self.height, n, self.frames)
-                    if self.host_gather:
-                        import torch
-
-                        torch.cuda.current_stream().synchronize()  # `src` is a temporary
+                    ea = torch.cuda.Event()
+                    ea.record(st)
+                    self.ev_assembled[b] = ea
+        elif work is not None:
+            work.wait()
+            if self.rank == 0:
+                src = self.recv[b].to(self.frames.device)
+                self.ctx.assemble_bands(src, self.K * self.slice, self.slice, self.world, self.layout.band_rows,
+                                        self.width, self.height, n, self.frames)
+                torch.cuda.current_stream().synchronize()  # `src` is a temporary
         self.frames_done += n
         if self.last is None or seq > self.last[0]:
             self.last = (seq, b, n - 1)
 
     def step(self, i: int, steps_total=None, events=None, scene=None) -> None:
+        torch = self.torch
         b, sub = (i // self.K) % 2, i % self.K
         if sub == 0:
             self._retire(b)  # the batch that used this buffer two batches ago
-        if events is not None:
-            events[0].record()
-        self.render_local(self.local_view(i), scene=scene, steps_total=steps_total)
-        if events is not None:
-            events[1].record()
+        st = self._render_stream(i)
+        if sub < self.S and self.ev_free[b] is not None:
+            st.wait_event(self.ev_free[b])  # first render of this stream into the batch buffer
+            if sub == min(self.S, self.K) - 1:
+                self.ev_free[b] = None
+        with torch.cuda.stream(st):
+            if events is not None:
+                events[0].record()
+            self.render_local(self.local_view(i), scene=scene, steps_total=steps_total)
+            if events is not None:
+                events[1].record()
+            if self.world > 1:
+                ev = torch.cuda.Event()
+                ev.record(st)
+                self.ev_rendered[b][i % self.S] = ev
         self.rendered = sub + 1
         self.open = b
         if sub == self.K - 1:
@@ -189,11 +227,19 @@ class ShardedFrame:
             self.rendered = 0
 
     def drain(self) -> None:
+        """Finish every batch; afterwards the current stream is ordered after all work."""
         if self.rendered:  # a partial batch
             self._launch(self.open, self.rendered)
             self.rendered = 0
         for b in (0, 1):
             self._retire(b)
+        self._join()
+        cur = self.torch.cuda.current_stream()
+        for st in (self.side, self.gstream):
+            if st is not None:
+                ev = self.torch.cuda.Event()
+                ev.record(st)
+                cur.wait_event(ev)
 
     def frame_rgba(self, i: int | None = None):
         """Rank 0's assembled frame: the last one retired (or frame slot i of

@@ -47,8 +47,9 @@ class FakeRcclGather:
         return _Work(t, done)
 
 
-@pytest.mark.parametrize("world,K,nframes", [(2, 4, 41), (3, 3, 10), (8, 4, 16)])
-def test_rank0_pipeline_assembles_frames(world, K, nframes):
+@pytest.mark.parametrize("S", [1, 2])
+@pytest.mark.parametrize("world,K,nframes", [(2, 4, 41), (3, 3, 10), (8, 4, 16), (8, 1, 5)])
+def test_rank0_pipeline_assembles_frames(world, K, nframes, S):
     import torch
 
     if not torch.cuda.is_available():
@@ -72,7 +73,7 @@ def test_rank0_pipeline_assembles_frames(world, K, nframes):
             ctx.render_bands(frame, scene, W, H, B, r, world, L.nb_mine, one)
         peers.append(one.repeat(K))
     fake = FakeRcclGather(torch, peers)
-    sf = ShardedFrame(ctx, frame, scene, W, H, B, 0, world, dev, dist=fake, frames_per_gather=K)
+    sf = ShardedFrame(ctx, frame, scene, W, H, B, 0, world, dev, dist=fake, frames_per_gather=K, render_streams=S)
     assert sf.side is not None
     for i in range(nframes):
         sf.step(i)
@@ -90,7 +91,8 @@ def test_rank0_pipeline_assembles_frames(world, K, nframes):
         assert torch.equal(sf.frame_rgba(k), ref), k
 
 
-def test_peer_rank_pipeline_runs_batches():
+@pytest.mark.parametrize("S", [1, 2])
+def test_peer_rank_pipeline_runs_batches(S):
     """A peer rank (rank 3 of 4): batches of K frames, each sent with one
     gather; the send buffer is re-rendered only after its gather completed."""
     import torch
@@ -123,7 +125,7 @@ def test_peer_rank_pipeline_runs_batches():
     ctx.set_sky(make_sky("equirect", (128, 64)))
     frame, scene = default_frame(W, H), default_scene(256)
     pg = PeerGather()
-    sf = ShardedFrame(ctx, frame, scene, W, H, B, rank, world, dev, dist=pg, frames_per_gather=K)
+    sf = ShardedFrame(ctx, frame, scene, W, H, B, rank, world, dev, dist=pg, frames_per_gather=K, render_streams=S)
     for i in range(10):
         sf.step(i)
     sf.drain()
@@ -133,6 +135,7 @@ def test_peer_rank_pipeline_runs_batches():
     one = torch.zeros(L.nb_max * B * W * 4, dtype=torch.uint8, device=dev)
     ctx.render_bands(frame, scene, W, H, B, rank, world, L.nb_mine, one)
     torch.cuda.synchronize()
-    for batch in pg.sent:
-        for k in range(K):
-            assert torch.equal(batch[k * one.numel():(k + 1) * one.numel()], one) or batch is pg.sent[-1]
+    used = L.nb_mine * B * W * 4  # rows past the rank's last band are never written
+    for j, batch in enumerate(pg.sent):
+        for k in range(K if j < 2 else 10 - 2 * K):
+            assert torch.equal(batch[k * one.numel():k * one.numel() + used], one[:used]), (j, k)

@@ -40,8 +40,11 @@ def main():
     st = np.empty(thetas.shape, np.uint32)
     for i, t in enumerate(thetas):
         ang[i], st[i] = O.geodesic_at_theta(50.0, 1.0, 2048, STEP, 2.5, float(t))
+    # configs' observer radii (rs = 1): configs 1-4 at |(2.5, 0, 0.1)|, config 5 at 1.3 (inside the photon sphere)
+    fan_cfg = O.solve_ray_fan(50.0, 1.0, 1000, STEP, 400, math.sqrt(2.5 ** 2 + 0.1 ** 2))
+    fan_cfg5 = O.solve_ray_fan(50.0, 1.0, 1000, STEP, 400, 1.3)
     np.savez(os.path.join(HERE, "fans.npz"), fan_ref=fan_ref, fan_test=fan_test, thetas=thetas,
-             angles=ang, steps=st)
+             angles=ang, steps=st, fan_cfg=fan_cfg, fan_cfg5=fan_cfg5)
 
     w, h = 64, 36
     frame = oracle_frame(w, h)

@@ -102,3 +102,17 @@ def test_theta_sweep_golden():
     for t, a, s in zip(gold["thetas"], gold["angles"], gold["steps"]):
         a2, s2 = O.geodesic_at_theta(50.0, 1.0, 2048, STEP, 2.5, float(t))
         assert a2 == a and s2 == s
+
+
+def test_config_radii_fan_goldens():
+    """400-node fans at the configs' observer radii (rs = 1): configs 1-4 at
+    |(2.5, 0, 0.1)| and config 5 at 1.3 rs.  Inside the photon sphere every
+    falling ray (theta > 0: nodes 0..199) is captured by the pre-filter
+    (sphere_ray_tracer.rs:116)."""
+    gold = np.load(os.path.join(GOLD, "fans.npz"))
+    np.testing.assert_array_equal(O.solve_ray_fan(50.0, 1.0, 1000, STEP, 400, math.sqrt(2.5 ** 2 + 0.01)),
+                                  gold["fan_cfg"])
+    f5 = O.solve_ray_fan(50.0, 1.0, 1000, STEP, 400, 1.3)
+    np.testing.assert_array_equal(f5, gold["fan_cfg5"])
+    assert np.all(f5[:200] < -7)
+    assert np.all(f5[-20:] > -7)  # outgoing rays near radial escape to the sphere

@@ -8,8 +8,9 @@
 //   geo_draw_kernel     the point pipeline: vs_main + PointList raster of the
 //                       red fs_main colour, REPLACE blend (shader.wgsl:36-74, pipeline.rs:55-74)
 //
-// Layout (HBM, SoA so that lane c touches consecutive words): node values
-// u[node * n_conn + c] (48 x 4 B per connector), point positions x[n] y[n]
+// Layout (HBM): node values in 64-connector tiles, u[(c/64)*48*64 + node*64 +
+// c%64] (48 x 4 B per connector; a wave's load of one node is 256 contiguous
+// bytes and its 48 loads one contiguous 12-KB block), point positions x[n] y[n]
 // z[n], one needs_reset byte per connector, vertices float4 per connector
 // (near-side connectors first, then far-side: get_vertices /
 // get_vertices_farside).  The 48-node state, the Thomas factors and residuals
@@ -27,7 +28,13 @@
 
 namespace {
 
-constexpr int kRaysBlock = 256;
+#ifndef GEO_RAYS_BLOCK
+#define GEO_RAYS_BLOCK 64  // one wave per block: +2 % over 256 (tools/gpu_ab.sh)
+#endif
+constexpr int kRaysBlock = GEO_RAYS_BLOCK;
+#ifndef GEO_RAYS_TILED
+#define GEO_RAYS_TILED 1  // node-value layout: 1 = 64-connector tiles (+4.5 %), 0 = node-major SoA (tools/gpu_ab.sh)
+#endif
 constexpr int kOrbitBlock = 64;  // f64 orbit lanes: few points, long serial chains
 
 // fastrand 2.0.1's generator (wyrand) and its f64 mapping, restated: one
@@ -78,6 +85,25 @@ struct RaysArgs {
     float4* out;                 // [n_conn]
 };
 
+// Node-value stream: read once and written once per call (GEO_RAYS_NT: non-temporal hints).
+#ifndef GEO_RAYS_NT
+#define GEO_RAYS_NT 1  // +5.5 % (tools/gpu_ab.sh, bench_points)
+#endif
+__device__ __forceinline__ float ld_(const float* p) {
+#if GEO_RAYS_NT
+    return __builtin_nontemporal_load(p);
+#else
+    return *p;
+#endif
+}
+__device__ __forceinline__ void st_(float* p, float v) {
+#if GEO_RAYS_NT
+    __builtin_nontemporal_store(v, p);
+#else
+    *p = v;
+#endif
+}
+
 // RESPAWN = false: one RayConnector call per connector (update_ray / reset_ray).
 // RESPAWN = true: the respawn pre-pass of PointCloud::update with orbits
 // (point_cloud.rs:129-134) — only the connectors of respawned points run, a
@@ -92,8 +118,14 @@ __global__ __launch_bounds__(kRaysBlock) void geo_rays_kernel(const RaysArgs a) 
     const uint32_t p = c >= a.n_points ? c - a.n_points : c;
     const uint32_t n = a.n_points;
     if (RESPAWN && !a.respawn[p]) return;
+#if GEO_RAYS_TILED
+    // node values in 64-connector tiles: a wave's 48 loads cover one contiguous 12-KB block
+    float* const ug = a.u + (size_t)(c / 64u) * (geo::kRayNodes * 64u) + (c % 64u);
+    const size_t stride = 64;
+#else
     float* const ug = a.u + c;
     const size_t stride = a.n_conn;
+#endif
     float u[geo::kRayNodes];
     bool needs = a.needs_reset[c] != 0;
     float ox = a.ox, oy = a.oy, oz = a.oz;
@@ -105,9 +137,9 @@ __global__ __launch_bounds__(kRaysBlock) void geo_rays_kernel(const RaysArgs a) 
     const float* src = RESPAWN ? a.respawn_pos : a.pos;
     const float px = src[p], py = src[n + p], pz = src[2 * n + p];
     const float angle = geo::ray_connect(a.rs, !far, px, py, pz, ox, oy, oz, RESPAWN || a.reset != 0,
-                                         a.iterations, &needs, [=](int i) { return ug[(size_t)i * stride]; }, u);
+                                         a.iterations, &needs, [=](int i) { return ld_(ug + (size_t)i * stride); }, u);
 #pragma unroll
-    for (int i = 0; i < geo::kRayNodes; ++i) ug[(size_t)i * stride] = u[i];
+    for (int i = 0; i < geo::kRayNodes; ++i) st_(ug + (size_t)i * stride, u[i]);
     a.needs_reset[c] = needs ? 1 : 0;
     if (!RESPAWN && a.out) a.out[c] = make_float4(px, py, pz, angle);
 }
@@ -208,12 +240,12 @@ int rays_init(geo_rays* r, geo_ctx* ctx, float rs, uint32_t n_points, uint32_t s
     r->sides = sides;
     r->n_conn = n_points * ((sides & GEO_RAYS_NEAR ? 1u : 0u) + (sides & GEO_RAYS_FAR ? 1u : 0u));
     int st;
-    if ((st = dmalloc(&r->pos, 3 * (size_t)n_points)) || (st = dmalloc(&r->u, (size_t)geo::kRayNodes * r->n_conn)) ||
+    if ((st = dmalloc(&r->pos, 3 * (size_t)n_points)) || (st = dmalloc(&r->u, (size_t)geo::kRayNodes * ((r->n_conn + 63u) / 64u * 64u))) ||
         (st = dmalloc(&r->needs_reset, r->n_conn)) || (st = dmalloc(&r->other, 3 * (size_t)n_points)) ||
         (st = dmalloc(&r->verts, r->n_conn)))
         return st;
     // RayConnector::new (:16-25): u_ray = 1, needs_reset
-    std::vector<float> ones((size_t)geo::kRayNodes * r->n_conn, 1.0f);
+    std::vector<float> ones((size_t)geo::kRayNodes * ((r->n_conn + 63u) / 64u * 64u), 1.0f);
     if (hipMemcpy(r->u, ones.data(), ones.size() * sizeof(float), hipMemcpyHostToDevice) != hipSuccess ||
         hipMemset(r->needs_reset, 1, r->n_conn) != hipSuccess ||
         hipMemset(r->verts, 0, sizeof(float4) * r->n_conn) != hipSuccess)

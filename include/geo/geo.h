@@ -171,11 +171,17 @@ int geo_render_bands(geo_ctx* ctx, const geo_frame* frame, const geo_scene* scen
  * (multi-GPU present): `src` (device) holds `world` rank blocks
  * of rank_stride bytes, rank r's block being its packed bands (bands r,
  * r+world, r+2*world, ... of band_rows rows) for nframes frames at
- * frame_stride bytes apart.  Writes nframes width x height RGBA8 frames
- * back to back to `dst` (device).  Asynchronous on `stream`. */
+ * frame_stride bytes apart, src_bpp bytes per pixel (4: RGBA8 as rendered,
+ * 3: RGB24 from geo_pack_rgb, width % 4 == 0).  Writes nframes width x height
+ * RGBA8 frames back to back to `dst` (device).  Asynchronous on `stream`. */
 int geo_assemble_bands(geo_ctx* ctx, const uint8_t* src, size_t rank_stride, size_t frame_stride, uint32_t world,
-                       uint32_t band_rows, uint32_t width, uint32_t height, uint32_t nframes, uint8_t* dst,
-                       void* stream);
+                       uint32_t band_rows, uint32_t width, uint32_t height, uint32_t nframes, uint32_t src_bpp,
+                       uint8_t* dst, void* stream);
+
+/* RGBA8 -> RGB24 (the alpha byte dropped: frames are opaque after the clear,
+ * renderer.rs:233-238) of npixels (a multiple of 4) device pixels: 25 % fewer
+ * bytes on the links for the multi-GPU present.  Asynchronous on `stream`. */
+int geo_pack_rgb(geo_ctx* ctx, const uint8_t* rgba, uint64_t npixels, uint8_t* rgb, void* stream);
 
 /* Adds the steps accumulated under GEO_FLAG_DEFER_STEPS to *steps_total
  * (device u64) and clears the context's counter.  Asynchronous on `stream`. */

@@ -149,11 +149,15 @@ class Context:
         check("geo_steps_flush", lib.geo_steps_flush(self._h, _ptr(steps_total), _stream_handle(stream)))
 
     def assemble_bands(self, src, rank_stride: int, frame_stride: int, world: int, band_rows: int, width: int,
-                       height: int, nframes: int, dst, stream=None) -> None:
-        """geo_assemble_bands: rank-packed bands (device) -> nframes frames (device)."""
+                       height: int, nframes: int, dst, src_bpp: int = 4, stream=None) -> None:
+        """geo_assemble_bands: rank-packed bands (device, RGBA8 or RGB24) -> nframes RGBA8 frames (device)."""
         check("geo_assemble_bands", lib.geo_assemble_bands(self._h, _ptr(src), rank_stride, frame_stride, world,
-                                                           band_rows, width, height, nframes, _ptr(dst),
+                                                           band_rows, width, height, nframes, src_bpp, _ptr(dst),
                                                            _stream_handle(stream)))
+
+    def pack_rgb(self, rgba, npixels: int, rgb, stream=None) -> None:
+        """geo_pack_rgb: RGBA8 -> RGB24 on the device (npixels % 4 == 0)."""
+        check("geo_pack_rgb", lib.geo_pack_rgb(self._h, _ptr(rgba), npixels, _ptr(rgb), _stream_handle(stream)))
 
     def render_rows(self, frame: GeoFrame, scene: GeoScene, width: int, height: int, row0: int, nrows: int,
                     out_rgba, out_mask=None, out_uv=None, out_steps=None, steps_total=None, stream=None) -> None:

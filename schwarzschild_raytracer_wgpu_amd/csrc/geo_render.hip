@@ -152,6 +152,43 @@ __global__ __launch_bounds__(256) void geo_assemble_kernel(const uint8_t* __rest
     d[x] = s[x];
 }
 
+// The same from RGB24-packed bands (geo_pack_rgb; alpha restored to 255):
+// one thread per 4 pixels (12 B in, 16 B out), W % 4 == 0.
+__global__ __launch_bounds__(256) void geo_assemble_rgb_kernel(const uint8_t* __restrict__ src, size_t rank_stride,
+                                                               size_t frame_stride, uint32_t world,
+                                                               uint32_t band_rows, uint32_t quads, uint32_t height,
+                                                               uint8_t* __restrict__ dst) {
+    const uint32_t x = blockIdx.x * 256u + threadIdx.x;
+    const uint32_t y = blockIdx.y;
+    const uint32_t f = blockIdx.z;
+    if (x >= quads) return;
+    const uint32_t b = y / band_rows;
+    const uint32_t r = b % world;
+    const size_t lrow = (size_t)(b / world) * band_rows + y % band_rows;
+    const uint32_t* s = reinterpret_cast<const uint32_t*>(src + r * rank_stride + f * frame_stride +
+                                                         lrow * (size_t)quads * 12u) + 3u * x;
+    const uint32_t w0 = s[0], w1 = s[1], w2 = s[2];  // r0 g0 b0 r1 | g1 b1 r2 g2 | b2 r3 g3 b3
+    uint4 o;
+    o.x = (w0 & 0x00FFFFFFu) | 0xFF000000u;
+    o.y = (w0 >> 24) | ((w1 & 0xFFFFu) << 8) | 0xFF000000u;
+    o.z = (w1 >> 16) | ((w2 & 0xFFu) << 16) | 0xFF000000u;
+    o.w = (w2 >> 8) | 0xFF000000u;
+    reinterpret_cast<uint4*>(dst + ((size_t)f * height + y) * (size_t)quads * 16u)[x] = o;
+}
+
+// RGBA8 -> RGB24 (alpha dropped: every frame pixel is opaque after the clear),
+// 4 pixels per thread.
+__global__ __launch_bounds__(256) void geo_pack_rgb_kernel(const uint4* __restrict__ src, uint64_t quads,
+                                                           uint32_t* __restrict__ dst) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+    if (i >= quads) return;
+    const uint4 p = src[i];
+    uint32_t* d = dst + 3u * i;
+    d[0] = (p.x & 0x00FFFFFFu) | (p.y << 24);
+    d[1] = ((p.y >> 8) & 0xFFFFu) | (p.z << 16);
+    d[2] = ((p.z >> 16) & 0xFFu) | (p.w << 8);
+}
+
 __global__ __launch_bounds__(kStepSlots) void geo_steps_finalize(unsigned long long* slots,
                                                                   unsigned long long* total) {
     __shared__ unsigned long long s[kStepSlots / 64];
@@ -483,18 +520,27 @@ static int render_impl(geo_ctx* c, const geo_frame* frame, const geo_scene* scen
 }
 
 int geo_assemble_bands(geo_ctx* c, const uint8_t* src, size_t rank_stride, size_t frame_stride, uint32_t world,
-                       uint32_t band_rows, uint32_t width, uint32_t height, uint32_t nframes, uint8_t* dst,
-                       void* stream) {
+                       uint32_t band_rows, uint32_t width, uint32_t height, uint32_t nframes, uint32_t src_bpp,
+                       uint8_t* dst, void* stream) {
     if (!c || !src || !dst || world == 0 || band_rows == 0 || width == 0 || height == 0 || nframes == 0 ||
-        height > 65535u || nframes > 65535u)
+        height > 65535u || nframes > 65535u || (src_bpp != 3u && src_bpp != 4u))
         return GEO_EINVAL;
-    const size_t row_bytes = (size_t)width * 4;
+    if (src_bpp == 3u && (width % 4u != 0 || rank_stride % 4u != 0 || frame_stride % 4u != 0 ||
+                          (uintptr_t)src % 4u != 0 || (uintptr_t)dst % 16u != 0))
+        return GEO_EINVAL;
+    const size_t row_bytes = (size_t)width * src_bpp;
     const size_t nb_max = ((size_t)(height + band_rows - 1) / band_rows + world - 1) / world;
     if (frame_stride < nb_max * band_rows * row_bytes || rank_stride < (size_t)nframes * frame_stride)
         return GEO_EINVAL;
     DeviceGuard g(c->device);
     if (!g.ok) return GEO_EHIP;
     hipStream_t s = (hipStream_t)stream;
+    if (src_bpp == 3u) {
+        const uint32_t quads = width / 4u;
+        hipLaunchKernelGGL(geo_assemble_rgb_kernel, dim3((quads + 255u) / 256u, height, nframes), dim3(256), 0, s,
+                           src, rank_stride, frame_stride, world, band_rows, quads, height, dst);
+        return hipGetLastError() == hipSuccess ? GEO_OK : GEO_EHIP;
+    }
     const bool wide = (width % 4u) == 0 && (rank_stride % 16u) == 0 && (frame_stride % 16u) == 0 &&
                       ((uintptr_t)src % 16u) == 0 && ((uintptr_t)dst % 16u) == 0;
     const uint32_t units = wide ? width / 4u : width;
@@ -505,6 +551,18 @@ int geo_assemble_bands(geo_ctx* c, const uint8_t* src, size_t rank_stride, size_
     else
         hipLaunchKernelGGL(geo_assemble_kernel<uint32_t>, grid, dim3(256), 0, s, src, rank_stride, frame_stride,
                            world, band_rows, units, height, dst);
+    return hipGetLastError() == hipSuccess ? GEO_OK : GEO_EHIP;
+}
+
+int geo_pack_rgb(geo_ctx* c, const uint8_t* rgba, uint64_t npixels, uint8_t* rgb, void* stream) {
+    if (!c || !rgba || !rgb || npixels == 0 || npixels % 4u != 0 || (uintptr_t)rgba % 16u != 0 ||
+        (uintptr_t)rgb % 4u != 0)
+        return GEO_EINVAL;
+    DeviceGuard g(c->device);
+    if (!g.ok) return GEO_EHIP;
+    const uint64_t quads = npixels / 4u;
+    hipLaunchKernelGGL(geo_pack_rgb_kernel, dim3((unsigned)((quads + 255u) / 256u)), dim3(256), 0, (hipStream_t)stream,
+                       reinterpret_cast<const uint4*>(rgba), quads, reinterpret_cast<uint32_t*>(rgb));
     return hipGetLastError() == hipSuccess ? GEO_OK : GEO_EHIP;
 }
 

@@ -47,9 +47,10 @@ class FakeRcclGather:
         return _Work(t, done)
 
 
+@pytest.mark.parametrize("rgb", [True, False], ids=["rgb24", "rgba8"])
 @pytest.mark.parametrize("S", [1, 2])
 @pytest.mark.parametrize("world,K,nframes", [(2, 4, 41), (3, 3, 10), (8, 4, 16), (8, 1, 5)])
-def test_rank0_pipeline_assembles_frames(world, K, nframes, S):
+def test_rank0_pipeline_assembles_frames(world, K, nframes, S, rgb):
     import torch
 
     if not torch.cuda.is_available():
@@ -63,18 +64,22 @@ def test_rank0_pipeline_assembles_frames(world, K, nframes, S):
     ctx = g.Context(0)
     ctx.set_sky(make_sky("equirect", (256, 128)))
     frame, scene = default_frame(W, H), default_scene(512)
-    # the peers' K-frame batches (every frame identical)
-    peers = []
+    fake = FakeRcclGather(torch, [])
+    sf = ShardedFrame(ctx, frame, scene, W, H, B, 0, world, dev, dist=fake, frames_per_gather=K, render_streams=S,
+                      present_rgb=rgb)
+    assert sf.side is not None and sf.bpp == (3 if rgb else 4)
+    # the peers' K-frame batches (every frame identical), in the travelling format
     for r in range(1, world):
         L = BandLayout(H, B, world, r)
         sl = L.nb_max * B * W * 4
         one = torch.zeros(sl, dtype=torch.uint8, device=dev)
         if L.nb_mine:
             ctx.render_bands(frame, scene, W, H, B, r, world, L.nb_mine, one)
-        peers.append(one.repeat(K))
-    fake = FakeRcclGather(torch, peers)
-    sf = ShardedFrame(ctx, frame, scene, W, H, B, 0, world, dev, dist=fake, frames_per_gather=K, render_streams=S)
-    assert sf.side is not None
+        if sf.bpp == 3:
+            packed = torch.empty(sl // 4 * 3, dtype=torch.uint8, device=dev)
+            ctx.pack_rgb(one, sl // 4, packed)
+            one = packed
+        fake.peer_bufs.append(one.repeat(K))
     for i in range(nframes):
         sf.step(i)
     sf.drain()
@@ -135,7 +140,12 @@ def test_peer_rank_pipeline_runs_batches(S):
     one = torch.zeros(L.nb_max * B * W * 4, dtype=torch.uint8, device=dev)
     ctx.render_bands(frame, scene, W, H, B, rank, world, L.nb_mine, one)
     torch.cuda.synchronize()
-    used = L.nb_mine * B * W * 4  # rows past the rank's last band are never written
+    if sf.bpp == 3:
+        packed = torch.empty(one.numel() // 4 * 3, dtype=torch.uint8, device=dev)
+        ctx.pack_rgb(one, one.numel() // 4, packed)
+        torch.cuda.synchronize()
+        one = packed
+    used = L.nb_mine * B * W * sf.bpp  # rows past the rank's last band are never written
     for j, batch in enumerate(pg.sent):
         for k in range(K if j < 2 else 10 - 2 * K):
             assert torch.equal(batch[k * one.numel():k * one.numel() + used], one[:used]), (j, k)

@@ -442,3 +442,14 @@ def test_assemble_bands_matches_host_assembly(geo, torch_mod, world, W, H, B, K)
         full = torch_mod.zeros(frame_bytes, dtype=torch_mod.uint8)
         assemble(full, gl, L, row_bytes, frame=f, frame_stride=sl)
         assert np.array_equal(got[f * H * row_bytes:(f + 1) * H * row_bytes], full[:H * row_bytes].numpy()), f
+    if W % 4 == 0:
+        # RGB24 transport: pack, reassemble with alpha restored == the RGBA path on opaque pixels
+        src[3::4] = 255
+        dsrc = torch_mod.from_numpy(src).to(dev)
+        packed = torch_mod.empty(src.size // 4 * 3, dtype=torch_mod.uint8, device=dev)
+        ctx.pack_rgb(dsrc, src.size // 4, packed)
+        out3 = torch_mod.zeros_like(out)
+        ctx.assemble_bands(packed, K * sl // 4 * 3, sl // 4 * 3, world, B, W, H, K, out3, src_bpp=3)
+        out4 = torch_mod.zeros_like(out)
+        ctx.assemble_bands(dsrc, K * sl, sl, world, B, W, H, K, out4)
+        assert torch_mod.equal(out3, out4)

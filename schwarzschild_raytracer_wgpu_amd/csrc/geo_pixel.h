@@ -18,6 +18,12 @@
 
 #include "geo_math.h"
 
+// 1: one exit test per group where the stop set is absorbing (run_groups);
+// 0: a test per step everywhere (A/B switch, tools/gpu_ab.sh).
+#ifndef GEO_ABSORBING_TEST
+#define GEO_ABSORBING_TEST 1
+#endif
+
 namespace geo {
 
 constexpr float kNoValue = 15.0f;          // SphereRayTracer::NO_VALUE, sphere_ray_tracer.rs:22
@@ -290,9 +296,12 @@ template <int KIND>
 struct StopTest {
     float SU, BD, HU, lo, hi;
     bool above0;
+    bool absorbing;  // the stop set is absorbing (run_groups): observer inside the sphere, sphere
+                     // beyond the photon sphere (SU < 1: F < 0 below SU), outside the horizon
     GEO_HDM explicit StopTest(const PixelConsts& k) : SU(k.SU), BD(k.BD), HU(k.HU), above0(k.U0 > k.SU) {
         lo = above0 ? k.SUp : BD;
         hi = above0 ? HU : SU;
+        absorbing = KIND != kCurvedIn && above0 && (KIND == kFlat || SU < 1.0f);
     }
     GEO_HDM bool operator()(float NU, float NUB) const {
         if constexpr (KIND == kCurvedIn)
@@ -301,6 +310,44 @@ struct StopTest {
             return med3_(NU, lo, hi) != NU;
     }
 };
+
+// The group loop: G RK4 steps per exit test; returns the steps before the
+// stopping group (or `all` when the budget of whole groups runs out), with the
+// group's G + 1 states in su_/sb_.
+//
+// LAST_ONLY tests only the group's last state.  That is exact when the stop
+// set is ABSORBING: once a step's state is in it, every later state is too.
+// It holds for an observer inside the sphere outside the horizon (kCurvedOut,
+// kFlat with U0 > SU) when the sphere lies beyond the photon sphere (SU < 1),
+// whose stop set is then {U <= SU} + {U > HU} + NaN:
+//  * U <= SU < 1 (r > 1.5 rs): F(U) < 0, so U' falls by ~h|F| per step.  The
+//    step that first lands at U <= SU came from above, and U' is already
+//    negative after it.  u has no minimum beyond the photon sphere (u'' < 0
+//    there), so U keeps falling until it escapes (U < BD < SU) or goes NaN.
+//  * U > HU = 1.5 (inside the horizon): F(U) > 0, so U' grows by ~h F and U
+//    keeps rising.
+// The margins (h|F| ~ 1e-3 per step) dwarf f32 rounding.  The GPU parity tests
+// and the host-compiled header tests check it bit for bit against the
+// oracle's literal per-step test.  An observer outside the sphere can graze
+// it, entering and leaving within a group, and inside the photon sphere u has
+// minima, so those keep the per-step test.
+template <int G, int KIND, bool LAST_ONLY>
+GEO_HD uint32_t run_groups(const StopTest<KIND>& stop_at, uint32_t ngroups, uint32_t all, float h, float hh,
+                           float hh2, float hhh, float h6, float h2_6, float (&su_)[G + 1], float (&sb_)[G + 1]) {
+    for (uint32_t q = 0; q < ngroups; ++q) {
+        bool stop = false;
+#pragma unroll
+        for (int j = 0; j < G; ++j) {
+            rk4_step<KIND>(su_[j], sb_[j], h, hh, hh2, hhh, h6, h2_6, &su_[j + 1], &sb_[j + 1]);
+            if constexpr (!LAST_ONLY) stop = stop | stop_at(su_[j + 1], sb_[j + 1]);
+        }
+        if constexpr (LAST_ONLY) stop = stop_at(su_[G], sb_[G]);
+        if (stop) return q * (uint32_t)G;
+        su_[0] = su_[G];
+        sb_[0] = sb_[G];
+    }
+    return all;
+}
 
 // Traveled angle of the ray at angle theta to the black hole, or kNoValue.
 // *steps = executed main-loop RK4 steps.  LOOP = RK4 steps per exit test
@@ -323,7 +370,6 @@ GEO_HD float geodesic_angle_v(const PixelConsts& k, float st, float ct, uint32_t
     constexpr int G = LOOP;
     const uint32_t ms = k.max_steps;
     const uint32_t ngroups = ms / (uint32_t)G;
-    uint32_t it = ngroups * (uint32_t)G;  // per lane: steps before its stopping group (budget: all)
     float su_[G + 1], sb_[G + 1];
     su_[0] = U;
     sb_[0] = UB;
@@ -332,20 +378,14 @@ GEO_HD float geodesic_angle_v(const PixelConsts& k, float st, float ct, uint32_t
         su_[j] = U;
         sb_[j] = UB;
     }
-    for (uint32_t q = 0; q < ngroups; ++q) {
-        bool stop = false;
-#pragma unroll
-        for (int j = 0; j < G; ++j) {
-            rk4_step<KIND>(su_[j], sb_[j], h, hh, hh2, hhh, h6, h2_6, &su_[j + 1], &sb_[j + 1]);
-            stop = stop | stop_at(su_[j + 1], sb_[j + 1]);
-        }
-        if (stop) {
-            it = q * (uint32_t)G;
-            break;
-        }
-        su_[0] = su_[G];
-        sb_[0] = sb_[G];
-    }
+    // per lane: steps before its stopping group (budget: all)
+    uint32_t it;
+    if (stop_at.absorbing)  // frame-uniform
+        it = run_groups<G, KIND, GEO_ABSORBING_TEST != 0>(stop_at, ngroups, ngroups * (uint32_t)G, h, hh, hh2, hhh,
+                                                          h6, h2_6, su_, sb_);
+    else
+        it = run_groups<G, KIND, false>(stop_at, ngroups, ngroups * (uint32_t)G, h, hh, hh2, hhh, h6, h2_6, su_,
+                                        sb_);
     // Opaque copies: the per-step flags are recomputed from the state rather
     // than carried out of the loop as lane masks.
 #pragma unroll

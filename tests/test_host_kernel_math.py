@@ -61,6 +61,14 @@ CASES = [
     ("inside_horizon", 64, 64, dict(pos=(0.8, 0.0, 0.05)), dict(r_obs=math.sqrt(0.64 + 0.0025))),
     ("flat_space", 64, 36, dict(rs=0.0, state=0), dict(rs=0.0)),
     ("outside_sphere", 64, 36, dict(pos=(60.0, 0.0, 1.0)), dict(r_obs=math.sqrt(3601.0))),
+    # the one-test-per-group loop (absorbing stop set) right at its limit, SU = 1.5/1.51 < 1,
+    # and the per-step loop with the sphere inside the photon sphere (SU = 1.5/1.4 > 1)
+    ("sphere_just_beyond_photon_sphere", 96, 54, dict(pos=(1.2, 0.3, 0.05), camera=(math.pi + 0.4, 0.2)),
+     dict(sphere_r=1.51, r_obs=math.sqrt(1.44 + 0.09 + 0.0025))),
+    ("sphere_1p6_observer_near_it", 96, 54, dict(pos=(1.55, 0.1, 0.0), camera=(0.3, 0.1)),
+     dict(sphere_r=1.6, r_obs=math.sqrt(1.55 ** 2 + 0.01))),
+    ("sphere_inside_photon_sphere", 96, 54, dict(pos=(1.2, 0.0, 0.05), camera=(math.pi + 1.0, 0.0)),
+     dict(sphere_r=1.4, r_obs=math.sqrt(1.44 + 0.0025))),
 ]
 
 

@@ -101,6 +101,11 @@ SCENES = [
     ("single_row", 97, 1, {}, dict(max_steps=512), "equirect"),
     ("single_col", 1, 77, {}, dict(max_steps=512), "equirect"),
     ("translucent_sky", 120, 68, {}, dict(max_steps=512), "random_alpha"),
+    # both sides of the one-test-per-group loop's limit (sphere beyond / inside the photon sphere)
+    ("sphere_just_beyond_photon_sphere", 160, 90, dict(pos=(1.2, 0.3, 0.05), camera=(math.pi + 0.4, 0.2)),
+     dict(sphere_r=1.51, r_obs=math.sqrt(1.44 + 0.09 + 0.0025)), "equirect"),
+    ("sphere_inside_photon_sphere", 160, 90, dict(pos=(1.2, 0.0, 0.05), camera=(math.pi + 1.0, 0.0)),
+     dict(sphere_r=1.4, r_obs=math.sqrt(1.44 + 0.0025)), "equirect"),
 ]
 
 
@@ -345,8 +350,33 @@ def test_invalid_arguments(geo, torch_mod):
         st = _lib.lib.geo_render_rows(ctx._h, ctypes.byref(frame), ctypes.byref(sc), 8, 8, 0, 8, out.data_ptr(),
                                       None, None, None, None, None)
         assert st == _lib.GEO_EINVAL
+    # empty frames / row ranges and the step budget limit (a wave's step sum must fit u32)
+    for args in ((0, 8, 0, 8), (8, 0, 0, 8), (8, 8, 0, 0)):
+        st = _lib.lib.geo_render_rows(ctx._h, ctypes.byref(frame), ctypes.byref(scene), *args, out.data_ptr(),
+                                      None, None, None, None, None)
+        assert st == _lib.GEO_EINVAL, args
+    big = default_scene((1 << 24) + 1)
+    st = _lib.lib.geo_render_rows(ctx._h, ctypes.byref(frame), ctypes.byref(big), 8, 8, 0, 8, out.data_ptr(),
+                                  None, None, None, None, None)
+    assert st == _lib.GEO_EINVAL
     with pytest.raises(geo.GeoError):
         geo.Context(99)
+
+
+def test_maximum_step_budget_bitexact(geo, torch_mod):
+    """The largest budget the ABI accepts (2^24 steps): every ray still stops on its own
+    (crossing, escape or horizon), so the frame equals the oracle's and the 2048-step frame's."""
+    w, h = 64, 36
+    from schwarzschild_raytracer_wgpu_amd.scenes import make_sky
+
+    sky = make_sky("equirect", (128, 64))
+    frame = default_frame(w, h)
+    ctx = make_ctx(geo, sky)
+    hip = render(geo, torch_mod, ctx, frame, default_scene(1 << 24), w, h)
+    ref = O.render_f32(frame, default_scene(1 << 24), sky, w, h, threads=8)
+    assert_same(hip, ref)
+    hip2k = render(geo, torch_mod, ctx, frame, default_scene(2048), w, h)
+    assert np.array_equal(hip["rgba"], hip2k["rgba"]) and np.array_equal(hip["steps"], hip2k["steps"])
 
 
 def test_three_sphere_composite_bitexact(geo, torch_mod):

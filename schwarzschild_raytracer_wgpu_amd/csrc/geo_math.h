@@ -41,6 +41,33 @@ constexpr float kInvPi = 0.318309886183790671538f;
 constexpr float kInvTwoPi = 0.159154943091895335769f;
 
 GEO_HD float fmaf_(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
+
+// Correctly rounded sqrt, equal to __builtin_sqrtf for every input.  On the
+// device, hipcc's correctly rounded sequence wraps the ±1-ulp correction of
+// v_sqrt_f32 in a 2^32 pre-scale for x < 2^-96 and a class fix-up for
+// ±0/+inf (≈ 17 VALU).  For x >= 2^-96 (finite or +inf) the scale is not
+// applied and the fix-up returns the corrected value, so the correction alone
+// gives the same bits (9 VALU).  Smaller, zero and NaN inputs take the builtin
+// (a branch that no lane of a typical wave takes).  Exhaustively checked
+// against __builtin_sqrtf over all 2^32 inputs (tests/test_gpu_math.py).
+#ifndef GEO_FAST_SQRT
+#define GEO_FAST_SQRT 1  // 0: the builtin everywhere (A/B switch, tools/gpu_ab.sh)
+#endif
+GEO_HD float sqrtf_(float x) {
+#if defined(__HIP_DEVICE_COMPILE__) && GEO_FAST_SQRT
+    if (x >= 0x1p-96f) {
+        const float s = __builtin_amdgcn_sqrtf(x);
+        const uint32_t si = __builtin_bit_cast(uint32_t, s);
+        const float sm = __builtin_bit_cast(float, si - 1u);
+        const float sp = __builtin_bit_cast(float, si + 1u);
+        const float rm = __builtin_fmaf(-sm, s, x);
+        const float rp = __builtin_fmaf(-sp, s, x);
+        const float t = (0.0f >= rm) ? sm : s;
+        return (0.0f < rp) ? sp : t;
+    }
+#endif
+    return __builtin_sqrtf(x);
+}
 GEO_HD float clampf_(float x, float lo, float hi) { return x < lo ? lo : (x > hi ? hi : x); }
 // max(a, b) with a NaN `a` mapped to b (used to clamp radicands at 0).
 GEO_HD float fmaxf_(float a, float b) { return a > b ? a : b; }
@@ -70,7 +97,7 @@ GEO_HD float asinf_(float x) {
     const float a = __builtin_fabsf(x);
     const bool big = a > 0.5f;
     const float z = big ? 0.5f * (1.0f - a) : a * a;
-    const float s = big ? __builtin_sqrtf(z) : a;
+    const float s = big ? sqrtf_(z) : a;
     const float p = fmaf_(fmaf_(fmaf_(fmaf_(4.2163199048e-2f, z, 2.4181311049e-2f), z,
                                       4.5470025998e-2f), z, 7.4953002686e-2f), z,
                           1.6666752422e-1f);
@@ -104,7 +131,7 @@ GEO_HD float acosf_(float x) {
     const float a = __builtin_fabsf(x);
     if (a <= 0.5f) return kPi2 - asinf_(x);
     const float z = 0.5f * (1.0f - a);
-    const float s = __builtin_sqrtf(z);
+    const float s = sqrtf_(z);
     const float p = fmaf_(fmaf_(fmaf_(fmaf_(4.2163199048e-2f, z, 2.4181311049e-2f), z,
                                       4.5470025998e-2f), z, 7.4953002686e-2f), z,
                           1.6666752422e-1f);

@@ -269,7 +269,7 @@ GEO_HD bool geodesic_init(const PixelConsts& k, float st, float ct, float* early
     }
     // RK4 init (:122-132); the radicand is clamped at 0 (the reference yields
     // NaN there only for |theta| < ~1e-8, never at a fan node).
-    float ub = __builtin_sqrtf(fmaxf_(0.0f, inv_b2 - k.h_over_r2));
+    float ub = sqrtf_(fmaxf_(0.0f, inv_b2 - k.h_over_r2));
     if (!falling) ub = -ub;
     // loop test of :134-135 on the initial state (schwarz_u = +inf for rs = 0)
     if ((k.u0 > k.schwarz_u && ub > 0.0f) || k.max_steps == 0u || !(k.u0 > 0.0f)) {
@@ -567,7 +567,7 @@ GEO_HD void pixel_central_dir(const float* m0, const float* m1, float psi_k, flo
     const float cz = m0[14];
     float dx, dy, dz;
     mat3_mul(m0, cx, cy, cz, &dx, &dy, &dz);
-    const float len = __builtin_sqrtf(fmaf_(dz, dz, fmaf_(dy, dy, dx * dx)));
+    const float len = sqrtf_(fmaf_(dz, dz, fmaf_(dy, dy, dx * dx)));
     const float id = 1.0f / fmaf_(-psi_k, dz, len);
     const float g = kt * id;
     // to_cart, then movement_to_central (:72-74)
@@ -587,7 +587,7 @@ GEO_HD float fan_lerp(const float* fan, uint32_t n, float st) {
 }
 
 // |(c2x, c2y)| = cos theta of the central-frame direction (to_polar, :75).
-GEO_HD float central_rho(float c2x, float c2y) { return __builtin_sqrtf(fmaf_(c2y, c2y, c2x * c2x)); }
+GEO_HD float central_rho(float c2x, float c2y) { return sqrtf_(fmaf_(c2y, c2y, c2x * c2x)); }
 
 // shader.wgsl:90-100 — (phi of c2, lambda') to sky-sphere (U, V); rho = central_rho.
 GEO_HD void sky_uv(const float* m2, float c2x, float c2y, float rho, float lam, float* U, float* V) {

@@ -1,0 +1,28 @@
+"""Device math that must equal hipcc's correctly rounded builtins bit for bit:
+geo::sqrtf_ (geo_math.h) against __builtin_sqrtf over all 2^32 inputs, on the
+GPU (tests/native/sqrt_exhaustive.hip, built here with hipcc for gfx950)."""
+import os
+import shutil
+import subprocess
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+
+
+def test_sqrt_exhaustive(tmp_path):
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    if not (os.path.exists(HIPCC) or shutil.which("hipcc")):
+        pytest.skip("no hipcc")
+    exe = str(tmp_path / "sqrt_exhaustive")
+    subprocess.run([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off",
+                    "-fhip-fp32-correctly-rounded-divide-sqrt", "-fno-gpu-flush-denormals-to-zero",
+                    os.path.join(HERE, "native", "sqrt_exhaustive.hip"), "-o", exe], check=True)
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "mismatches 0" in r.stdout, r.stdout + r.stderr

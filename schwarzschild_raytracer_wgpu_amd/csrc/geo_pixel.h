@@ -616,7 +616,20 @@ GEO_HD void sky_uv(const float* m2, float c2x, float c2y, float rho, float lam, 
 // (R|B and G|A in the two 16-bit halves of a u32; no field overflows).
 GEO_HD uint32_t rb_(uint32_t t) { return t & 0x00FF00FFu; }
 GEO_HD uint32_t ga_(uint32_t t) { return (t >> 8) & 0x00FF00FFu; }
-GEO_HD uint32_t lerp2_(uint32_t a, uint32_t b, uint32_t ia, uint32_t wb) { return a * ia + b * wb; }
+// Operands < 2^24 (packed pairs <= 0x00FF00FF, weights <= 256): the 24-bit
+// multiply (v_mul_u32_u24 / v_mad_u32_u24, full rate) gives the same low 32
+// bits as v_mul_lo_u32 (quarter rate), which is what hipcc picks otherwise.
+#ifndef GEO_MUL24
+#define GEO_MUL24 1  // 0: plain 32-bit multiplies (A/B switch, tools/gpu_ab.sh)
+#endif
+GEO_HD uint32_t mul24_(uint32_t a, uint32_t b) {
+#if defined(__HIP_DEVICE_COMPILE__) && GEO_MUL24
+    return (uint32_t)__umul24(a, b);
+#else
+    return a * b;
+#endif
+}
+GEO_HD uint32_t lerp2_(uint32_t a, uint32_t b, uint32_t ia, uint32_t wb) { return mul24_(a, ia) + mul24_(b, wb); }
 GEO_HD uint32_t div255_(uint32_t v) {  // round(v / 255) for v <= 255 * 255
     const uint32_t p = v + 128u;
     return (p + (p >> 8)) >> 8;

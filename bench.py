@@ -29,10 +29,10 @@ PEAK_FP32_TFLOPS = 157.3  # MI355X FP32 vector peak (MI355X_MICROARCH.md, spec)
 FLOPS_PER_EVAL = 40  # one RK4 evaluation of u'' = -u + 1.5 rs u^2
 NEWTON_EVALS = 3  # per sphere crossing (sphere_ray_tracer.rs:129)
 # adaptive mode (config 5): one Dormand-Prince RK5(4) attempt in Nystrom form
-# (geo_pixel.h dp5_step, counting an FMA as 2): 83 flops with the error
-# estimate, 72 for a Newton evaluation (no estimate)
-FLOPS_PER_ATTEMPT = 83
-FLOPS_PER_NEWTON_DP5 = 72
+# (geo_pixel.h dp5_step, counting an FMA as 2): 77 flops with the error
+# estimate and its h^2 scaling, 67 for a Newton evaluation (no estimate)
+FLOPS_PER_ATTEMPT = 77
+FLOPS_PER_NEWTON_DP5 = 67
 
 
 def parse():

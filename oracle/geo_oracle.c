@@ -402,17 +402,20 @@ static void dp5f(float U, float V, float h, int flat, float* NU, float* NV, floa
     const float A2[6][4] = {{0}, {0}, {DP_A31}, {DP_A41, DP_A42}, {DP_A51, DP_A52, DP_A53},
                             {DP_A61, DP_A62, DP_A63, DP_A64}};
     const float C[6] = {0.0f, DP_C2, DP_C3, DP_C4, DP_C5, 1.0f};
+    /* U_i = (U + c_i hV) + h^2 S_i, S_i over j < i-1 ((A^2)_{i,i-1} = 0);
+     * c6 = 1: U + hV itself, shared with NU */
+    const float hv = h * V, hh = h * h, w = U + hv;
     G[0] = Ff(U, flat);
     for (int i = 1; i < 6; ++i) {
-        /* U_i = U + h (c_i V + h S_i); S_i over j < i-1 ((A^2)_{i,i-1} = 0); c6 = 1: V itself */
-        float cv = i == 5 ? V : C[i] * V;
         if (i == 1)
-            Ui = fmaf(h, cv, U);
+            Ui = fmaf(C[i], hv, U);
+        else if (i == 5)
+            Ui = fmaf(hh, wsum(A2[i], G, i - 1), w);
         else
-            Ui = fmaf(h, fmaf(h, wsum(A2[i], G, i - 1), cv), U);
+            Ui = fmaf(hh, wsum(A2[i], G, i - 1), fmaf(C[i], hv, U));
         G[i] = Ff(Ui, flat);
     }
-    *NU = fmaf(h, fmaf(h, wsum(DP_Q, G, 6), V), U);
+    *NU = fmaf(hh, wsum(DP_Q, G, 6), w);
     *NV = fmaf(h, wsum(DP_B, G, 6), V);
     *SE = wsum(DP_E, G, 6);
 }

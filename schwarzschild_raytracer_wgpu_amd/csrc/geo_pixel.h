@@ -449,7 +449,7 @@ GEO_HD float geodesic_angle(const PixelConsts& k, float st, float ct, uint32_t* 
 // and the embedded error estimate in U is h^2 sum_j ((b - b*)A)_j G_j (stage 7,
 // the FSAL stage, does not enter it).  Coefficients: exact rationals rounded
 // once to f32 (tools/dp5_coeffs.py); zeros dropped ((A^2)_{i,i-1} = b2 =
-// (bA)_2 = (bA)_6 = (eA)_2 = 0, c6 = 1).  49 VALU ops per attempt.
+// (bA)_2 = (bA)_6 = (eA)_2 = 0, c6 = 1).  44 VALU ops per attempt.
 namespace dp5 {
 constexpr float c2 = 0x1.99999ap-3f, c3 = 0x1.333334p-2f, c4 = 0x1.99999ap-1f, c5 = 0x1.c71c72p-1f;
 constexpr float a31 = 0x1.70a3d8p-5f;
@@ -464,21 +464,25 @@ constexpr float e1 = 0x1.5b9754p-9f, e3 = -0x1.938a4p-8f, e4 = 0x1.4da74p-7f, e5
 }  // namespace dp5
 
 // One attempt: 5th-order (NU, NV) and the error sum SE (error = |SE| h^2).
+// Stage values as U_i = (U + c_i hV) + h^2 S_i with hV = h V and h^2 formed
+// once (c6 = 1 shares U + hV with NU): 44 VALU per attempt.
 template <int KIND>
-GEO_HD void dp5_step(float U, float V, float h, float* NU, float* NV, float* SE) {
+GEO_HD void dp5_step(float U, float V, float h, float hh, float* NU, float* NV, float* SE) {
     using namespace dp5;
+    const float hv = h * V;
     const float g1 = F_<KIND>(U);
-    const float u2 = fmaf_(h, c2 * V, U);
+    const float u2 = fmaf_(c2, hv, U);
     const float g2 = F_<KIND>(u2);
-    const float u3 = fmaf_(h, fmaf_(h, a31 * g1, c3 * V), U);
+    const float u3 = fmaf_(hh, a31 * g1, fmaf_(c3, hv, U));
     const float g3 = F_<KIND>(u3);
-    const float u4 = fmaf_(h, fmaf_(h, fmaf_(a42, g2, a41 * g1), c4 * V), U);
+    const float u4 = fmaf_(hh, fmaf_(a42, g2, a41 * g1), fmaf_(c4, hv, U));
     const float g4 = F_<KIND>(u4);
-    const float u5 = fmaf_(h, fmaf_(h, fmaf_(a53, g3, fmaf_(a52, g2, a51 * g1)), c5 * V), U);
+    const float u5 = fmaf_(hh, fmaf_(a53, g3, fmaf_(a52, g2, a51 * g1)), fmaf_(c5, hv, U));
     const float g5 = F_<KIND>(u5);
-    const float u6 = fmaf_(h, fmaf_(h, fmaf_(a64, g4, fmaf_(a63, g3, fmaf_(a62, g2, a61 * g1))), V), U);
+    const float w = U + hv;
+    const float u6 = fmaf_(hh, fmaf_(a64, g4, fmaf_(a63, g3, fmaf_(a62, g2, a61 * g1))), w);
     const float g6 = F_<KIND>(u6);
-    *NU = fmaf_(h, fmaf_(h, fmaf_(q5, g5, fmaf_(q4, g4, fmaf_(q3, g3, q1 * g1))), V), U);
+    *NU = fmaf_(hh, fmaf_(q5, g5, fmaf_(q4, g4, fmaf_(q3, g3, q1 * g1))), w);
     *NV = fmaf_(h, fmaf_(b6, g6, fmaf_(b5, g5, fmaf_(b4, g4, fmaf_(b3, g3, b1 * g1)))), V);
     *SE = fmaf_(e6, g6, fmaf_(e5, g5, fmaf_(e4, g4, fmaf_(e3, g3, e1 * g1))));
 }
@@ -508,15 +512,17 @@ GEO_HD float geodesic_angle_adaptive(const PixelConsts& k, float st, float ct, u
     while (it < ms) {
         ++it;
         float SE;
-        dp5_step<KIND>(U, V, h, &NU, &NV, &SE);
-        const float err = __builtin_fabsf(SE) * (h * h);
+        const float hh = h * h;
+        dp5_step<KIND>(U, V, h, hh, &NU, &NV, &SE);
+        const float err = __builtin_fabsf(SE) * hh;
         const bool acc = !(err > k.tolU);
         if (acc && stop_at(NU, NV)) {
             stopped = true;
             break;
         }
-        const float h2 = h + h;
-        const float hg = err < k.tolG ? (h2 < k.hmax ? h2 : k.hmax) : h;
+        // min(2h, hmax) as a growth test: h is step/2^j or step*2^j <= hmax with
+        // hmax = 16 step, so h < hmax implies 2h <= hmax (same bits, 2 fewer VALU)
+        const float hg = (err < k.tolG && h < k.hmax) ? h + h : h;
         U = acc ? NU : U;
         V = acc ? NV : V;
         ang = acc ? ang + h : ang;
@@ -534,7 +540,7 @@ GEO_HD float geodesic_angle_adaptive(const PixelConsts& k, float st, float ct, u
     for (int n = 0; n < kNewtonIters; ++n) {
         ns = ns - (wu - k.SU) / wv;
         float se;
-        dp5_step<KIND>(U, V, ns, &wu, &wv, &se);
+        dp5_step<KIND>(U, V, ns, ns * ns, &wu, &wv, &se);
     }
     return ang + ns;
 }

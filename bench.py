@@ -174,6 +174,22 @@ def main():
         dist.barrier()
     t1 = time.perf_counter()
     elapsed = t1 - t0
+    # compute-only pass (SURVEY.md §8e asks for compute-only and end-to-end
+    # scaling): the same K frames, rendered on the same streams, without the
+    # RGB24 pack, the gather or the reassembly
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    c0 = time.perf_counter()
+    for i in range(args.steps):
+        with torch.cuda.stream(sf._render_stream(i)):
+            sf.render_local(sf.local_view(i), scene=scene_defer)
+    sf._join()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed_compute = time.perf_counter() - c0
+    ctx.steps_flush(torch.zeros(1, dtype=torch.int64, device=dev))  # discard this pass's steps
     if sf.S > 1:
         iso = [(HipEvent(), HipEvent()) for _ in range(20)]
         for a, b in iso:
@@ -190,12 +206,12 @@ def main():
     if steps_done != steps_diag * args.steps:
         raise SystemExit(f"step counter mismatch: {steps_done} vs {steps_diag} x {args.steps}")
     rdev = dev if args.dist_backend == "nccl" else "cpu"
-    stats = torch.tensor([elapsed, kernel_ms_avg], dtype=torch.float64, device=rdev)
+    stats = torch.tensor([elapsed, kernel_ms_avg, elapsed_compute], dtype=torch.float64, device=rdev)
     tot = torch.tensor([steps_done, rows_mine * W * args.steps, evals_per_launch], dtype=torch.int64, device=rdev)
     if world > 1:
         dist.all_reduce(stats, op=dist.ReduceOp.MAX)
         dist.all_reduce(tot, op=dist.ReduceOp.SUM)
-    elapsed_max, kernel_ms_max = float(stats[0]), float(stats[1])
+    elapsed_max, kernel_ms_max, compute_max = float(stats[0]), float(stats[1]), float(stats[2])
     total_steps, total_pixels, evals_all = (int(x) for x in tot.tolist())
 
     if args.check_frame and rank == 0:
@@ -257,6 +273,9 @@ def main():
                       "events": ("hipEventDisableSystemFence pairs on every %d-th timed frame" % args.event_every
                                  if sf.S == 1 else "hipEventDisableSystemFence pairs on 20 isolated launches after "
                                  "the timed region (%d render streams overlap launches inside it)" % sf.S)},
+        "compute_only": {"value": total_steps / compute_max, "ms_per_step": compute_max / args.steps * 1e3,
+                         "what": "the same K frames rendered on the same streams without pack, gather or "
+                                 "reassembly (max over ranks)"},
         "spinup_frames": spin,
         "roofline": {
             "bound": "valu",

@@ -33,7 +33,9 @@ namespace {
 #endif
 constexpr int kRaysBlock = GEO_RAYS_BLOCK;
 #ifndef GEO_RAYS_TILED
-#define GEO_RAYS_TILED 1  // node-value layout: 1 = 64-connector tiles (+4.5 %), 0 = node-major SoA (tools/gpu_ab.sh)
+// node-value layout (tools/gpu_ab.sh): 2 = 64-connector tiles of node quads (16-B loads and stores),
+// 1 = 64-connector tiles of single nodes (+4.5 % over 0), 0 = node-major SoA
+#define GEO_RAYS_TILED 2
 #endif
 constexpr int kOrbitBlock = 64;  // f64 orbit lanes: few points, long serial chains
 
@@ -103,6 +105,21 @@ __device__ __forceinline__ void st_(float* p, float v) {
     *p = v;
 #endif
 }
+typedef float f4_ __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ f4_ ld4_(const float* p) {
+#if GEO_RAYS_NT
+    return __builtin_nontemporal_load(reinterpret_cast<const f4_*>(p));
+#else
+    return *reinterpret_cast<const f4_*>(p);
+#endif
+}
+__device__ __forceinline__ void st4_(float* p, f4_ v) {
+#if GEO_RAYS_NT
+    __builtin_nontemporal_store(v, reinterpret_cast<f4_*>(p));
+#else
+    *reinterpret_cast<f4_*>(p) = v;
+#endif
+}
 
 // RESPAWN = false: one RayConnector call per connector (update_ray / reset_ray).
 // RESPAWN = true: the respawn pre-pass of PointCloud::update with orbits
@@ -118,14 +135,6 @@ __global__ __launch_bounds__(kRaysBlock) void geo_rays_kernel(const RaysArgs a) 
     const uint32_t p = c >= a.n_points ? c - a.n_points : c;
     const uint32_t n = a.n_points;
     if (RESPAWN && !a.respawn[p]) return;
-#if GEO_RAYS_TILED
-    // node values in 64-connector tiles: a wave's 48 loads cover one contiguous 12-KB block
-    float* const ug = a.u + (size_t)(c / 64u) * (geo::kRayNodes * 64u) + (c % 64u);
-    const size_t stride = 64;
-#else
-    float* const ug = a.u + c;
-    const size_t stride = a.n_conn;
-#endif
     float u[geo::kRayNodes];
     bool needs = a.needs_reset[c] != 0;
     float ox = a.ox, oy = a.oy, oz = a.oz;
@@ -136,10 +145,43 @@ __global__ __launch_bounds__(kRaysBlock) void geo_rays_kernel(const RaysArgs a) 
     }
     const float* src = RESPAWN ? a.respawn_pos : a.pos;
     const float px = src[p], py = src[n + p], pz = src[2 * n + p];
-    const float angle = geo::ray_connect(a.rs, !far, px, py, pz, ox, oy, oz, RESPAWN || a.reset != 0,
-                                         a.iterations, &needs, [=](int i) { return ld_(ug + (size_t)i * stride); }, u);
+    const bool reset = RESPAWN || a.reset != 0;
+#if GEO_RAYS_TILED == 2
+    // node quads in 64-connector tiles, u[(c/64)*48*64 + (i/4)*256 + (c%64)*4 + i%4]: a lane moves
+    // its 48 nodes with 12 16-B loads and stores, a wave's quad q is one contiguous 1-KB block.
+    // Without a reset pending, ray_connect reads every node (the jump test reads node 0 first),
+    // so they are loaded up front; with one, none is read.
+    float* const ug = a.u + (size_t)(c / 64u) * (geo::kRayNodes * 64u) + (c % 64u) * 4u;
+    float v[geo::kRayNodes];
+    if (!reset && !needs) {
+#pragma unroll
+        for (int q = 0; q < geo::kRayNodes / 4; ++q) {
+            const f4_ t = ld4_(ug + q * 256);
+            v[4 * q] = t.x;
+            v[4 * q + 1] = t.y;
+            v[4 * q + 2] = t.z;
+            v[4 * q + 3] = t.w;
+        }
+    }
+    const float angle = geo::ray_connect(a.rs, !far, px, py, pz, ox, oy, oz, reset, a.iterations, &needs,
+                                         [&](int i) { return v[i]; }, u);
+#pragma unroll
+    for (int q = 0; q < geo::kRayNodes / 4; ++q)
+        st4_(ug + q * 256, f4_{u[4 * q], u[4 * q + 1], u[4 * q + 2], u[4 * q + 3]});
+#else
+#if GEO_RAYS_TILED == 1
+    // node values in 64-connector tiles: a wave's 48 loads cover one contiguous 12-KB block
+    float* const ug = a.u + (size_t)(c / 64u) * (geo::kRayNodes * 64u) + (c % 64u);
+    const size_t stride = 64;
+#else
+    float* const ug = a.u + c;
+    const size_t stride = a.n_conn;
+#endif
+    const float angle = geo::ray_connect(a.rs, !far, px, py, pz, ox, oy, oz, reset, a.iterations, &needs,
+                                         [=](int i) { return ld_(ug + (size_t)i * stride); }, u);
 #pragma unroll
     for (int i = 0; i < geo::kRayNodes; ++i) st_(ug + (size_t)i * stride, u[i]);
+#endif
     a.needs_reset[c] = needs ? 1 : 0;
     if (!RESPAWN && a.out) a.out[c] = make_float4(px, py, pz, angle);
 }

@@ -127,7 +127,14 @@ __device__ __forceinline__ void st4_(float* p, f4_ v) {
 // reset_ray at the new position; the regular pass follows.  Two launches keep
 // one solve per lane (VGPR budget: 48 nodes + 46 + 46 Thomas values).
 template <bool RESPAWN>
+#ifndef GEO_RAYS_MINW
+#define GEO_RAYS_MINW 0  // > 0: __launch_bounds__ min waves per SIMD (VGPR cap; A/B switch)
+#endif
+#if GEO_RAYS_MINW > 0
+__global__ __launch_bounds__(kRaysBlock, GEO_RAYS_MINW) void geo_rays_kernel(const RaysArgs a) {
+#else
 __global__ __launch_bounds__(kRaysBlock) void geo_rays_kernel(const RaysArgs a) {
+#endif
     const uint32_t c = blockIdx.x * kRaysBlock + threadIdx.x;
     if (c >= a.n_conn) return;
     // connector c: point c mod n, near side (less_than_180) first

@@ -127,6 +127,9 @@ __device__ __forceinline__ void st4_(float* p, f4_ v) {
 // reset_ray at the new position; the regular pass follows.  Two launches keep
 // one solve per lane (VGPR budget: 48 nodes + 46 + 46 Thomas values).
 template <bool RESPAWN>
+#ifndef GEO_RAYS_NOCOMPUTE
+#define GEO_RAYS_NOCOMPUTE 0
+#endif
 #ifndef GEO_RAYS_MINW
 #define GEO_RAYS_MINW 0  // > 0: __launch_bounds__ min waves per SIMD (VGPR cap; A/B switch)
 #endif
@@ -160,7 +163,7 @@ __global__ __launch_bounds__(kRaysBlock) void geo_rays_kernel(const RaysArgs a) 
     // so they are loaded up front; with one, none is read.
     float* const ug = a.u + (size_t)(c / 64u) * (geo::kRayNodes * 64u) + (c % 64u) * 4u;
     float v[geo::kRayNodes];
-    if (!reset && !needs) {
+    if (GEO_RAYS_NOCOMPUTE || (!reset && !needs)) {
 #pragma unroll
         for (int q = 0; q < geo::kRayNodes / 4; ++q) {
             const f4_ t = ld4_(ug + q * 256);
@@ -170,8 +173,14 @@ __global__ __launch_bounds__(kRaysBlock) void geo_rays_kernel(const RaysArgs a) 
             v[4 * q + 3] = t.w;
         }
     }
+#if GEO_RAYS_NOCOMPUTE  // diagnostic only: the memory traffic without the solve (outputs are wrong)
+    float angle = px + py + pz + ox + oy + oz;
+#pragma unroll
+    for (int i = 0; i < geo::kRayNodes; ++i) u[i] = v[i] + angle;
+#else
     const float angle = geo::ray_connect(a.rs, !far, px, py, pz, ox, oy, oz, reset, a.iterations, &needs,
                                          [&](int i) { return v[i]; }, u);
+#endif
 #pragma unroll
     for (int q = 0; q < geo::kRayNodes / 4; ++q)
         st4_(ug + q * 256, f4_{u[4 * q], u[4 * q + 1], u[4 * q + 2], u[4 * q + 3]});

@@ -17,6 +17,7 @@
 // live in VGPRs for the whole call (no LDS, no scratch).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstring>
 #include <new>
 #include <vector>
@@ -202,6 +203,84 @@ __global__ __launch_bounds__(kRaysBlock) void geo_rays_kernel(const RaysArgs a) 
     if (!RESPAWN && a.out) a.out[c] = make_float4(px, py, pz, angle);
 }
 
+#ifndef GEO_RAYS_PREFETCH
+#define GEO_RAYS_PREFETCH 0  // 1: geo_rays_pf_kernel for the regular pass (A/B switch)
+#endif
+#ifndef GEO_RAYS_PF_BLOCKS_PER_CU
+#define GEO_RAYS_PF_BLOCKS_PER_CU 12  // resident 1-wave blocks per CU (160 VGPRs: 3 waves/SIMD)
+#endif
+// The regular pass with the next tile's state in flight during the solve: a
+// grid of resident 1-wave blocks walks the 64-connector tiles; each tile's 48
+// node quads (12 KB) arrive in LDS by LDS-DMA (global_load_lds_dwordx4, one
+// 1-KB quad per wave instruction, lane-linear = the tile's own layout) issued
+// before the previous tile's solve.  Small per-connector inputs use ordinary
+// loads, waited before the DMA is issued (hipcc would otherwise drain the DMA
+// at their first use).
+__global__ __launch_bounds__(64) void geo_rays_pf_kernel(const RaysArgs a, uint32_t n_tiles) {
+    __shared__ __attribute__((aligned(16))) float s_u[geo::kRayNodes * 64];
+    const uint32_t lane = threadIdx.x;
+    const uint32_t n = a.n_points;
+    auto prefetch = [&](uint32_t tile) {
+        const float* src = a.u + (size_t)tile * (geo::kRayNodes * 64u) + lane * 4u;
+#pragma unroll
+        for (int q = 0; q < geo::kRayNodes / 4; ++q)
+            __builtin_amdgcn_global_load_lds(src + q * 256, (__attribute__((address_space(3))) void*)(s_u + q * 256),
+                                             16, 0, GEO_RAYS_NT ? 2 : 0);
+    };
+    uint32_t t = blockIdx.x;
+    if (t < n_tiles) prefetch(t);
+    for (; t < n_tiles; t += gridDim.x) {
+        const uint32_t c = t * 64u + lane;
+        const bool live = c < a.n_conn;
+        const uint32_t cc = live ? c : 0u;
+        const bool far = a.sides == GEO_RAYS_FAR ? true : cc >= n;
+        const uint32_t p = cc >= n ? cc - n : cc;
+        bool needs = a.needs_reset[cc] != 0;
+        float ox = a.ox, oy = a.oy, oz = a.oz;
+        if (a.other) {
+            ox = a.other[3 * (size_t)p];
+            oy = a.other[3 * (size_t)p + 1];
+            oz = a.other[3 * (size_t)p + 2];
+        }
+        float px = a.pos[p], py = a.pos[n + p], pz = a.pos[2 * n + p];
+        GEO_OPAQUE(px);
+        GEO_OPAQUE(py);
+        GEO_OPAQUE(pz);
+        GEO_OPAQUE(ox);
+        GEO_OPAQUE(oy);
+        GEO_OPAQUE(oz);
+        uint32_t nb = needs ? 1u : 0u;
+        GEO_OPAQUE(nb);
+        needs = nb != 0;
+        // this tile's DMA (issued one tile ago) and the previous stores
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const bool reset = a.reset != 0;
+        float v[geo::kRayNodes];
+        if (!reset && !needs) {  // as geo_rays_kernel: no node is read when a reset is pending
+#pragma unroll
+            for (int q = 0; q < geo::kRayNodes / 4; ++q) {
+                const float4 w = *reinterpret_cast<const float4*>(s_u + q * 256 + lane * 4);
+                v[4 * q] = w.x;
+                v[4 * q + 1] = w.y;
+                v[4 * q + 2] = w.z;
+                v[4 * q + 3] = w.w;
+            }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // LDS read before the DMA rewrites it
+        if (t + gridDim.x < n_tiles) prefetch(t + gridDim.x);
+        if (!live) continue;
+        float u[geo::kRayNodes];
+        const float angle = geo::ray_connect(a.rs, !far, px, py, pz, ox, oy, oz, reset, a.iterations, &needs,
+                                             [&](int i) { return v[i]; }, u);
+        float* const ug = a.u + (size_t)t * (geo::kRayNodes * 64u) + lane * 4u;
+#pragma unroll
+        for (int q = 0; q < geo::kRayNodes / 4; ++q)
+            st4_(ug + q * 256, f4_{u[4 * q], u[4 * q + 1], u[4 * q + 2], u[4 * q + 3]});
+        a.needs_reset[c] = needs ? 1 : 0;
+        if (a.out) a.out[c] = make_float4(px, py, pz, angle);
+    }
+}
+
 // PointCloud::update, orbit half (point_cloud.rs:119-141): step, then respawn
 // a particle that hit the singularity or fell inside rs.  The connectors get
 // the PRE-respawn position for this frame's update_ray (the reference sets
@@ -341,7 +420,17 @@ int rays_launch(geo_rays* r, float ox, float oy, float oz, const float* other_de
         hipLaunchKernelGGL(geo_rays_kernel<true>, grid, dim3(kRaysBlock), 0, s, a);
         if (hipGetLastError() != hipSuccess) return GEO_EHIP;
     }
+#if GEO_RAYS_PREFETCH && GEO_RAYS_TILED == 2
+    {
+        const uint32_t n_tiles = (r->n_conn + 63u) / 64u;
+        int cus = 256;
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, r->device);
+        const uint32_t blocks = std::min<uint32_t>(n_tiles, (uint32_t)cus * GEO_RAYS_PF_BLOCKS_PER_CU);
+        hipLaunchKernelGGL(geo_rays_pf_kernel, dim3(blocks), dim3(64), 0, s, a, n_tiles);
+    }
+#else
     hipLaunchKernelGGL(geo_rays_kernel<false>, grid, dim3(kRaysBlock), 0, s, a);
+#endif
     return hipGetLastError() == hipSuccess ? GEO_OK : GEO_EHIP;
 }
 

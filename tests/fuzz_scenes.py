@@ -1,0 +1,59 @@
+"""Seeded random scenes for the fuzz parity tests (tests/test_host_fuzz.py on
+the CPU, tests/test_gpu_fuzz.py on the GPU): observer inside/outside the
+photon sphere, the horizon and the sky sphere, small spheres on both sides of
+the photon sphere, flat space, random cameras, fields of view, energies,
+motion states, step budgets and (adaptive) tolerances."""
+import math
+
+import numpy as np
+
+from schwarzschild_raytracer_wgpu_amd import Observer, make_scene
+from schwarzschild_raytracer_wgpu_amd._lib import GEO_MODE_ADAPTIVE, GEO_MODE_DIRECT
+
+KINDS = ("sky", "near_ring", "inside_photon_sphere", "inside_horizon", "flat", "outside_sphere", "small_sphere")
+
+
+def random_scene(seed: int, w: int, h: int, adaptive: bool = False):
+    """(frame, scene, description) for seed."""
+    rng = np.random.default_rng(seed)
+    kind = KINDS[seed % len(KINDS)]
+    rs, sphere_r = 1.0, 50.0
+    if kind == "sky":
+        r = rng.uniform(1.6, 40.0)
+    elif kind == "near_ring":
+        r = rng.uniform(1.45, 1.6)
+    elif kind == "inside_photon_sphere":
+        r = rng.uniform(1.01, 1.5)
+    elif kind == "inside_horizon":
+        r = rng.uniform(0.3, 0.99)
+    elif kind == "flat":
+        rs, r = 0.0, rng.uniform(0.5, 40.0)
+    elif kind == "outside_sphere":
+        r = rng.uniform(52.0, 300.0)
+    else:  # small_sphere: the sky sphere itself on either side of the photon sphere
+        sphere_r = rng.uniform(1.05, 3.0)
+        r = rng.uniform(1.01, sphere_r * 0.99) if rng.random() < 0.7 else rng.uniform(sphere_r * 1.05, 10.0)
+    d = rng.normal(size=3)
+    d /= np.linalg.norm(d)
+    pos = tuple(float(x) for x in r * d)
+    fov = float(rng.uniform(0.6, 2.4))
+    o = Observer(rs, fov, w, h)
+    o.set_position(*pos)
+    o.set_camera(float(rng.uniform(0.0, 2.0 * math.pi)), float(rng.uniform(-1.3, 1.3)))
+    o.set_energy(float(rng.uniform(1.0, 1.6)))
+    unmoving = kind != "inside_horizon" and rng.random() < 0.3
+    if unmoving:
+        o.start_unmoving()
+    else:
+        o.start_frozen_fall()
+    frame = o.calc_transformation_pipeline()
+    max_steps = int(rng.choice([1, 3, 17, 300, 2048, 2048, 2048, 4096]))
+    step = math.pi / 100 if rng.random() < 0.7 else float(rng.uniform(0.005, 0.1))
+    if adaptive:
+        tol = float(10.0 ** rng.uniform(-7.5, -4.0)) if rng.random() < 0.8 else 0.0
+        scene = make_scene(rs, sphere_r, o.get_radial_position(), step, max_steps, GEO_MODE_ADAPTIVE, tol=tol)
+    else:
+        scene = make_scene(rs, sphere_r, o.get_radial_position(), step, max_steps, GEO_MODE_DIRECT)
+    desc = (f"seed={seed} kind={kind} r={r:.4f} sphere_r={sphere_r:.3f} rs={rs} fov={fov:.3f} "
+            f"unmoving={unmoving} steps={max_steps} step={step:.4f} adaptive={adaptive}")
+    return frame, scene, desc

@@ -1,0 +1,28 @@
+"""Fuzz parity on the CPU: the kernel's per-pixel header (geo_pixel.h, host
+build) equals the oracle's f32 restatement bit for bit on seeded random
+scenes (tests/fuzz_scenes.py), direct and adaptive.  The GPU twin is
+tests/test_gpu_fuzz.py."""
+import numpy as np
+import pytest
+
+import oracle as O
+from fuzz_scenes import random_scene
+from schwarzschild_raytracer_wgpu_amd.scenes import make_sky
+from test_host_kernel_math import host, run_host  # noqa: F401  (fixture)
+
+W, H = 48, 27
+
+
+@pytest.mark.parametrize("adaptive", [False, True], ids=["direct", "adaptive"])
+def test_host_header_fuzz(host, adaptive):  # noqa: F811
+    sky = make_sky("equirect", (128, 64))
+    bad = []
+    for seed in range(400 if not adaptive else 200):
+        frame, scene, desc = random_scene(seed, W, H, adaptive=adaptive)
+        a = run_host(host, frame, scene, sky, W, H, variant=4)
+        b = O.render_f32(frame, scene, sky, W, H, threads=4)
+        same = all(np.array_equal(a[f], b[f]) for f in ("mask", "steps", "rgba")) and np.array_equal(
+            a["uv"].view(np.uint32), b["uv"].view(np.uint32))
+        if not same:
+            bad.append(desc)
+    assert not bad, bad[:5]

@@ -1,0 +1,107 @@
+#!/usr/bin/env python3
+"""The reference's whole frame on one GPU (SR/lib.rs:62-94, renderer.rs:208-264):
+sky sphere (r 50), planet sphere (r 1.1), translucent cloud sphere (r 1.2),
+each a per-pixel geodesic draw composited in order, then the accretion disk
+(PointCloud::update with f64 orbits and both RayConnector sides, then the
+near and far point draws).  One JSON line: ms per frame (wall, K frames back
+to back on one stream), frames/s, and each part's GPU time from event pairs.
+
+  python tools/bench_scene.py [--width 3840 --height 2160] [--frames 200] [--points 5000]
+
+Textures are synthetic (the reference's are absent): the benchmark equirect
+sky, a 2048x1024 checkerboard planet and a seeded random-alpha cloud layer.
+Units: rs = 1 (the reference's rs = 10 scene divided by 10), observer
+FrozenFall from (2.5, 0, 0.1), moving with the reference's controls idle.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--width", type=int, default=3840)
+    p.add_argument("--height", type=int, default=2160)
+    p.add_argument("--frames", type=int, default=200)
+    p.add_argument("--warmup", type=int, default=100)
+    p.add_argument("--points", type=int, default=5000)
+    p.add_argument("--max-steps", type=int, default=1000, help="per sphere (basic_sphere_buffer.rs:42-51)")
+    args = p.parse_args()
+
+    import numpy as np
+    import torch
+
+    import schwarzschild_raytracer_wgpu_amd as g
+    from schwarzschild_raytracer_wgpu_amd.scenes import make_sky
+    from schwarzschild_raytracer_wgpu_amd.timing import HipEvent
+
+    w, h = args.width, args.height
+    obs = g.Observer(1.0, math.pi / 2, w, h)
+    obs.set_position(2.5, 0.0, 0.1)
+    sky = make_sky("equirect", (4096, 2048))
+    planet = make_sky("equirect", (2048, 1024), seed=7)
+    clouds = np.random.default_rng(11).integers(0, 256, size=(1024, 2048, 4), dtype=np.uint8)
+    spheres = [g.BasicSphereBuffer(0, 50.0, 1.0, sky, max_iter=args.max_steps),
+               g.BasicSphereBuffer(0, 1.1, 1.0, planet, max_iter=args.max_steps),
+               g.BasicSphereBuffer(0, 1.2, 1.0, clouds, max_iter=args.max_steps)]
+    disk = g.PointCloud.new_accretion_disk(spheres[0].ctx, 1.0, obs.get_position(), True, n=args.points)
+    tgt = g.RenderTarget(w, h, torch.empty(w * h * 4, dtype=torch.uint8, device="cuda:0"))
+
+    parts = ("disk update", "sky", "planet", "clouds", "points")
+
+    def frame(evs=None):
+        obs.update_position((0.0, 0.0, 0.0), 1 / 60)
+        r = obs.get_radial_position()
+        for s in spheres:
+            s.update_ray_fan(r)  # records r (direct mode integrates per pixel)
+        f = obs.calc_transformation_pipeline()
+        if evs:
+            evs[0].record()
+        disk.update(obs.get_position(), 1 / 60)
+        if evs:
+            evs[1].record()
+        for i, s in enumerate(spheres):
+            s.draw(f, tgt, composite=i > 0)
+            if evs:
+                evs[2 + i].record()
+        disk.draw(f, tgt)
+        if evs:
+            evs[5].record()
+
+    for _ in range(args.warmup):
+        frame()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.frames):
+        frame()
+    torch.cuda.synchronize()
+    wall = (time.perf_counter() - t0) / args.frames
+    # per-part GPU time on separate frames with event pairs
+    acc = np.zeros(len(parts))
+    nev = 20
+    for _ in range(nev):
+        evs = [HipEvent() for _ in range(6)]
+        frame(evs)
+        torch.cuda.synchronize()
+        acc += [evs[i].elapsed_time(evs[i + 1]) for i in range(5)]
+    acc /= nev
+    print(json.dumps({
+        "what": "the reference's frame: 3 composited per-pixel geodesic spheres + accretion disk "
+                "(orbits, 2 x RayConnector, point draws)",
+        "width": w, "height": h, "frames": args.frames, "points": args.points, "max_steps": args.max_steps,
+        "ms_per_frame": wall * 1e3, "frames_per_s": 1.0 / wall,
+        "gpu_ms": {k: float(v) for k, v in zip(parts, acc)},
+        "data": "synthetic textures (sky 4096x2048, planet 2048x1024, random-alpha clouds 2048x1024)",
+    }), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -4,11 +4,14 @@
 over N GPUs with an RCCL gather to rank 0).
 
 One "step" = one frame: every rank renders its interleaved row bands of the
-4K frame with the HIP kernel (geo_render_bands), then (N > 1) rank 0 gathers
-the bands over RCCL and reassembles the frame for present (geo_assemble_bands).
-Gathers run on RCCL's stream in batches of --frames-per-gather frames,
-double-buffered, so a batch's gather overlaps the next batch's compute.  value = executed RK4 main-loop steps of all ranks / max-over-ranks
-wall time of the K timed frames (inputs resident in HBM, sky uploaded once).
+4K frame with the HIP kernel (geo_render_band_set), then (N > 1) rank 0
+gathers the peers' bands over RCCL and reassembles the frame for present
+(geo_assemble_lead).  Gathers run on RCCL's stream in batches of
+--frames-per-gather frames, double-buffered, so a batch's gather overlaps the
+next batch's compute.  Rank 0's share (--rank0-lead) is picked by measuring
+the whole pipeline before the timed region.  value = executed RK4 main-loop
+steps of all ranks / max-over-ranks wall time of the K timed frames (inputs
+resident in HBM, sky uploaded once).
 
   python bench.py [--gpus N] [--steps K] [--warmup W]
   torchrun --nproc-per-node N bench.py --gpus N ...
@@ -52,7 +55,13 @@ def parse():
                         "the tail of a rank's small share)")
     p.add_argument("--frames-per-gather", type=int, default=4,
                    help="N > 1: frames per RCCL gather to rank 0 (amortises the ~34 us host cost of a gather; "
-                        "rank 0 reassembles each batch with one geo_assemble_bands launch)")
+                        "rank 0 reassembles each batch with one geo_assemble_lead launch)")
+    p.add_argument("--rank0-lead", default="auto", choices=["auto", "1", "2", "4"],
+                   help="N > 1: rank 0's band height in 8-row bands per cycle (it renders rows that never cross "
+                        "an xGMI link, so a link-bound present wants it larger); auto = the fastest of 1, 2, 4 "
+                        "measured on the whole pipeline before the timed region")
+    p.add_argument("--lead-trial-frames", type=int, default=120,
+                   help="frames per --rank0-lead auto trial (after a quarter as many warm-up frames)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-threads", type=int, default=16)
     p.add_argument("--cpu-row-step", type=int, default=None,
@@ -109,18 +118,71 @@ def main():
         ctx.solve_ray_fan(cfg.sphere_r, cfg.rs, cfg.max_steps, cfg.step, 400, obs.get_radial_position())
 
     # interleaved 8-row bands: rank g owns bands g, g+N, ... (balances the centre-heavy frame:
-    # 270 bands of the 4K frame -> 34 vs 33.75 per rank at N=8); gather to rank 0 over RCCL
+    # 270 bands of the 4K frame -> 34 vs 33.75 per rank at N=8); gather to rank 0 over RCCL.
+    # With lead > 1 rank 0 owns lead-times-taller bands (it renders rows that never cross a link).
     from schwarzschild_raytracer_wgpu_amd.dist import ShardedFrame
 
-    sf = ShardedFrame(ctx, frame, scene, W, H, args.band_rows, rank, world, dev, dist if world > 1 else None,
-                      host_gather=args.dist_backend == "gloo", frames_per_gather=args.frames_per_gather,
-                      render_streams=args.render_streams or (1 if world == 1 else 2))
-    L = sf.layout
+    rdev = dev if args.dist_backend == "nccl" else "cpu"
+
+    def make_sf(lead):
+        return ShardedFrame(ctx, frame, scene, W, H, args.band_rows, rank, world, dev, dist if world > 1 else None,
+                            host_gather=args.dist_backend == "gloo", frames_per_gather=args.frames_per_gather,
+                            render_streams=args.render_streams or (1 if world == 1 else 2), lead=lead)
+
+    if world == 1:
+        leads = [1]
+    elif args.rank0_lead == "auto":
+        leads = [1, 2, 4]
+    else:
+        leads = [int(args.rank0_lead)]
+    sf = make_sf(leads[0])
     steps_ctr = torch.zeros(1, dtype=torch.int64, device=dev)
+
+    # GPU clock spin-up (untimed, not counted as warmup): from idle the first
+    # frames run up to 5x slower while the clock ramps (tools/ubench/gap_probe2.py)
+    spin = args.spinup_frames * world
+    for i in range(spin):
+        sf.step(i)
+        if i % 50 == 49:
+            sf.drain()
+            torch.cuda.synchronize()
+    sf.drain()
+    torch.cuda.synchronize()
+
+    # rank 0's share (--rank0-lead auto): every layout runs the whole pipeline
+    # (render, pack, gather, reassembly) for the same frames, untimed for the
+    # metric; the fastest by max-over-ranks wall time is used for the timed
+    # region.  Every rank holds the same all-reduced times, so all pick alike.
+    lead_trials = None
+    if len(leads) > 1:
+        times = []
+        for ld in leads:
+            t_sf = sf if ld == sf.layout.lead else make_sf(ld)
+            for i in range(args.lead_trial_frames // 4):
+                t_sf.step(i)
+            t_sf.drain()
+            torch.cuda.synchronize()
+            dist.barrier()
+            t0 = time.perf_counter()
+            for i in range(args.lead_trial_frames):
+                t_sf.step(i)
+            t_sf.drain()
+            torch.cuda.synchronize()
+            dist.barrier()
+            times.append(time.perf_counter() - t0)
+            if t_sf is not sf:
+                del t_sf
+        tt = torch.tensor(times, dtype=torch.float64, device=rdev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        best = leads[int(torch.argmin(tt).item())]
+        lead_trials = {str(ld): float(tt[j]) / args.lead_trial_frames * 1e3 for j, ld in enumerate(leads)}
+        if best != sf.layout.lead:
+            sf = make_sf(best)
+    L = sf.layout
 
     # untimed diagnostic pass: per-pixel steps + mask give the RK4 evaluations
     # per launch (main-loop steps + 3 Newton evaluations per sphere crossing)
-    n_loc = L.nb_max * L.band_rows * W
+    n_loc = max(1, L.packed_rows()) * W
     diag_mask = torch.zeros(n_loc, dtype=torch.uint8, device=dev)
     diag_steps = torch.zeros(n_loc, dtype=torch.int32, device=dev)
     diag_ctr = torch.zeros(1, dtype=torch.int64, device=dev)
@@ -136,16 +198,8 @@ def main():
     else:
         flops_per_launch = FLOPS_PER_EVAL * evals_per_launch
 
-    # GPU clock spin-up (untimed, not counted as warmup): from idle the first
-    # frames run up to 5x slower while the clock ramps (tools/ubench/gap_probe2.py)
-    spin = args.spinup_frames * world
-    for i in range(spin):
-        sf.step(i)
-        if i % 50 == 49:
-            sf.drain()
-            torch.cuda.synchronize()
     for i in range(args.warmup):
-        sf.step(spin + i)
+        sf.step(i)
     sf.drain()
     torch.cuda.synchronize()
 
@@ -205,7 +259,6 @@ def main():
     steps_done = int(steps_ctr.item())
     if steps_done != steps_diag * args.steps:
         raise SystemExit(f"step counter mismatch: {steps_done} vs {steps_diag} x {args.steps}")
-    rdev = dev if args.dist_backend == "nccl" else "cpu"
     stats = torch.tensor([elapsed, kernel_ms_avg, elapsed_compute], dtype=torch.float64, device=rdev)
     tot = torch.tensor([steps_done, rows_mine * W * args.steps, evals_per_launch], dtype=torch.int64, device=rdev)
     if world > 1:
@@ -261,6 +314,8 @@ def main():
             "parallelism": f"rowbands{world}" if world > 1 else "single",
             "band_rows": args.band_rows,
             "frames_per_gather": sf.K,
+            "rank0_lead": L.lead,
+            "lead_trials_ms_per_frame": lead_trials,
             "render_streams": sf.S,
         },
         "per_gpu": value / world,

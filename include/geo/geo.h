@@ -178,6 +178,37 @@ int geo_assemble_bands(geo_ctx* ctx, const uint8_t* src, size_t rank_stride, siz
                        uint32_t band_rows, uint32_t width, uint32_t height, uint32_t nframes, uint32_t src_bpp,
                        uint8_t* dst, void* stream);
 
+/* The general strided band set: bands starting at rows row0, row0+row_stride,
+ * ..., nbands of them, each band_rows tall (a power of two >= 8) and clipped
+ * to height; row_stride >= band_rows.  Outputs packed band after band as in
+ * geo_render_bands (which is the case row0 = band0*band_rows,
+ * row_stride = band_step*band_rows).  Used for the lead layout below, where
+ * rank 0 renders taller bands than its peers. */
+int geo_render_band_set(geo_ctx* ctx, const geo_frame* frame, const geo_scene* scene,
+                        uint32_t width, uint32_t height, uint32_t band_rows, uint32_t row0,
+                        uint32_t row_stride, uint32_t nbands, uint8_t* out_rgba8, uint8_t* out_mask,
+                        float* out_uv, uint32_t* out_steps, unsigned long long* steps_total,
+                        void* stream);
+
+/* Rank 0's reassembly for the LEAD layout (multi-GPU present with rank 0
+ * taking a larger share: it renders but never sends its rows, while the peers'
+ * rows cross the xGMI links).  The frame is cut into cycles of
+ * (lead + world - 1) * band_rows rows: the first lead*band_rows rows of each
+ * cycle are rank 0's (one band of that height), then one band_rows band per
+ * peer r = 1..world-1 in order.  lead = 1 is geo_assemble_bands' layout.
+ *   lead_src  rank 0's packed RGBA8 bands (geo_render_band_set output), nframes
+ *             frames lead_frame_stride bytes apart
+ *   src       the gathered peer blocks: rank r's packed bands at
+ *             src + r*rank_stride + f*frame_stride, src_bpp bytes per pixel
+ *             (4 or 3 = RGB24 from geo_pack_rgb); block 0 is not read
+ * Writes nframes RGBA8 frames back to back to dst.  width % 4 == 0 and
+ * 16-byte aligned device buffers (4-byte for src with src_bpp 3).
+ * Asynchronous on `stream`. */
+int geo_assemble_lead(geo_ctx* ctx, const uint8_t* lead_src, size_t lead_frame_stride, uint32_t lead,
+                      const uint8_t* src, size_t rank_stride, size_t frame_stride, uint32_t world,
+                      uint32_t band_rows, uint32_t width, uint32_t height, uint32_t nframes, uint32_t src_bpp,
+                      uint8_t* dst, void* stream);
+
 /* RGBA8 -> RGB24 (the alpha byte dropped: frames are opaque after the clear,
  * renderer.rs:233-238) of npixels (a multiple of 4) device pixels: 25 % fewer
  * bytes on the links for the multi-GPU present.  Asynchronous on `stream`. */

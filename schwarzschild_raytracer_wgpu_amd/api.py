@@ -155,6 +155,15 @@ class Context:
                                                            band_rows, width, height, nframes, src_bpp, _ptr(dst),
                                                            _stream_handle(stream)))
 
+    def assemble_lead(self, lead_src, lead_frame_stride: int, lead: int, src, rank_stride: int, frame_stride: int,
+                      world: int, band_rows: int, width: int, height: int, nframes: int, dst, src_bpp: int = 4,
+                      stream=None) -> None:
+        """geo_assemble_lead: rank 0's own packed RGBA8 bands (lead*band_rows rows per cycle) plus the gathered
+        peer blocks (RGBA8 or RGB24; block 0 unread) -> nframes RGBA8 frames (device)."""
+        check("geo_assemble_lead", lib.geo_assemble_lead(
+            self._h, _ptr(lead_src), lead_frame_stride, lead, _ptr(src), rank_stride, frame_stride, world, band_rows,
+            width, height, nframes, src_bpp, _ptr(dst), _stream_handle(stream)))
+
     def pack_rgb(self, rgba, npixels: int, rgb, stream=None) -> None:
         """geo_pack_rgb: RGBA8 -> RGB24 on the device (npixels % 4 == 0)."""
         check("geo_pack_rgb", lib.geo_pack_rgb(self._h, _ptr(rgba), npixels, _ptr(rgb), _stream_handle(stream)))
@@ -183,6 +192,20 @@ class Context:
                 raise ValueError("outputs must be contiguous device tensors of sufficient size")
         check("geo_render_bands", lib.geo_render_bands(
             self._h, ctypes.byref(frame), ctypes.byref(scene), width, height, band_rows, band0, band_step, nbands,
+            _ptr(out_rgba), _ptr(out_mask), _ptr(out_uv), _ptr(out_steps), _ptr(steps_total),
+            _stream_handle(stream)))
+
+    def render_band_set(self, frame: GeoFrame, scene: GeoScene, width: int, height: int, band_rows: int, row0: int,
+                        row_stride: int, nbands: int, out_rgba, out_mask=None, out_uv=None, out_steps=None,
+                        steps_total=None, stream=None) -> None:
+        """geo_render_band_set: bands at rows row0 + j*row_stride (j < nbands), band_rows tall, packed."""
+        nrows = nbands * band_rows
+        for t, n in ((out_rgba, nrows * width * 4), (out_mask, nrows * width), (out_uv, nrows * width * 2),
+                     (out_steps, nrows * width), (steps_total, 1)):
+            if t is not None and (not t.is_cuda or not t.is_contiguous() or t.numel() < n):
+                raise ValueError("outputs must be contiguous device tensors of sufficient size")
+        check("geo_render_band_set", lib.geo_render_band_set(
+            self._h, ctypes.byref(frame), ctypes.byref(scene), width, height, band_rows, row0, row_stride, nbands,
             _ptr(out_rgba), _ptr(out_mask), _ptr(out_uv), _ptr(out_steps), _ptr(steps_total),
             _stream_handle(stream)))
 

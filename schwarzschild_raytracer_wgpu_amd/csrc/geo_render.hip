@@ -18,6 +18,7 @@
 #include <cstdio>
 #include <cstring>
 #include <new>
+#include <type_traits>
 
 #include "../../include/geo/geo.h"
 #include "geo_ctx.h"
@@ -174,6 +175,51 @@ __global__ __launch_bounds__(256) void geo_assemble_rgb_kernel(const uint8_t* __
     o.z = (w1 >> 16) | ((w2 & 0xFFu) << 16) | 0xFF000000u;
     o.w = (w2 >> 8) | 0xFF000000u;
     reinterpret_cast<uint4*>(dst + ((size_t)f * height + y) * (size_t)quads * 16u)[x] = o;
+}
+
+// The lead layout (geo_assemble_lead): cycles of lead*band_rows rows of rank 0
+// followed by one band_rows band per peer.  QUAD: one thread per 4 pixels
+// (16 B out; peers' rows RGBA8 or RGB24), else one per pixel (RGBA8 only).
+// The row's source (rank 0's own bands or a peer's) is block-uniform.
+template <bool QUAD>
+__global__ __launch_bounds__(256) void geo_assemble_lead_kernel(
+    const uint8_t* __restrict__ lead_src, size_t lead_frame_stride, uint32_t lead, const uint8_t* __restrict__ src,
+    size_t rank_stride, size_t frame_stride, uint32_t world, uint32_t band_rows, uint32_t units, uint32_t height,
+    uint32_t src_bpp, uint8_t* __restrict__ dst) {
+    using T = typename std::conditional<QUAD, uint4, uint32_t>::type;
+    constexpr uint32_t kPix = QUAD ? 4u : 1u;  // pixels per unit
+    const uint32_t x = blockIdx.x * 256u + threadIdx.x;
+    const uint32_t y = blockIdx.y;
+    const uint32_t f = blockIdx.z;
+    if (x >= units) return;
+    const uint32_t lead_rows = lead * band_rows;
+    const uint32_t cycle = lead_rows + (world - 1u) * band_rows;
+    const uint32_t c = y / cycle, off = y % cycle;
+    const size_t rgba_row = (size_t)units * sizeof(T);
+    T* d = reinterpret_cast<T*>(dst + ((size_t)f * height + y) * rgba_row);
+    if (off < lead_rows) {
+        const size_t lrow = (size_t)c * lead_rows + off;
+        d[x] = reinterpret_cast<const T*>(lead_src + f * lead_frame_stride + lrow * rgba_row)[x];
+        return;
+    }
+    const uint32_t o2 = off - lead_rows;
+    const uint32_t r = 1u + o2 / band_rows;
+    const size_t lrow = (size_t)c * band_rows + o2 % band_rows;
+    const uint8_t* row = src + r * rank_stride + f * frame_stride + lrow * (size_t)units * kPix * src_bpp;
+    if constexpr (QUAD) {
+        if (src_bpp == 3u) {
+            const uint32_t* s = reinterpret_cast<const uint32_t*>(row) + 3u * x;
+            const uint32_t w0 = s[0], w1 = s[1], w2 = s[2];  // r0 g0 b0 r1 | g1 b1 r2 g2 | b2 r3 g3 b3
+            uint4 o;
+            o.x = (w0 & 0x00FFFFFFu) | 0xFF000000u;
+            o.y = (w0 >> 24) | ((w1 & 0xFFFFu) << 8) | 0xFF000000u;
+            o.z = (w1 >> 16) | ((w2 & 0xFFu) << 16) | 0xFF000000u;
+            o.w = (w2 >> 8) | 0xFF000000u;
+            d[x] = o;
+            return;
+        }
+    }
+    d[x] = reinterpret_cast<const T*>(row)[x];
 }
 
 // RGBA8 -> RGB24 (alpha dropped: every frame pixel is opaque after the clear),
@@ -554,6 +600,48 @@ int geo_assemble_bands(geo_ctx* c, const uint8_t* src, size_t rank_stride, size_
     return hipGetLastError() == hipSuccess ? GEO_OK : GEO_EHIP;
 }
 
+int geo_assemble_lead(geo_ctx* c, const uint8_t* lead_src, size_t lead_frame_stride, uint32_t lead,
+                      const uint8_t* src, size_t rank_stride, size_t frame_stride, uint32_t world,
+                      uint32_t band_rows, uint32_t width, uint32_t height, uint32_t nframes, uint32_t src_bpp,
+                      uint8_t* dst, void* stream) {
+    if (!c || !lead_src || !dst || world == 0 || lead == 0 || band_rows == 0 || width == 0 || height == 0 ||
+        nframes == 0 || height > 65535u || nframes > 65535u || (src_bpp != 3u && src_bpp != 4u))
+        return GEO_EINVAL;
+    // 16-B units need width % 4 == 0 and aligned buffers; RGB24 peers need them
+    const size_t lead_align = width % 4u == 0 ? 16u : 4u;
+    if (src_bpp == 3u && width % 4u != 0) return GEO_EINVAL;
+    if ((uint64_t)(lead + world - 1u) * band_rows > (1u << 20)) return GEO_EINVAL;
+    const uint32_t lead_rows = lead * band_rows, cycle = lead_rows + (world - 1u) * band_rows;
+    // rank 0 has ceil(H / cycle) bands; rank 1, the first peer, the most of the peers
+    const size_t nb0 = (height + cycle - 1u) / cycle;
+    const size_t nb1 = height > lead_rows ? (height - lead_rows + cycle - 1u) / cycle : 0;
+    if (lead_frame_stride < nb0 * lead_rows * (size_t)width * 4u) return GEO_EINVAL;
+    if (lead_frame_stride % lead_align != 0 || (uintptr_t)lead_src % lead_align != 0 ||
+        (uintptr_t)dst % lead_align != 0)
+        return GEO_EINVAL;
+    if (world > 1u) {
+        if ((nb1 > 0 && !src) || frame_stride < nb1 * band_rows * (size_t)width * src_bpp ||
+            rank_stride < (size_t)nframes * frame_stride)
+            return GEO_EINVAL;
+        const size_t align = src_bpp == 4u ? lead_align : 4u;
+        if (rank_stride % align != 0 || frame_stride % align != 0 || (uintptr_t)src % align != 0) return GEO_EINVAL;
+    }
+    DeviceGuard g(c->device);
+    if (!g.ok) return GEO_EHIP;
+    hipStream_t s = (hipStream_t)stream;
+    if (width % 4u == 0) {
+        const uint32_t quads = width / 4u;
+        hipLaunchKernelGGL(geo_assemble_lead_kernel<true>, dim3((quads + 255u) / 256u, height, nframes), dim3(256),
+                           0, s, lead_src, lead_frame_stride, lead, src, rank_stride, frame_stride, world, band_rows,
+                           quads, height, src_bpp, dst);
+    } else {
+        hipLaunchKernelGGL(geo_assemble_lead_kernel<false>, dim3((width + 255u) / 256u, height, nframes), dim3(256),
+                           0, s, lead_src, lead_frame_stride, lead, src, rank_stride, frame_stride, world, band_rows,
+                           width, height, src_bpp, dst);
+    }
+    return hipGetLastError() == hipSuccess ? GEO_OK : GEO_EHIP;
+}
+
 int geo_pack_rgb(geo_ctx* c, const uint8_t* rgba, uint64_t npixels, uint8_t* rgb, void* stream) {
     if (!c || !rgba || !rgb || npixels == 0 || npixels % 4u != 0 || (uintptr_t)rgba % 16u != 0 ||
         (uintptr_t)rgb % 4u != 0)
@@ -603,6 +691,21 @@ int geo_render_bands(geo_ctx* c, const geo_frame* frame, const geo_scene* scene,
     return render_impl(c, frame, scene, width, height, (uint32_t)first, (uint32_t)nrows,
                        (uint32_t)__builtin_ctz(band_rows), band_step * band_rows, out_rgba8, out_mask, out_uv,
                        out_steps, steps_total, stream);
+}
+
+int geo_render_band_set(geo_ctx* c, const geo_frame* frame, const geo_scene* scene, uint32_t width,
+                        uint32_t height, uint32_t band_rows, uint32_t row0, uint32_t row_stride, uint32_t nbands,
+                        uint8_t* out_rgba8, uint8_t* out_mask, float* out_uv, uint32_t* out_steps,
+                        unsigned long long* steps_total, void* stream) {
+    if (!c || !frame || !scene || !out_rgba8 || width == 0 || height == 0 || band_rows == 0 || nbands == 0 ||
+        row_stride < band_rows || band_rows < (uint32_t)kWaveRows || (band_rows & (band_rows - 1)) != 0)
+        return GEO_EINVAL;
+    if (width > (1u << 20) || height > (1u << 20)) return GEO_EINVAL;
+    const uint64_t last = (uint64_t)row0 + (uint64_t)(nbands - 1) * row_stride;
+    const uint64_t nrows = (uint64_t)nbands * band_rows;
+    if (row0 >= height || last >= height || nrows > (1u << 20)) return GEO_EINVAL;
+    return render_impl(c, frame, scene, width, height, row0, (uint32_t)nrows, (uint32_t)__builtin_ctz(band_rows),
+                       row_stride, out_rgba8, out_mask, out_uv, out_steps, steps_total, stream);
 }
 
 }  // extern "C"

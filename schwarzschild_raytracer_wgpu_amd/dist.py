@@ -1,12 +1,14 @@
 """Row-band sharding of a frame over the ranks of one node, and the gather to
 rank 0 for present (config 4: 3840x2160 over 8 MI355X).
 
-Rank g renders the interleaved bands g, g+N, g+2N, ... (band_rows rows each,
-geo_render_bands) into a packed local buffer; rank 0 gathers the N packed
-buffers (RCCL over xGMI on GPUs, gloo in the CPU tests) and scatters the bands
-back into frame order (geo_assemble_bands, one launch per gathered batch).  Interleaving balances the frame, whose cost is
-concentrated around the black hole image (8 ranks, 8-row bands: max/mean
-rows 1.007).  The reference has no multi-device path; this is
+Rank g renders its interleaved bands (BandLayout; geo_render_band_set) into a
+packed local buffer; rank 0 gathers the peers' packed buffers (RCCL over xGMI
+on GPUs, gloo in the CPU tests) and scatters them, with its own bands, back
+into frame order (geo_assemble_lead, one launch per gathered batch).
+Interleaving balances the frame, whose cost is concentrated around the black
+hole image (8 ranks, 8-row bands: max/mean rows 1.007).  Every peer row
+crosses an xGMI link into rank 0 and rank 0's rows cross none, so when the
+links bound the present rank 0 takes `lead` times a peer's share.  The reference has no multi-device path; this is
 the present-side exchange the north star asks for.
 """
 from __future__ import annotations
@@ -16,53 +18,114 @@ from dataclasses import dataclass
 
 @dataclass(frozen=True)
 class BandLayout:
+    """Rows of a `height`-row frame owned by each of `world` ranks.
+
+    The frame is cut into cycles of (lead + world - 1) * band_rows rows: rank 0
+    owns the first lead * band_rows rows of every cycle (one band of that
+    height), rank r >= 1 the band_rows rows after rank r - 1's.  lead = 1 is
+    the plain interleave (band b of band_rows rows belongs to rank b % world).
+    lead > 1 is the LEAD layout: rank 0 renders but never sends its rows, so
+    when the present gather is link-bound it takes a larger share
+    (bench.py --rank0-lead picks lead by measurement)."""
     height: int
     band_rows: int
     world: int
     rank: int
+    lead: int = 1
 
+    def __post_init__(self):
+        if self.lead < 1 or self.band_rows < 1 or self.world < 1:
+            raise ValueError("lead, band_rows and world must be >= 1")
+
+    @property
+    def cycle_rows(self) -> int:
+        return (self.lead + self.world - 1) * self.band_rows
+
+    def _r(self, rank):
+        return self.rank if rank is None else rank
+
+    def band_height(self, rank: int | None = None) -> int:
+        """Rows per band of a rank (lead * band_rows for rank 0)."""
+        return self.lead * self.band_rows if self._r(rank) == 0 else self.band_rows
+
+    def row0(self, rank: int | None = None) -> int:
+        """First frame row of a rank's first band."""
+        r = self._r(rank)
+        return 0 if r == 0 else (self.lead + r - 1) * self.band_rows
+
+    def nbands(self, rank: int | None = None) -> int:
+        r0 = self.row0(rank)
+        return 0 if r0 >= self.height else (self.height - r0 + self.cycle_rows - 1) // self.cycle_rows
+
+    def packed_rows(self, rank: int | None = None) -> int:
+        """Rows of a rank's packed buffer (its last band may be clipped)."""
+        return self.nbands(rank) * self.band_height(rank)
+
+    @property
+    def peer_packed_rows(self) -> int:
+        """Packed rows of the largest peer share (rank 1): the size every
+        rank's gather contribution has."""
+        return self.packed_rows(1) if self.world > 1 else 0
+
+    # the plain interleave's vocabulary (lead = 1)
     @property
     def nb_total(self) -> int:
         return (self.height + self.band_rows - 1) // self.band_rows
 
     @property
     def nb_max(self) -> int:
-        return (self.nb_total + self.world - 1) // self.world
+        """Bands of the largest share (rank 0's)."""
+        return self.packed_rows(0) // self.band_rows
 
     def bands(self, rank: int | None = None) -> range:
-        r = self.rank if rank is None else rank
+        if self.lead != 1:
+            raise ValueError("bands() indexes the plain interleave (lead = 1)")
+        r = self._r(rank)
         return range(r, self.nb_total, self.world)
 
     @property
     def nb_mine(self) -> int:
-        return len(self.bands())
-
-    def rows_mine(self) -> int:
-        """Frame rows this rank renders (the last band may be clipped)."""
-        return sum(min(self.band_rows, self.height - b * self.band_rows) for b in self.bands())
+        return self.nbands()
 
     def local_to_frame_rows(self, rank: int | None = None) -> list[int]:
         """Frame row of every local (packed) row; -1 for rows past the frame."""
         out = []
-        for b in self.bands(rank):
-            for i in range(self.band_rows):
-                r = b * self.band_rows + i
+        bh, r0 = self.band_height(rank), self.row0(rank)
+        for j in range(self.nbands(rank)):
+            for i in range(bh):
+                r = r0 + j * self.cycle_rows + i
                 out.append(r if r < self.height else -1)
         return out
 
+    def rows_mine(self) -> int:
+        """Frame rows this rank renders (the last band may be clipped)."""
+        return sum(1 for r in self.local_to_frame_rows() if r >= 0)
 
-def assemble(full, recv, layout: BandLayout, row_bytes: int, frame: int = 0, frame_stride: int | None = None) -> None:
+
+def assemble(full, recv, layout: BandLayout, row_bytes: int, frame: int = 0, frame_stride=None) -> None:
     """Host (torch) reassembly, for the CPU tests: scatter frame `frame` of the
-    gathered packed buffers (one per rank, frames `frame_stride` bytes apart,
-    nb_max bands each) into `full` (nb_total*band_rows*row_bytes elements,
-    frame order).  The GPU path uses geo_assemble_bands."""
-    band = layout.band_rows * row_bytes
-    fs = layout.nb_max * band if frame_stride is None else frame_stride
-    fv = full.view(layout.nb_total, band)
+    gathered packed buffers (recv[r] = rank r's, frames `frame_stride` bytes
+    apart: an int for every rank, a per-rank list, or None = the rank's packed
+    size) into `full` (>= height*row_bytes elements, frame order).  The GPU
+    path uses geo_assemble_bands / geo_assemble_lead."""
+    import torch
+
+    fv = full.view(-1, row_bytes)
     for r in range(layout.world):
-        n = len(layout.bands(r))
-        if n:
-            fv[r::layout.world] = recv[r][frame * fs: frame * fs + layout.nb_max * band].view(layout.nb_max, band)[:n]
+        rows = layout.local_to_frame_rows(r)
+        if not rows:
+            continue
+        n = len(rows)
+        if frame_stride is None:
+            fs = n * row_bytes
+        elif isinstance(frame_stride, int):
+            fs = frame_stride
+        else:
+            fs = frame_stride[r]
+        src = recv[r][frame * fs: frame * fs + n * row_bytes].view(n, row_bytes)
+        rt = torch.tensor(rows)
+        keep = rt >= 0
+        fv[rt[keep]] = src[keep]
 
 
 class ShardedFrame:
@@ -73,43 +136,56 @@ class ShardedFrame:
     batch one async gather (RCCL, launched from its own stream once the
     batch's renders are done) sends the K packed frames to rank 0, so a
     batch's gather overlaps the next batch's renders.  Rank 0 reassembles all
-    K frames of a batch with one geo_assemble_bands launch on a side stream
-    when the batch retires.
+    K frames of a batch, its own bands and the peers', with one
+    geo_assemble_lead launch on a side stream when the batch retires.
 
     K amortises the host cost of a gather (~26-34 us, tools/host_overhead.py)
     over K frames; S = 2 render streams let frame i+1's waves fill frame i's
     tail (at N = 8 a rank's share of a 4K frame is only ~2 waves per slot:
     0.0417 -> 0.0309 ms/frame back to back, tools/scale_probe.py).  All
-    cross-stream hazards are ordered with events: a batch buffer is
-    re-rendered only after its gather completed, rank 0's receive buffer is
-    re-filled only after its reassembly completed.
+    cross-stream hazards are ordered with events: a peer's batch buffer is
+    re-rendered only after its gather completed, rank 0's only after the
+    reassembly that reads it, and rank 0's receive buffer is re-filled only
+    after its reassembly completed.
     """
 
     def __init__(self, ctx, frame, scene, width: int, height: int, band_rows: int, rank: int, world: int, device,
                  dist=None, host_gather: bool = False, frames_per_gather: int = 1, render_streams: int = 1,
-                 present_rgb: bool = True):
+                 present_rgb: bool = True, lead: int = 1):
         """host_gather: stage through host memory (gloo backend; rehearsals only).
-        present_rgb: gather RGB24 (geo_pack_rgb after each render; 25 % fewer
-        bytes on the links) when the width is a multiple of 4."""
+        present_rgb: peers send RGB24 (geo_pack_rgb after each render; 25 %
+        fewer bytes on the links) when the width is a multiple of 4.
+        lead: rank 0's band height in band_rows (BandLayout); rank 0 never
+        sends its own rows, its reassembly reads them from its local bands
+        (geo_assemble_lead)."""
         import torch
 
         self.torch = torch
         self.host_gather = host_gather
         self.ctx, self.frame, self.scene = ctx, frame, scene
         self.width, self.height = width, height
-        self.layout = BandLayout(height, band_rows, world, rank)
+        self.layout = BandLayout(height, band_rows, world, rank, lead if world > 1 else 1)
         self.rank, self.world, self.dist = rank, world, dist
         self.K = max(1, int(frames_per_gather)) if world > 1 else 1
         self.S = min(2, max(1, int(render_streams)))
         L = self.layout
         self.row_bytes = width * 4
-        self.slice = L.nb_max * band_rows * self.row_bytes  # one frame's packed bands
+        # one frame's packed bands: rank 0's share, or the largest peer share
+        # (every gather contribution has the same size)
+        rows = L.packed_rows(0) if rank == 0 else L.peer_packed_rows
+        self.slice = rows * self.row_bytes
         self.bufs = [torch.empty(self.K * self.slice, dtype=torch.uint8, device=device) for _ in range(2)]
         # what travels: RGB24 (3/4 of the bytes) or the RGBA8 bands themselves
         self.bpp = 3 if (present_rgb and world > 1 and width % 4 == 0) else 4
-        self.tslice = self.slice // 4 * self.bpp
-        self.sbufs = self.bufs if self.bpp == 4 else [
-            torch.empty(self.K * self.tslice, dtype=torch.uint8, device=device) for _ in range(2)]
+        self.tslice = L.peer_packed_rows * width * self.bpp
+        if rank == 0 and world > 1:
+            # rank 0's own contribution to the gather is never read (its rows
+            # are reassembled from self.bufs): one zero block
+            dummy = torch.zeros(self.K * self.tslice, dtype=torch.uint8, device=device)
+            self.sbufs = [dummy, dummy]
+        else:
+            self.sbufs = self.bufs if self.bpp == 4 else [
+                torch.empty(self.K * self.tslice, dtype=torch.uint8, device=device) for _ in range(2)]
         self.frame_bytes = height * self.row_bytes  # assembled frames, back to back
         self.extra = [torch.cuda.Stream(device) for _ in range(self.S - 1)]
         self.recv = None
@@ -141,8 +217,16 @@ class ShardedFrame:
 
     def render_local(self, buf, scene=None, **outs) -> None:
         L = self.layout
-        self.ctx.render_bands(self.frame, self.scene if scene is None else scene, self.width, self.height,
-                              L.band_rows, self.rank, self.world, L.nb_mine, buf, **outs)
+        if L.nbands() == 0:  # a frame too small to give this rank a band
+            return
+        self.ctx.render_band_set(self.frame, self.scene if scene is None else scene, self.width, self.height,
+                                 L.band_height(), L.row0(), L.cycle_rows, L.nbands(), buf, **outs)
+
+    def _assemble(self, b: int, src, n: int) -> None:
+        """Rank 0: frames of batch b from its own bands (bufs[b]) and the peers' gathered blocks."""
+        self.ctx.assemble_lead(self.bufs[b], self.slice, self.layout.lead, src, self.K * self.tslice, self.tslice,
+                               self.world, self.layout.band_rows, self.width, self.height, n, self.frames,
+                               src_bpp=self.bpp)
 
     def _render_stream(self, i: int):
         k = i % self.S
@@ -159,7 +243,7 @@ class ShardedFrame:
     def _launch(self, b: int, n: int) -> None:
         self.batches += 1
         if self.world == 1:
-            self.pending[b] = (None, n, self.batches)
+            self.pending[b] = (None, n, self.batches, [])
             return
         torch = self.torch
         gl = list(self.recv[b].chunk(self.world)) if self.rank == 0 else None
@@ -168,42 +252,48 @@ class ShardedFrame:
             work = self.dist.gather(self.sbufs[b].cpu(), gather_list=gl, dst=0, async_op=True)
         else:
             with torch.cuda.stream(self.gstream):
-                for ev in self.ev_rendered[b]:
-                    if ev is not None:
-                        self.gstream.wait_event(ev)
+                # a peer sends after its renders; rank 0 sends nothing it
+                # renders, so its receives are posted at once (its reassembly
+                # waits for its renders instead)
+                if self.rank != 0:
+                    for ev in self.ev_rendered[b]:
+                        if ev is not None:
+                            self.gstream.wait_event(ev)
                 if self.ev_assembled[b] is not None:
                     self.gstream.wait_event(self.ev_assembled[b])  # recv[b] is still being reassembled
                 work = self.dist.gather(self.sbufs[b], gather_list=gl, dst=0, async_op=True)
+        rendered = [ev for ev in self.ev_rendered[b] if ev is not None]
         self.ev_rendered[b] = [None] * self.S
-        self.pending[b] = (work, n, self.batches)
+        self.pending[b] = (work, n, self.batches, rendered)
 
     def _retire(self, b: int) -> None:
         p = self.pending[b]
         if p is None:
             return
         torch = self.torch
-        work, n, seq = p
+        work, n, seq, rendered = p
         self.pending[b] = None
         if work is not None and not self.host_gather:
             st = self.side if self.side is not None else self.gstream
             with torch.cuda.stream(st):
                 work.wait()  # this stream waits for the gather
-                ev = torch.cuda.Event()
-                ev.record(st)
-                self.ev_free[b] = ev
                 if self.side is not None:
-                    self.ctx.assemble_bands(self.recv[b], self.K * self.tslice, self.tslice, self.world,
-                                            self.layout.band_rows, self.width, self.height, n, self.frames,
-                                            src_bpp=self.bpp)
+                    for ev in rendered:  # rank 0's own bands of the batch
+                        st.wait_event(ev)
+                    self._assemble(b, self.recv[b], n)
                     ea = torch.cuda.Event()
                     ea.record(st)
                     self.ev_assembled[b] = ea
+                    self.ev_free[b] = ea  # the reassembly read bufs[b]
+                else:
+                    ev = torch.cuda.Event()
+                    ev.record(st)
+                    self.ev_free[b] = ev
         elif work is not None:
             work.wait()
             if self.rank == 0:
                 src = self.recv[b].to(self.frames.device)
-                self.ctx.assemble_bands(src, self.K * self.tslice, self.tslice, self.world, self.layout.band_rows,
-                                        self.width, self.height, n, self.frames, src_bpp=self.bpp)
+                self._assemble(b, src, n)
                 torch.cuda.current_stream().synchronize()  # `src` is a temporary
         self.frames_done += n
         if self.last is None or seq > self.last[0]:
@@ -225,7 +315,7 @@ class ShardedFrame:
             self.render_local(self.local_view(i), scene=scene, steps_total=steps_total)
             if events is not None:
                 events[1].record()
-            if self.bpp == 3:
+            if self.bpp == 3 and self.rank != 0:
                 self.ctx.pack_rgb(self.local_view(i), self.slice // 4,
                                   self.sbufs[b][sub * self.tslice:(sub + 1) * self.tslice])
             if self.world > 1:

@@ -135,3 +135,85 @@ def test_gloo_batched_gather_reassembles_frames(world, W, H, B, K, nframes):
         p.join(timeout=240)
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
     assert q.get(timeout=10) is True
+
+
+@pytest.mark.parametrize("H,B,world,lead", [(2160, 8, 8, 2), (2160, 8, 2, 4), (180, 8, 3, 2), (27, 8, 2, 2),
+                                            (40, 8, 8, 4), (7, 8, 3, 1), (1080, 16, 4, 4)])
+def test_lead_layout_owns_every_row_once(H, B, world, lead):
+    L = [BandLayout(H, B, world, r, lead) for r in range(world)]
+    owned = sorted(x for l in L for x in l.local_to_frame_rows() if x >= 0)
+    assert owned == list(range(H))
+    assert L[0].band_height() == lead * B and all(l.band_height() == B for l in L[1:])
+    # rank 1 holds the largest peer share: the size of every gather contribution
+    assert all(l.packed_rows() <= L[0].peer_packed_rows for l in L[1:])
+    # rank 0's share is lead times a peer's, up to the last partial cycle
+    if H >= 16 * L[0].cycle_rows:
+        assert abs(L[0].rows_mine() / L[1].rows_mine() - lead) < 0.1
+
+
+def test_lead_one_is_the_plain_interleave():
+    for H, B, world in [(2160, 8, 8), (33, 8, 3), (1080, 16, 4)]:
+        for r in range(world):
+            a, b = BandLayout(H, B, world, r), BandLayout(H, B, world, r, lead=1)
+            rows = [f for band in a.bands() for f in range(band * B, band * B + B)]
+            assert b.local_to_frame_rows() == [f if f < H else -1 for f in rows]
+
+
+def _worker_lead(rank, world, port, W, H, B, lead, K, q):
+    """The lead layout as dist.ShardedFrame runs it: peers send their packed
+    bands (all contributions the size of rank 1's), rank 0 contributes a
+    dummy and reassembles its own rows from its local bands."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import math
+
+        import oracle as O
+        from helpers import default_frame, default_scene
+        from schwarzschild_raytracer_wgpu_amd.scenes import make_sky
+
+        sky = make_sky("equirect", (64, 32))
+        scene = default_scene(256)
+        L = BandLayout(H, B, world, rank, lead)
+        row_bytes = W * 4
+        frames = [default_frame(W, H, camera=(math.pi + 0.1 * f, 0.05 * f)) for f in range(K)]
+        rows = L.packed_rows() if rank == 0 else L.peer_packed_rows
+        sl = rows * row_bytes
+        local = torch.zeros(K * max(sl, 1), dtype=torch.uint8)
+        for f in range(K):
+            lv = local[f * sl:(f + 1) * sl].view(rows, row_bytes)
+            for i, fr in enumerate(L.local_to_frame_rows()):
+                if fr >= 0:
+                    r = O.render_f32(frames[f], scene, sky, W, H, row0=fr, nrows=1, threads=1)
+                    lv[i] = torch.from_numpy(r["rgba"].reshape(-1).copy())
+        tsl = L.peer_packed_rows * row_bytes
+        send = torch.zeros(K * max(tsl, 1), dtype=torch.uint8) if rank == 0 else local
+        recv = torch.empty(world * send.numel(), dtype=torch.uint8) if rank == 0 else None
+        dist.gather(send, gather_list=list(recv.chunk(world)) if rank == 0 else None, dst=0)
+        if rank == 0:
+            gl = list(recv.chunk(world))
+            gl[0] = local  # rank 0's rows never travel
+            ok = True
+            for f in range(K):
+                full = torch.zeros(H * row_bytes, dtype=torch.uint8)
+                assemble(full, gl, L, row_bytes, frame=f, frame_stride=[sl] + [tsl] * (world - 1))
+                ref = O.render_f32(frames[f], scene, sky, W, H, threads=2)["rgba"].reshape(-1)
+                ok = ok and bool(np.array_equal(full.numpy(), ref))
+            q.put(ok)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,W,H,B,lead,K", [(2, 40, 52, 8, 2, 2), (3, 28, 72, 8, 4, 1), (3, 33, 40, 8, 2, 2)])
+def test_gloo_lead_layout_reassembles_frames(world, W, H, B, lead, K):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_lead, args=(r, world, port, W, H, B, lead, K, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=240)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    assert q.get(timeout=10) is True

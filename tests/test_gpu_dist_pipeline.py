@@ -4,7 +4,7 @@ events) on ONE GPU: RCCL cannot put two ranks on one device ("Duplicate GPU
 detected"), so the peer ranks are simulated by a gather stand-in with NCCL's
 stream semantics (the copy runs on its own stream after the caller's stream;
 wait() makes the caller's current stream wait).  Peer data = the peers'
-bands rendered here with geo_render_bands."""
+bands rendered here with geo_render_band_set (plain and lead layouts)."""
 import math
 
 import numpy as np
@@ -47,10 +47,28 @@ class FakeRcclGather:
         return _Work(t, done)
 
 
+def _peer_bands(ctx, torch, frame, scene, W, H, B, r, world, lead, dev, bpp):
+    """Peer r's packed bands in the travelling format, padded to rank 1's size."""
+    from schwarzschild_raytracer_wgpu_amd.dist import BandLayout
+
+    L = BandLayout(H, B, world, r, lead)
+    sl = L.peer_packed_rows * W * 4
+    one = torch.zeros(sl, dtype=torch.uint8, device=dev)
+    if L.nbands():
+        ctx.render_band_set(frame, scene, W, H, B, L.row0(), L.cycle_rows, L.nbands(), one)
+    if bpp == 3:
+        packed = torch.empty(sl // 4 * 3, dtype=torch.uint8, device=dev)
+        ctx.pack_rgb(one, sl // 4, packed)
+        one = packed
+    return one
+
+
 @pytest.mark.parametrize("rgb", [True, False], ids=["rgb24", "rgba8"])
 @pytest.mark.parametrize("S", [1, 2])
-@pytest.mark.parametrize("world,K,nframes", [(2, 4, 41), (3, 3, 10), (8, 4, 16), (8, 1, 5)])
-def test_rank0_pipeline_assembles_frames(world, K, nframes, S, rgb):
+@pytest.mark.parametrize("world,K,nframes,lead", [(2, 4, 41, 1), (3, 3, 10, 1), (8, 4, 16, 1), (8, 1, 5, 1),
+                                                  (2, 4, 13, 2), (2, 2, 7, 4), (4, 3, 10, 2), (8, 4, 9, 2),
+                                                  (8, 2, 6, 4)])
+def test_rank0_pipeline_assembles_frames(world, K, nframes, lead, S, rgb):
     import torch
 
     if not torch.cuda.is_available():
@@ -66,20 +84,11 @@ def test_rank0_pipeline_assembles_frames(world, K, nframes, S, rgb):
     frame, scene = default_frame(W, H), default_scene(512)
     fake = FakeRcclGather(torch, [])
     sf = ShardedFrame(ctx, frame, scene, W, H, B, 0, world, dev, dist=fake, frames_per_gather=K, render_streams=S,
-                      present_rgb=rgb)
-    assert sf.side is not None and sf.bpp == (3 if rgb else 4)
+                      present_rgb=rgb, lead=lead)
+    assert sf.side is not None and sf.bpp == (3 if rgb else 4) and sf.layout.lead == lead
     # the peers' K-frame batches (every frame identical), in the travelling format
     for r in range(1, world):
-        L = BandLayout(H, B, world, r)
-        sl = L.nb_max * B * W * 4
-        one = torch.zeros(sl, dtype=torch.uint8, device=dev)
-        if L.nb_mine:
-            ctx.render_bands(frame, scene, W, H, B, r, world, L.nb_mine, one)
-        if sf.bpp == 3:
-            packed = torch.empty(sl // 4 * 3, dtype=torch.uint8, device=dev)
-            ctx.pack_rgb(one, sl // 4, packed)
-            one = packed
-        fake.peer_bufs.append(one.repeat(K))
+        fake.peer_bufs.append(_peer_bands(ctx, torch, frame, scene, W, H, B, r, world, lead, dev, sf.bpp).repeat(K))
     for i in range(nframes):
         sf.step(i)
     sf.drain()
@@ -96,8 +105,9 @@ def test_rank0_pipeline_assembles_frames(world, K, nframes, S, rgb):
         assert torch.equal(sf.frame_rgba(k), ref), k
 
 
+@pytest.mark.parametrize("lead", [1, 2])
 @pytest.mark.parametrize("S", [1, 2])
-def test_peer_rank_pipeline_runs_batches(S):
+def test_peer_rank_pipeline_runs_batches(S, lead):
     """A peer rank (rank 3 of 4): batches of K frames, each sent with one
     gather; the send buffer is re-rendered only after its gather completed."""
     import torch
@@ -130,22 +140,63 @@ def test_peer_rank_pipeline_runs_batches(S):
     ctx.set_sky(make_sky("equirect", (128, 64)))
     frame, scene = default_frame(W, H), default_scene(256)
     pg = PeerGather()
-    sf = ShardedFrame(ctx, frame, scene, W, H, B, rank, world, dev, dist=pg, frames_per_gather=K, render_streams=S)
+    sf = ShardedFrame(ctx, frame, scene, W, H, B, rank, world, dev, dist=pg, frames_per_gather=K, render_streams=S,
+                      lead=lead)
     for i in range(10):
         sf.step(i)
     sf.drain()
     torch.cuda.synchronize()
     assert len(pg.sent) == 3 and sf.frames_done == 10
-    L = BandLayout(H, B, world, rank)
-    one = torch.zeros(L.nb_max * B * W * 4, dtype=torch.uint8, device=dev)
-    ctx.render_bands(frame, scene, W, H, B, rank, world, L.nb_mine, one)
+    L = BandLayout(H, B, world, rank, lead)
+    one = _peer_bands(ctx, torch, frame, scene, W, H, B, rank, world, lead, dev, sf.bpp)
     torch.cuda.synchronize()
-    if sf.bpp == 3:
-        packed = torch.empty(one.numel() // 4 * 3, dtype=torch.uint8, device=dev)
-        ctx.pack_rgb(one, one.numel() // 4, packed)
-        torch.cuda.synchronize()
-        one = packed
-    used = L.nb_mine * B * W * sf.bpp  # rows past the rank's last band are never written
+    assert pg.sent[0].numel() == K * one.numel()  # every contribution has rank 1's size
+    used = L.nbands() * B * W * sf.bpp  # rows past the rank's last band are never written
     for j, batch in enumerate(pg.sent):
         for k in range(K if j < 2 else 10 - 2 * K):
             assert torch.equal(batch[k * one.numel():k * one.numel() + used], one[:used]), (j, k)
+
+
+@pytest.mark.parametrize("W,H,B,world,lead,bpp,nframes", [
+    (320, 180, 8, 2, 2, 3, 3), (320, 180, 8, 8, 4, 4, 2), (36, 50, 8, 3, 2, 3, 1), (33, 27, 8, 2, 4, 4, 2),
+    (64, 64, 16, 4, 1, 3, 2), (20, 8, 8, 3, 2, 4, 1)])
+def test_assemble_lead_matches_host_assembly(W, H, B, world, lead, bpp, nframes):
+    """geo_assemble_lead on random bytes == dist.assemble (the host reassembly
+    the gloo tests check against the oracle), RGB24 and RGBA8 peers, widths
+    that are and are not multiples of 4, frames with empty peer shares."""
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    import schwarzschild_raytracer_wgpu_amd as g
+    from schwarzschild_raytracer_wgpu_amd.dist import BandLayout, assemble
+
+    dev = torch.device("cuda:0")
+    ctx = g.Context(0)
+    L = BandLayout(H, B, world, 0, lead)
+    gen = torch.Generator().manual_seed(W * 7919 + H * 31 + world * 7 + lead)
+    own_sl = L.packed_rows(0) * W * 4
+    own_sl += (-own_sl) % 16
+    tsl = L.peer_packed_rows * W * bpp
+    tsl += (-tsl) % 16
+    own = torch.randint(0, 256, (nframes * own_sl,), dtype=torch.uint8, generator=gen)
+    peers = torch.randint(0, 256, (world * nframes * max(tsl, 1),), dtype=torch.uint8, generator=gen)
+    out = torch.full((nframes * H * W * 4,), 7, dtype=torch.uint8, device=dev)
+    ctx.assemble_lead(own.to(dev), own_sl, lead, peers.to(dev), nframes * tsl, tsl, world, B, W, H, nframes, out,
+                      src_bpp=bpp)
+    torch.cuda.synchronize()
+    got = out.cpu()
+    for f in range(nframes):
+        # host reference: RGBA8 blocks per rank (RGB24 peers widened, alpha 255)
+        blocks = [own]
+        for r in range(1, world):
+            blk = peers[r * nframes * tsl:(r + 1) * nframes * tsl]
+            if bpp == 3:
+                px = blk.view(nframes, tsl)[:, :L.peer_packed_rows * W * 3].reshape(nframes, -1, 3)
+                rgba = torch.cat([px, torch.full(px.shape[:2] + (1,), 255, dtype=torch.uint8)], dim=2)
+                blk = rgba.reshape(-1)
+            blocks.append(blk)
+        peer_stride = L.peer_packed_rows * W * 4 if bpp == 3 else tsl
+        ref = torch.zeros(H * W * 4, dtype=torch.uint8)
+        assemble(ref, blocks, L, W * 4, frame=f, frame_stride=[own_sl] + [peer_stride] * (world - 1))
+        assert torch.equal(got[f * H * W * 4:(f + 1) * H * W * 4], ref), f

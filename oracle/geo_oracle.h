@@ -8,8 +8,12 @@
  * wgpu_renderer submodule is empty) and its only hot-path test,
  * sphere_geodesics_test (SR/simulation/tests.rs:8-13), asserts nothing.  The
  * oracle is pinned instead by analytic known-answer tests (flat space,
- * capture threshold, scale invariance, radial rays: tests/test_oracle_kat.py)
- * and by committed golden vectors of its own output (tests/golden/).
+ * capture threshold, scale invariance, radial rays: tests/test_oracle_kat.py),
+ * by an independent high-precision solution of the reference's initial value
+ * problem and stop rules (scipy DOP853, tests/test_oracle_physics.py: within
+ * 5.2e-8 rad, hit/capture identical) and by committed golden vectors of its
+ * own output (tests/golden/).  The point-path oracle (geo_oracle_points.c) is
+ * pinned by the reference's own RayConnector tests (tests.rs:15-79).
  *
  * Contents:
  *   f64 restatements, operation for operation, of the reference:

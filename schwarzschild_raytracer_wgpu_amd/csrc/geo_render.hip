@@ -24,6 +24,10 @@
 #include "geo_ctx.h"
 #include "geo_pixel.h"
 
+#ifndef GEO_BH_SKIP_UV
+#define GEO_BH_SKIP_UV 1
+#endif
+
 namespace {
 
 constexpr int kTileW = 8;   // a wave64 covers an 8x8 pixel square (fewest divergent
@@ -99,8 +103,14 @@ __global__ __launch_bounds__(kBlock) void geo_render_kernel(const RenderArgs a) 
             lam = geo::kPi2 - geo::geodesic_angle_v<GEO_LOOP_VARIANT, KIND>(a.k, st, ct, &steps);
         }
         const bool bh = lam < geo::kBlackHoleLambda;
-        float U, V;
-        geo::sky_uv(a.frame.central_to_uv, c2x, c2y, ct, lam, &U, &V);
+        // A black-hole pixel is discarded (shader.wgsl:88): it needs its UV
+        // only when the caller asks for it, so a wave inside the shadow skips
+        // the sincos/atan2/asin and the sample (GEO_BH_SKIP_UV 0: always compute)
+        float U = 0.0f, V = 0.0f;
+#if GEO_BH_SKIP_UV
+        if (!bh || a.out_uv)
+#endif
+            geo::sky_uv(a.frame.central_to_uv, c2x, c2y, ct, lam, &U, &V);
         const uint32_t* sky = a.sky;
         auto fetch = [sky](uint32_t i) { return sky[i]; };
         const size_t o = (size_t)ly * a.width + px;

@@ -1,12 +1,16 @@
 #!/usr/bin/env python3
-"""The reference's whole frame on one GPU (SR/lib.rs:62-94, renderer.rs:208-264):
-sky sphere (r 50), planet sphere (r 1.1), translucent cloud sphere (r 1.2),
-each a per-pixel geodesic draw composited in order, then the accretion disk
-(PointCloud::update with f64 orbits and both RayConnector sides, then the
-near and far point draws).  One JSON line: ms per frame (wall, K frames back
-to back on one stream), frames/s, and each part's GPU time from event pairs.
+"""The reference's whole frame on one GPU (SR/lib.rs:62-94, 413-419,
+renderer.rs:208-264).  The reference builds three spheres -- sky (r 50),
+planet (r 1.1) and translucent clouds (r 1.2) -- but draws only the sky:
+lib.rs:415 passes `&[&self.first_sphere/*, &self.second_sphere ,
+&self.third_sphere*/]`.  --spheres 1 (default) is that frame: the sky's
+per-pixel geodesic draw, then the accretion disk (PointCloud::update with f64
+orbits and both RayConnector sides, then the near and far point draws).
+--spheres 3 adds the commented-out planet and clouds, composited in order.
+One JSON line: ms per frame (wall, K frames back to back on one stream),
+frames/s, and each part's GPU time from event pairs.
 
-  python tools/bench_scene.py [--width 3840 --height 2160] [--frames 200] [--points 5000]
+  python tools/bench_scene.py [--width 3840 --height 2160] [--frames 200] [--points 5000] [--spheres 1|3]
 
 Textures are synthetic (the reference's are absent): the benchmark equirect
 sky, a 2048x1024 checkerboard planet and a seeded random-alpha cloud layer.
@@ -34,6 +38,8 @@ def main():
     p.add_argument("--warmup", type=int, default=100)
     p.add_argument("--points", type=int, default=5000)
     p.add_argument("--max-steps", type=int, default=1000, help="per sphere (basic_sphere_buffer.rs:42-51)")
+    p.add_argument("--spheres", type=int, default=1, choices=[1, 3],
+                   help="1: the sky only, as the reference draws (lib.rs:415); 3: with planet and clouds")
     args = p.parse_args()
 
     import numpy as np
@@ -51,11 +57,11 @@ def main():
     clouds = np.random.default_rng(11).integers(0, 256, size=(1024, 2048, 4), dtype=np.uint8)
     spheres = [g.BasicSphereBuffer(0, 50.0, 1.0, sky, max_iter=args.max_steps),
                g.BasicSphereBuffer(0, 1.1, 1.0, planet, max_iter=args.max_steps),
-               g.BasicSphereBuffer(0, 1.2, 1.0, clouds, max_iter=args.max_steps)]
+               g.BasicSphereBuffer(0, 1.2, 1.0, clouds, max_iter=args.max_steps)][:args.spheres]
     disk = g.PointCloud.new_accretion_disk(spheres[0].ctx, 1.0, obs.get_position(), True, n=args.points)
     tgt = g.RenderTarget(w, h, torch.empty(w * h * 4, dtype=torch.uint8, device="cuda:0"))
 
-    parts = ("disk update", "sky", "planet", "clouds", "points")
+    parts = ("disk update", "sky", "planet", "clouds")[:2 + len(spheres) - 1] + ("points",)
 
     def frame(evs=None):
         obs.update_position((0.0, 0.0, 0.0), 1 / 60)
@@ -74,7 +80,7 @@ def main():
                 evs[2 + i].record()
         disk.draw(f, tgt)
         if evs:
-            evs[5].record()
+            evs[2 + len(spheres)].record()
 
     for _ in range(args.warmup):
         frame()
@@ -88,14 +94,17 @@ def main():
     acc = np.zeros(len(parts))
     nev = 20
     for _ in range(nev):
-        evs = [HipEvent() for _ in range(6)]
+        evs = [HipEvent() for _ in range(len(parts) + 1)]
         frame(evs)
         torch.cuda.synchronize()
-        acc += [evs[i].elapsed_time(evs[i + 1]) for i in range(5)]
+        acc += [evs[i].elapsed_time(evs[i + 1]) for i in range(len(parts))]
     acc /= nev
     print(json.dumps({
-        "what": "the reference's frame: 3 composited per-pixel geodesic spheres + accretion disk "
-                "(orbits, 2 x RayConnector, point draws)",
+        "what": ("the reference's frame as drawn (lib.rs:415): the sky's per-pixel geodesic draw + accretion disk "
+                 "(orbits, 2 x RayConnector, point draws)" if len(spheres) == 1 else
+                 "the reference's frame with its commented-out planet and clouds: 3 composited per-pixel geodesic "
+                 "spheres + accretion disk (orbits, 2 x RayConnector, point draws)"),
+        "spheres": len(spheres),
         "width": w, "height": h, "frames": args.frames, "points": args.points, "max_steps": args.max_steps,
         "ms_per_frame": wall * 1e3, "frames_per_s": 1.0 / wall,
         "gpu_ms": {k: float(v) for k, v in zip(parts, acc)},

@@ -27,11 +27,16 @@
 #ifndef GEO_BH_SKIP_UV
 #define GEO_BH_SKIP_UV 1
 #endif
+// rows of a workgroup's 8-wide tile (a multiple of 8): 8, 16 and 32 time the
+// same, 64 and 128 are 1.3 % and 4.5 % slower
+#ifndef GEO_TILE_H
+#define GEO_TILE_H 32
+#endif
 
 namespace {
 
 constexpr int kTileW = 8;   // a wave64 covers an 8x8 pixel square (fewest divergent
-constexpr int kTileH = 32;  // steps per wave; tools/ubench/loop_ab.hip), a block 8x32
+constexpr int kTileH = GEO_TILE_H;  // steps per wave; tools/ubench/loop_ab.hip), a block 8 x kTileH
 constexpr int kBlock = kTileW * kTileH;  // 256 threads = 4 waves
 constexpr int kWaveRows = 64 / kTileW;   // rows covered by one wave
 constexpr uint32_t kMaxFan = 4096;       // LDS fan capacity (16 KiB)

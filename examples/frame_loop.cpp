@@ -7,7 +7,7 @@
 // Build:
 //   g++ -std=c++17 -O2 -D__HIP_PLATFORM_AMD__ -I include -I /opt/rocm/include examples/frame_loop.cpp
 //       -L schwarzschild_raytracer_wgpu_amd -lgeo -L /opt/rocm/lib -lamdhip64 -o frame_loop
-//   ./frame_loop [W H FRAMES out.ppm]
+//   ./frame_loop [W H FRAMES out.ppm OVERLAP(1|0)]
 //
 // Prints frames/s of the whole loop (host + GPU, K frames back to back) and
 // writes the last frame.  Scene: the reference's, scaled to rs = 1 (its
@@ -24,6 +24,7 @@ int main(int argc, char** argv) {
     const uint32_t H = argc > 2 ? (uint32_t)std::atoi(argv[2]) : 1080u;
     const int frames = argc > 3 ? std::atoi(argv[3]) : 300;
     const char* out = argc > 4 ? argv[4] : "frame_loop.ppm";
+    const bool overlap = argc > 5 ? std::atoi(argv[5]) != 0 : true;
     try {
         sr::Image sky;
         sky.width = 2048;
@@ -45,13 +46,18 @@ int main(int argc, char** argv) {
         sr::PointCloud first_point_cloud =
             sr::PointCloud::new_accretion_disk(0, 1.0f, renderer.get_position(), true);
 
+        // The disk update is latency-bound (one lane per connector, sequential
+        // 48-node solves): on a side stream it overlaps the VALU-bound sky
+        // draw; PointCloud::draw waits for it (geo_points_draw).
+        hipStream_t side = nullptr;
+        if (overlap) sr::hip_check(hipStreamCreateWithFlags(&side, hipStreamNonBlocking), "hipStreamCreate");
         const double dt = 1.0 / 60.0;
         auto frame = [&]() {
             // State::update (lib.rs:287-300)
             renderer.update(dt);
             const double r = renderer.get_radial_position();
             first_sphere.update_ray_fan(r);
-            first_point_cloud.update(renderer.get_position(), dt);
+            first_point_cloud.update(renderer.get_position(), dt, side);
             // State::render (lib.rs:413-419): the first sphere and both point meshes
             renderer.render({&first_sphere}, {&first_point_cloud});
         };
@@ -68,8 +74,10 @@ int main(int argc, char** argv) {
         std::fprintf(f, "P6\n%u %u\n255\n", W, H);
         for (size_t i = 0; i < (size_t)W * H; ++i) std::fwrite(&rgba[4 * i], 1, 3, f);
         std::fclose(f);
-        std::printf("%ux%u: %d frames in %.3f s = %.1f frames/s (%.4f ms/frame); observer r = %.4f\n", W, H, frames,
-                    s, frames / s, s / frames * 1e3, renderer.get_radial_position());
+        std::printf("%ux%u%s: %d frames in %.3f s = %.1f frames/s (%.4f ms/frame); observer r = %.4f\n", W, H,
+                    overlap ? " (disk update on a side stream)" : "", frames, s, frames / s, s / frames * 1e3,
+                    renderer.get_radial_position());
+        if (side) sr::hip_check(hipStreamDestroy(side), "hipStreamDestroy");
         return 0;
     } catch (const sr::Error& e) {
         std::fprintf(stderr, "sr::Error: %s\n", e.what());

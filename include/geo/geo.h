@@ -265,7 +265,8 @@ int geo_points_update(geo_points* pts, const float* observer_xyz, double dt, voi
 /* get_vertices / get_vertices_farside: device pointer, 4 floats per point
  * (NULL for the far side of a cloud without one). */
 const float* geo_points_vertices(const geo_points* pts, int farside);
-/* current point positions (host, 3 floats per point); synchronises `stream`. */
+/* current point positions (host, 3 floats per point); `stream` waits for the
+ * last update, then the call synchronises it. */
 int geo_points_positions(const geo_points* pts, float* out_xyz, void* stream);
 
 /* The point pipeline (SR/schwarzschild_point_shader/shader.wgsl:36-74,
@@ -276,6 +277,16 @@ int geo_points_positions(const geo_points* pts, float* out_xyz, void* stream);
 int geo_draw_points(geo_ctx* ctx, const geo_frame* frame, const float* vertices, uint32_t n, uint32_t width,
                     uint32_t height, uint32_t row0, uint32_t nrows, uint8_t* out_rgba8, int* out_xy,
                     void* stream);
+
+/* The point meshes of a PointCloud (the near-side vertices, then the
+ * far-side ones; lib.rs:415-418, renderer.rs:256-264) drawn as by
+ * geo_draw_points.  out_xy (device, optional): 2 ints per connector, near
+ * side first.  Stream order: the draw waits for the cloud's last
+ * geo_points_update and the next update waits for this draw (events owned by
+ * the cloud), whichever streams they run on, so a caller may put the update
+ * on a side stream where it overlaps the sphere draws.  Async on `stream`. */
+int geo_points_draw(geo_points* pts, const geo_frame* frame, uint32_t width, uint32_t height, uint32_t row0,
+                    uint32_t nrows, uint8_t* out_rgba8, int* out_xy, void* stream);
 
 /* ---- observer (host, f64; SR/simulation/observer.rs) ----------------- */
 /* Observer::new (observer.rs:68-87): pos (25,0,1), camera (PI,0), FrozenFall,

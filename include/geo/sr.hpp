@@ -409,7 +409,8 @@ class PointCloud {
     }
 
     // update (:117-148): orbits and respawns, then update_ray(observer, 1);
-    // dt in seconds; asynchronous on `stream`
+    // dt in seconds; asynchronous on `stream` (a side stream overlaps it with
+    // the sphere draws; draw() orders itself after it)
     void update(Vec3 observer_pos, double dt, void* stream = nullptr) {
         const float o[3] = {observer_pos.x, observer_pos.y, observer_pos.z};
         check(geo_points_update(h_.get(), o, dt, stream), "geo_points_update");
@@ -425,13 +426,16 @@ class PointCloud {
     }
     // the point meshes' draw (schwarzschild_point_shader/shader.wgsl:36-74):
     // the near-side vertices, then the far-side ones
+    // (geo_points_draw).  The draw waits for the last update() and the next
+    // update() for the draw, on whichever streams they run, so update() may
+    // take a side stream and overlap the sphere draws.
     void draw(RenderPass& pass) const {
-        for (int far = 0; far < (farside_ ? 2 : 1); ++far)
-            check(geo_draw_points(ctx_->get(), &pass.uniform, geo_points_vertices(h_.get(), far), n_, pass.width,
-                                  pass.height, 0, pass.height, pass.target, nullptr, pass.stream),
-                  "geo_draw_points");
+        check(geo_points_draw(h_.get(), &pass.uniform, pass.width, pass.height, 0, pass.height, pass.target, nullptr,
+                              pass.stream),
+              "geo_points_draw");
     }
     uint32_t len() const { return n_; }
+    bool has_farside() const { return farside_; }
 
    private:
     struct Del {

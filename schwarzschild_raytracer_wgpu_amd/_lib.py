@@ -112,6 +112,7 @@ SIGNATURES = {
     "geo_points_vertices": (_vp, [_vp, _int]),
     "geo_points_positions": (_int, [_vp, _vp, _vp]),
     "geo_draw_points": (_int, [_vp, ctypes.POINTER(GeoFrame), _vp, _u32, _u32, _u32, _u32, _u32, _vp, _vp, _vp]),
+    "geo_points_draw": (_int, [_vp, ctypes.POINTER(GeoFrame), _u32, _u32, _u32, _u32, _vp, _vp, _vp]),
     "geo_observer_create": (_int, [_f64, _f64, _f64, _f64, ctypes.POINTER(_vp)]),
     "geo_observer_destroy": (None, [_vp]),
     "geo_observer_set_position": (_int, [_vp, _f64, _f64, _f64]),

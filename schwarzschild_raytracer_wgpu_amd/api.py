@@ -450,9 +450,14 @@ class PointCloud:
         return out
 
     def draw(self, frame: GeoFrame, target: "RenderTarget", out_xy=None, stream=None) -> None:
-        """The point pipeline over the target (both vertex buffers)."""
-        for far in ((False, True) if self.has_farside else (False,)):
-            draw_points(self.ctx, frame, self.vertices_ptr(far), self.n, target, out_xy=out_xy, stream=stream)
+        """The point pipeline over the target, near then far vertex buffer
+        (geo_points_draw).  It waits for the last update() on whatever stream
+        that ran, and the next update() waits for it, so update() may run on
+        a side stream, overlapping the sphere draws.  out_xy (device, int32):
+        2 per connector, near side first."""
+        check("geo_points_draw", lib.geo_points_draw(self._h, ctypes.byref(frame), target.width, target.height, 0,
+                                                     target.height, _ptr(target.rgba), _ptr(out_xy),
+                                                     _stream_handle(stream)))
 
 
 def draw_points(ctx: Context, frame: GeoFrame, vertices, n: int, target: "RenderTarget", row0: int = 0,

@@ -360,6 +360,12 @@ struct geo_rays {
 struct geo_points {
     geo_rays rays;
     bool has_orbits;
+    // Cross-stream order of the update and the draw (geo_points_draw): the
+    // draw waits for the last update, the next update for the last draw, so
+    // a caller may run the update on a side stream, overlapping the
+    // VALU-bound sphere draw with this latency-bound work.
+    hipEvent_t updated = nullptr, drawn = nullptr;
+    bool updated_rec = false, drawn_rec = false;
 };
 
 namespace {
@@ -536,10 +542,15 @@ int geo_points_create(geo_ctx* ctx, float schwarz_r, const float* model_xyz, uin
                     hipMemset(r->respawn, 0, n) != hipSuccess))
             st = GEO_EHIP;
     }
+    if (!st && (hipEventCreateWithFlags(&p->updated, hipEventDisableTiming) != hipSuccess ||
+                hipEventCreateWithFlags(&p->drawn, hipEventDisableTiming) != hipSuccess))
+        st = GEO_EHIP;
     // reset_ray(observer_pos) for every connector (:43, :46)
     if (!st) st = rays_launch(r, observer_xyz[0], observer_xyz[1], observer_xyz[2], nullptr, 0u, 1, false, nullptr, 0);
     if (!st && hipDeviceSynchronize() != hipSuccess) st = GEO_EHIP;
     if (st) {
+        for (hipEvent_t e : {p->updated, p->drawn})
+            if (e) (void)hipEventDestroy(e);
         rays_free(r);
         delete p;
         return st;
@@ -551,6 +562,8 @@ int geo_points_create(geo_ctx* ctx, float schwarz_r, const float* model_xyz, uin
 void geo_points_destroy(geo_points* p) {
     if (!p) return;
     DeviceGuard g(p->rays.device);
+    for (hipEvent_t e : {p->updated, p->drawn})
+        if (e) (void)hipEventDestroy(e);
     rays_free(&p->rays);
     delete p;
 }
@@ -563,14 +576,19 @@ int geo_points_update(geo_points* p, const float* observer_xyz, double dt, void*
     DeviceGuard g(r->device);
     if (!g.ok) return GEO_EHIP;
     hipStream_t s = (hipStream_t)stream;
+    if (p->drawn_rec && hipStreamWaitEvent(s, p->drawn, 0) != hipSuccess) return GEO_EHIP;  // last draw read the vertices
     if (p->has_orbits) {
         hipLaunchKernelGGL(geo_orbits_kernel, dim3((r->n_points + kOrbitBlock - 1) / kOrbitBlock), dim3(kOrbitBlock),
                            0, s, r->n_points, dt, r->rs, r->orbits, r->rng, r->pos, r->respawn, r->respawn_pos);
         if (hipGetLastError() != hipSuccess) return GEO_EHIP;
     }
     // update_ray(observer_pos, 1) (:143-146)
-    return rays_launch(r, observer_xyz[0], observer_xyz[1], observer_xyz[2], nullptr, 1u, 0, p->has_orbits, nullptr,
-                       s);
+    const int st = rays_launch(r, observer_xyz[0], observer_xyz[1], observer_xyz[2], nullptr, 1u, 0, p->has_orbits,
+                               nullptr, s);
+    if (st) return st;
+    if (hipEventRecord(p->updated, s) != hipSuccess) return GEO_EHIP;
+    p->updated_rec = true;
+    return GEO_OK;
 }
 
 const float* geo_points_vertices(const geo_points* p, int farside) {
@@ -587,6 +605,7 @@ int geo_points_positions(const geo_points* p, float* out_xyz, void* stream) {
     if (!g.ok) return GEO_EHIP;
     std::vector<float> soa(3 * (size_t)r->n_points);
     hipStream_t s = (hipStream_t)stream;
+    if (p->updated_rec && hipStreamWaitEvent(s, p->updated, 0) != hipSuccess) return GEO_EHIP;
     if (hipMemcpyAsync(soa.data(), r->pos, soa.size() * sizeof(float), hipMemcpyDeviceToHost, s) != hipSuccess ||
         hipStreamSynchronize(s) != hipSuccess)
         return GEO_EHIP;
@@ -595,14 +614,11 @@ int geo_points_positions(const geo_points* p, float* out_xyz, void* stream) {
     return GEO_OK;
 }
 
-int geo_draw_points(geo_ctx* ctx, const geo_frame* frame, const float* vertices, uint32_t n, uint32_t width,
-                    uint32_t height, uint32_t row0, uint32_t nrows, uint8_t* out_rgba8, int* out_xy, void* stream) {
-    if (!ctx || !frame || (!vertices && n) || !out_rgba8 || width == 0 || height == 0 || nrows == 0 ||
-        row0 >= height || nrows > height - row0)
-        return GEO_EINVAL;
-    if (n == 0) return GEO_OK;
-    DeviceGuard g(ctx->device);
-    if (!g.ok) return GEO_EHIP;
+}  // extern "C"
+
+namespace {
+int draw_launch(const geo_frame* frame, const float* vertices, uint32_t n, uint32_t width, uint32_t height,
+                uint32_t row0, uint32_t nrows, uint8_t* out_rgba8, int* out_xy, hipStream_t stream) {
     DrawArgs a;
     std::memcpy(&a.frame, frame, sizeof(geo_frame));
     a.verts = reinterpret_cast<const float4*>(vertices);
@@ -613,9 +629,46 @@ int geo_draw_points(geo_ctx* ctx, const geo_frame* frame, const float* vertices,
     a.nrows = nrows;
     a.out_rgba = reinterpret_cast<uint32_t*>(out_rgba8);
     a.out_xy = reinterpret_cast<int2*>(out_xy);
-    hipLaunchKernelGGL(geo_draw_kernel, dim3((n + kRaysBlock - 1) / kRaysBlock), dim3(kRaysBlock), 0,
-                       (hipStream_t)stream, a);
+    hipLaunchKernelGGL(geo_draw_kernel, dim3((n + kRaysBlock - 1) / kRaysBlock), dim3(kRaysBlock), 0, stream, a);
     return hipGetLastError() == hipSuccess ? GEO_OK : GEO_EHIP;
+}
+
+bool draw_args_ok(const geo_frame* frame, uint32_t width, uint32_t height, uint32_t row0, uint32_t nrows,
+                  const uint8_t* out_rgba8) {
+    return frame && out_rgba8 && width && height && nrows && row0 < height && nrows <= height - row0;
+}
+}  // namespace
+
+extern "C" {
+
+int geo_draw_points(geo_ctx* ctx, const geo_frame* frame, const float* vertices, uint32_t n, uint32_t width,
+                    uint32_t height, uint32_t row0, uint32_t nrows, uint8_t* out_rgba8, int* out_xy, void* stream) {
+    if (!ctx || (!vertices && n) || !draw_args_ok(frame, width, height, row0, nrows, out_rgba8)) return GEO_EINVAL;
+    if (n == 0) return GEO_OK;
+    DeviceGuard g(ctx->device);
+    if (!g.ok) return GEO_EHIP;
+    return draw_launch(frame, vertices, n, width, height, row0, nrows, out_rgba8, out_xy, (hipStream_t)stream);
+}
+
+int geo_points_draw(geo_points* p, const geo_frame* frame, uint32_t width, uint32_t height, uint32_t row0,
+                    uint32_t nrows, uint8_t* out_rgba8, int* out_xy, void* stream) {
+    if (!p || !draw_args_ok(frame, width, height, row0, nrows, out_rgba8)) return GEO_EINVAL;
+    const geo_rays* r = &p->rays;
+    DeviceGuard g(r->device);
+    if (!g.ok) return GEO_EHIP;
+    hipStream_t s = (hipStream_t)stream;
+    if (p->updated_rec && hipStreamWaitEvent(s, p->updated, 0) != hipSuccess) return GEO_EHIP;
+    // the near-side mesh, then the far-side one (lib.rs:415-418, renderer.rs:256-264)
+    const int sides = (r->sides & GEO_RAYS_FAR) ? 2 : 1;
+    for (int far = 0; far < sides; ++far) {
+        const int st = draw_launch(frame, reinterpret_cast<const float*>(r->verts + (far ? r->n_points : 0)),
+                                   r->n_points, width, height, row0, nrows, out_rgba8,
+                                   out_xy ? out_xy + 2 * (size_t)far * r->n_points : nullptr, s);
+        if (st) return st;
+    }
+    if (hipEventRecord(p->drawn, s) != hipSuccess) return GEO_EHIP;
+    p->drawn_rec = true;
+    return GEO_OK;
 }
 
 }  // extern "C"

@@ -135,7 +135,11 @@ def test_cpp_frame_loop_runs(tmp_path):
     if not _has_gpu():
         pytest.skip("no HIP device")
     exe = build(tmp_path, os.path.join(ROOT, "examples", "frame_loop.cpp"))
-    out = tmp_path / "f.ppm"
-    r = subprocess.run([exe, "192", "108", "20", str(out)], capture_output=True, text=True, timeout=120)
-    assert r.returncode == 0, r.stdout + r.stderr
-    assert "frames/s" in r.stdout and out.stat().st_size == len(b"P6\n192 108\n255\n") + 192 * 108 * 3
+    outs = []
+    for overlap in ("1", "0"):  # disk update on a side stream / on the render stream
+        out = tmp_path / f"f{overlap}.ppm"
+        r = subprocess.run([exe, "192", "108", "20", str(out), overlap], capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0, r.stdout + r.stderr
+        assert "frames/s" in r.stdout and out.stat().st_size == len(b"P6\n192 108\n255\n") + 192 * 108 * 3
+        outs.append(out.read_bytes())
+    assert outs[0] == outs[1]  # the same frame either way (geo_points_draw waits for the update)

@@ -426,6 +426,42 @@ def test_renderer_three_spheres_and_points(geo, torch_mod):
     assert np.array_equal(tgt.rgba.cpu().numpy().reshape(h, w, 4), img)
 
 
+def test_points_update_on_side_stream_matches_one_stream(geo, torch_mod):
+    """The frame loop with PointCloud.update on a side stream (overlapping the
+    sky draw; geo_points_draw orders itself after the update and the next
+    update after the draw) == the same loop on one stream, frame by frame,
+    with orbits and respawns running."""
+    from schwarzschild_raytracer_wgpu_amd.scenes import make_sky
+
+    w, h = 640, 360
+    dev = torch_mod.device("cuda:0")
+    sky = make_sky("equirect", (1024, 512))
+
+    def loop(side):
+        obs = geo.Observer(1.0, math.pi / 2, w, h)
+        obs.set_position(2.5, 0.0, 0.1)
+        sphere = geo.BasicSphereBuffer(0, 50.0, 1.0, sky, max_iter=2048)
+        disk = geo.PointCloud.new_accretion_disk(sphere.ctx, 1.0, obs.get_position(), True, seed=3, n=5000)
+        tgt = geo.RenderTarget(w, h, torch_mod.empty(w * h * 4, dtype=torch_mod.uint8, device=dev))
+        frames = []
+        for _ in range(8):
+            obs.update_position((0.0, 0.0, 0.0), 1 / 60)
+            sphere.update_ray_fan(obs.get_radial_position())
+            disk.update(obs.get_position(), 0.25, stream=side)  # long steps: particles fall and respawn
+            geo.Renderer(obs).render([sphere], tgt, point_clouds=[disk])
+            frames.append(tgt.rgba.clone())
+        torch_mod.cuda.synchronize()
+        return [f.cpu().numpy() for f in frames], disk.get_vertices(False), disk.get_vertices(True)
+
+    one = loop(None)
+    two = loop(torch_mod.cuda.Stream(dev))
+    for a, b in zip(one[0], two[0]):
+        assert np.array_equal(a, b)
+    assert np.array_equal(one[1], two[1]) and np.array_equal(one[2], two[2])
+    red = [int((f.reshape(h, w, 4)[..., :3] == np.array([255, 0, 0], np.uint8)).all(-1).sum()) for f in one[0]]
+    assert min(red) > 100  # the disk is drawn in every frame
+
+
 @pytest.mark.parametrize("rotation,nframes", [(3.2, 120), (2.0, 200)])
 def test_orbit_replay_render_bitexact(geo, torch_mod, rotation, nframes):
     """N2 scenario replay: an orbiting observer (non-identity movement_to_central,

@@ -7,10 +7,13 @@ lib.rs:415 passes `&[&self.first_sphere/*, &self.second_sphere ,
 per-pixel geodesic draw, then the accretion disk (PointCloud::update with f64
 orbits and both RayConnector sides, then the near and far point draws).
 --spheres 3 adds the commented-out planet and clouds, composited in order.
-One JSON line: ms per frame (wall, K frames back to back on one stream),
-frames/s, and each part's GPU time from event pairs.
+One JSON line: ms per frame (wall, K frames back to back), frames/s, and
+each part's GPU time from event pairs (parts back to back on one stream).
+--overlap 1 (default) puts the disk update on a side stream: it is
+latency-bound (10 000 lanes of sequential 48-node solves) and hides under the
+VALU-bound sky draw; the point draw waits for it (geo_points_draw).
 
-  python tools/bench_scene.py [--width 3840 --height 2160] [--frames 200] [--points 5000] [--spheres 1|3]
+  python tools/bench_scene.py [--width 3840 --height 2160] [--frames 200] [--points 5000] [--spheres 1|3] [--overlap 1|0]
 
 Textures are synthetic (the reference's are absent): the benchmark equirect
 sky, a 2048x1024 checkerboard planet and a seeded random-alpha cloud layer.
@@ -40,6 +43,9 @@ def main():
     p.add_argument("--max-steps", type=int, default=1000, help="per sphere (basic_sphere_buffer.rs:42-51)")
     p.add_argument("--spheres", type=int, default=1, choices=[1, 3],
                    help="1: the sky only, as the reference draws (lib.rs:415); 3: with planet and clouds")
+    p.add_argument("--overlap", type=int, default=1, choices=[0, 1],
+                   help="1: the disk update on a side stream, overlapping the sphere draws (geo_points_draw "
+                        "orders the point draw after it); 0: everything on one stream")
     args = p.parse_args()
 
     import numpy as np
@@ -62,6 +68,7 @@ def main():
     tgt = g.RenderTarget(w, h, torch.empty(w * h * 4, dtype=torch.uint8, device="cuda:0"))
 
     parts = ("disk update", "sky", "planet", "clouds")[:2 + len(spheres) - 1] + ("points",)
+    side = torch.cuda.Stream() if args.overlap else None
 
     def frame(evs=None):
         obs.update_position((0.0, 0.0, 0.0), 1 / 60)
@@ -69,11 +76,12 @@ def main():
         for s in spheres:
             s.update_ray_fan(r)  # records r (direct mode integrates per pixel)
         f = obs.calc_transformation_pipeline()
-        if evs:
+        if evs:  # per-part timing: the parts back to back on one stream
             evs[0].record()
-        disk.update(obs.get_position(), 1 / 60)
-        if evs:
+            disk.update(obs.get_position(), 1 / 60)
             evs[1].record()
+        else:
+            disk.update(obs.get_position(), 1 / 60, stream=side)
         for i, s in enumerate(spheres):
             s.draw(f, tgt, composite=i > 0)
             if evs:
@@ -105,6 +113,7 @@ def main():
                  "the reference's frame with its commented-out planet and clouds: 3 composited per-pixel geodesic "
                  "spheres + accretion disk (orbits, 2 x RayConnector, point draws)"),
         "spheres": len(spheres),
+        "overlap": bool(args.overlap),
         "width": w, "height": h, "frames": args.frames, "points": args.points, "max_steps": args.max_steps,
         "ms_per_frame": wall * 1e3, "frames_per_s": 1.0 / wall,
         "gpu_ms": {k: float(v) for k, v in zip(parts, acc)},

@@ -68,6 +68,26 @@ GEO_HD float sqrtf_(float x) {
 #endif
     return __builtin_sqrtf(x);
 }
+// Correctly rounded reciprocal, equal to 1.0f / x (hipcc's correctly rounded
+// division, ≈ 11 VALU) for every input.  For normal |x| < 2^126 the
+// Markstein step r + r(1 - x r) on the 1-ulp v_rcp_f32 seed is correctly
+// rounded (3 VALU; checked against the builtin for all 2^32 inputs on the GPU,
+// tests/test_gpu_math.py; outside that range the seed's result is denormal,
+// zero or infinite and the step is not exact).  The range test is one
+// v_med3_f32 + compare (NaN fails it); other inputs take the builtin.
+#ifndef GEO_FAST_RCP
+#define GEO_FAST_RCP 1  // 0: the builtin everywhere (A/B switch, tools/gpu_ab.sh)
+#endif
+GEO_HD float rcpf_(float x) {
+#if defined(__HIP_DEVICE_COMPILE__) && GEO_FAST_RCP
+    const float ax = __builtin_fabsf(x);
+    if (__builtin_amdgcn_fmed3f(ax, 0x1p-126f, 0x1.fffffep125f) == ax) {
+        const float r = __builtin_amdgcn_rcpf(x);
+        return __builtin_fmaf(__builtin_fmaf(-x, r, 1.0f), r, r);
+    }
+#endif
+    return 1.0f / x;
+}
 GEO_HD float clampf_(float x, float lo, float hi) { return x < lo ? lo : (x > hi ? hi : x); }
 // max(a, b) with a NaN `a` mapped to b (used to clamp radicands at 0).
 GEO_HD float fmaxf_(float a, float b) { return a > b ? a : b; }

@@ -574,7 +574,7 @@ GEO_HD void pixel_central_dir(const float* m0, const float* m1, float psi_k, flo
     float dx, dy, dz;
     mat3_mul(m0, cx, cy, cz, &dx, &dy, &dz);
     const float len = sqrtf_(fmaf_(dz, dz, fmaf_(dy, dy, dx * dx)));
-    const float id = 1.0f / fmaf_(-psi_k, dz, len);
+    const float id = rcpf_(fmaf_(-psi_k, dz, len));
     const float g = kt * id;
     // to_cart, then movement_to_central (:72-74)
     mat3_mul(m1, dx * g, dy * g, fmaf_(-psi_k, len, dz) * id, c2x, c2y, c2z);

@@ -11,7 +11,9 @@
 // them.  Transcendentals: glam's Vec3::angle_between uses its acos_approx (the
 // DirectXMath XMScalarAcos 7-degree minimax, restated below — the glam source
 // is not in this image, so this is restated from its published form); f32::acos,
-// f32::atan come from geo_math.h (<= 4 ulp from libm).  The oracle
+// f32::atan come from geo_math.h (<= 4 ulp from libm).  Reciprocals 1.0 / x
+// go through rcpf_ (geo_math.h), equal to the IEEE quotient for every input,
+// so the oracle's `1.0f / x` is unchanged.  The oracle
 // (oracle/geo_oracle_points.c) restates the same sequence; tests require bit
 // equality with it, and the reference's own RayConnector tests (tests.rs:15-79,
 // 5e-4 rad) on both.
@@ -60,10 +62,10 @@ GEO_HD float signum_(float x) { return x != x ? x : __builtin_copysignf(1.0f, x)
 GEO_HD float calc_ray_angle(float rs, bool lt180, float u_bar, float r) {
     float theta;
     if (r > rs) {
-        theta = signum_(u_bar) * acosf_(__builtin_sqrtf(1.0f / (1.0f + (r * r * u_bar * u_bar) / (1.0f - rs / r))));
+        theta = signum_(u_bar) * acosf_(__builtin_sqrtf(rcpf_(1.0f + (r * r * u_bar * u_bar) / (1.0f - rs / r))));
     } else {
         const float inter = -(r * r * u_bar * u_bar) / (1.0f - rs / r) - 1.0f;
-        theta = inter > 0.0f ? -kPi2 + atanf_(__builtin_sqrtf(1.0f / inter)) : 0.0f;
+        theta = inter > 0.0f ? -kPi2 + atanf_(__builtin_sqrtf(rcpf_(inter))) : 0.0f;
     }
     return (kPi2 - theta) * (lt180 ? 1.0f : -1.0f);
 }
@@ -83,14 +85,14 @@ GEO_HD float ray_connect(float rs, bool lt180, float px, float py, float pz, flo
     bool do_reset = reset || *needs_reset;
     if (!do_reset && !(phi < kSmallestAngle)) {
         // the jump test of update_ray (:82-84)
-        const float u0 = 1.0f / len3_(ox, oy, oz);
-        if (__builtin_fabsf(1.0f / u0 - 1.0f / load(0)) > 0.5f) do_reset = true;
+        const float u0 = rcpf_(len3_(ox, oy, oz));
+        if (__builtin_fabsf(rcpf_(u0) - rcpf_(load(0))) > 0.5f) do_reset = true;
     }
     if (do_reset) {
         // reset_ray (:28-40): linear initial guess between the two ends
         *needs_reset = false;
-        const float u0 = 1.0f / len3_(ox, oy, oz);
-        const float u1 = 1.0f / len3_(px, py, pz);
+        const float u0 = rcpf_(len3_(ox, oy, oz));
+        const float u1 = rcpf_(len3_(px, py, pz));
 #pragma unroll
         for (int i = 0; i < kRayNodes; ++i) {
             const float w = (float)i / (float)(kRayNodes - 1);
@@ -104,14 +106,14 @@ GEO_HD float ray_connect(float rs, bool lt180, float px, float py, float pz, flo
         // nearly straight ray (:61-76): no solve; reset on the next call
         *needs_reset = true;
         if (phi == 0.0f) return len3_(ox, oy, oz) > len3_(px, py, pz) ? 0.0f : kPi;
-        const float u0 = 1.0f / len3_(ox, oy, oz);
+        const float u0 = rcpf_(len3_(ox, oy, oz));
         const float u_bar =
-            (1.0f / len3_(px, py, pz) - u0) / phi - phi / 2.0f * (-u0 + 1.5f * rs * u0 * u0);
-        return calc_ray_angle(rs, lt180, u_bar, 1.0f / u0);
+            (rcpf_(len3_(px, py, pz)) - u0) / phi - phi / 2.0f * (-u0 + 1.5f * rs * u0 * u0);
+        return calc_ray_angle(rs, lt180, u_bar, rcpf_(u0));
     }
     // update_ray (:78-131); after a reset the end deltas are exactly 0
-    const float u0 = 1.0f / len3_(ox, oy, oz);
-    const float u1 = 1.0f / len3_(px, py, pz);
+    const float u0 = rcpf_(len3_(ox, oy, oz));
+    const float u1 = rcpf_(len3_(px, py, pz));
     const float u0_delta = u0 - u[0];
     const float u1_delta = u1 - u[kRayNodes - 1];
 #pragma unroll
@@ -123,19 +125,19 @@ GEO_HD float ray_connect(float rs, bool lt180, float px, float py, float pz, flo
     // differences, fixed ends), each step one tridiagonal solve (Thomas;
     // off-diagonals all -scale) (:94-126)
     const float h = phi / (float)(kRayNodes - 1);
-    const float scale = 1.0f / (h * h);
+    const float scale = rcpf_(h * h);
     const uint32_t iters = do_reset ? (uint32_t)kResetIterations : iterations;
     float res[kRayNodes - 2], tc[kRayNodes - 2];
     for (uint32_t k = 0; k < iters; ++k) {
 #pragma unroll
         for (int i = 1; i < kRayNodes - 1; ++i)
             res[i - 1] = scale * (-u[i - 1] + 2.0f * u[i] - u[i + 1]) - u[i] + 3.0f * rs / 2.0f * u[i] * u[i];
-        float mdi = 1.0f / (2.0f * scale - 1.0f + 3.0f * rs * u[1]);
+        float mdi = rcpf_(2.0f * scale - 1.0f + 3.0f * rs * u[1]);
         tc[0] = (-scale) * mdi;
         res[0] = res[0] * mdi;
 #pragma unroll
         for (int i = 1; i < kRayNodes - 2; ++i) {
-            mdi = 1.0f / (2.0f * scale - 1.0f + 3.0f * rs * u[i + 1] + scale * tc[i - 1]);
+            mdi = rcpf_(2.0f * scale - 1.0f + 3.0f * rs * u[i + 1] + scale * tc[i - 1]);
             tc[i] = (-scale) * mdi;
             res[i] = (res[i] + scale * res[i - 1]) * mdi;
         }
@@ -148,7 +150,7 @@ GEO_HD float ray_connect(float rs, bool lt180, float px, float py, float pz, flo
     }
     // incoming angle from the second-order one-sided derivative at node 0 (:129-130)
     const float u_bar = (u[1] - u[0]) / h - h / 2.0f * (-u[0] + 1.5f * rs * u[0] * u[0]);
-    return calc_ray_angle(rs, lt180, u_bar, 1.0f / u0);
+    return calc_ray_angle(rs, lt180, u_bar, rcpf_(u0));
 }
 
 // vs_main (shader.wgsl:36-68) for the vertex (x, y, z, incoming angle):

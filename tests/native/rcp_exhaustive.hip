@@ -1,0 +1,36 @@
+// geo::rcpf_ (geo_math.h) against 1.0f / x (hipcc's correctly rounded
+// division) for all 2^32 f32 bit patterns, on the GPU.  Prints
+// "mismatches N" and the first few differing inputs; exit status 0 iff N == 0.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+
+#include "../../schwarzschild_raytracer_wgpu_amd/csrc/geo_math.h"
+
+__global__ __launch_bounds__(256) void check(unsigned long long* bad, uint32_t* first) {
+    const uint64_t stride = (uint64_t)gridDim.x * 256u;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x; i < (1ull << 32); i += stride) {
+        const float x = __builtin_bit_cast(float, (uint32_t)i);
+        const uint32_t a = __builtin_bit_cast(uint32_t, geo::rcpf_(x));
+        const uint32_t b = __builtin_bit_cast(uint32_t, 1.0f / x);
+        if (a != b) {
+            const unsigned long long n = atomicAdd(bad, 1ull);
+            if (n < 8) first[n] = (uint32_t)i;
+        }
+    }
+}
+
+int main() {
+    unsigned long long* bad;
+    uint32_t* first;
+    if (hipMalloc(&bad, 8) != hipSuccess || hipMalloc(&first, 32) != hipSuccess) return 2;
+    hipMemset(bad, 0, 8);
+    hipLaunchKernelGGL(check, dim3(256 * 64), dim3(256), 0, 0, bad, first);
+    unsigned long long n = 0;
+    uint32_t f[8] = {0};
+    if (hipMemcpy(&n, bad, 8, hipMemcpyDeviceToHost) != hipSuccess) return 2;
+    hipMemcpy(f, first, 32, hipMemcpyDeviceToHost);
+    printf("mismatches %llu\n", n);
+    for (unsigned long long i = 0; i < n && i < 8; ++i) printf("  x = 0x%08x\n", f[i]);
+    return n == 0 ? 0 : 1;
+}

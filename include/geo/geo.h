@@ -126,7 +126,9 @@ void geo_ctx_destroy(geo_ctx* ctx);
 
 /* Uploads an equirect RGBA8 sky (row-major, w*h*4 bytes, host memory; the
  * bytes are copied, synchronously).  U wraps, V clamps, LOD-0 bilinear with
- * 8-bit sub-texel weights. */
+ * 8-bit sub-texel weights.  The device keeps a copy padded by one texel on
+ * every side, which must stay below 2^31 bytes: (w + 2) * (h + 2) * 4 < 2^31,
+ * w, h <= 2^20 (GEO_EINVAL otherwise). */
 int geo_set_sky(geo_ctx* ctx, const uint8_t* rgba8, uint32_t w, uint32_t h);
 
 /* Uploads a ray fan of n >= 2 nodes (host memory, copied synchronously):

@@ -617,9 +617,8 @@ GEO_HD void sky_uv(const float* m2, float c2x, float c2y, float rho, float lam, 
     *V = clampf_(v, 0.0f, 1.0f);
 }
 
-// LOD-0 bilinear sample of an RGBA8 equirect (U wraps, V clamps) with 8-bit
-// sub-texel weights, as texture units do, on packed channel pairs
-// (R|B and G|A in the two 16-bit halves of a u32; no field overflows).
+// Packed channel pairs of the bilinear sample: R|B and G|A in the two 16-bit
+// halves of a u32 (no field overflows).
 GEO_HD uint32_t rb_(uint32_t t) { return t & 0x00FF00FFu; }
 GEO_HD uint32_t ga_(uint32_t t) { return (t >> 8) & 0x00FF00FFu; }
 // Operands < 2^24 (packed pairs <= 0x00FF00FF, weights <= 256): the 24-bit
@@ -642,28 +641,61 @@ GEO_HD uint32_t div255_(uint32_t v) {  // round(v / 255) for v <= 255 * 255
 }
 GEO_HD uint32_t blend255_(uint32_t c, uint32_t a) { return div255_(c * a); }  // round(c*a/255)
 
+// The texel quad (ix0, iy0), (ix0+1, iy0), (ix0, iy0+1), (ix0+1, iy0+1) of a
+// tw x th equirect, U wrapping and V clamping; ix0 in [-1, tw-1] and iy0 in
+// [-1, th-1] for U, V in [0, 1].  fetch(i): texel i of the row-major texture.
 template <typename Fetch>
-GEO_HD uint32_t sample_sky_raw(Fetch fetch, uint32_t tw, uint32_t th, float U, float V) {
+struct WrapClampQuad {
+    Fetch fetch;
+    uint32_t tw, th;
+    GEO_HDM void operator()(int ix0, int iy0, uint32_t (&t)[4]) const {
+        const int w = (int)tw, h = (int)th;
+        if (ix0 < 0) ix0 += w;
+        if (ix0 >= w) ix0 -= w;
+        const int ix1 = (ix0 + 1 == w) ? 0 : ix0 + 1;
+        int iy1 = iy0 + 1;
+        iy0 = iy0 < 0 ? 0 : (iy0 > h - 1 ? h - 1 : iy0);
+        iy1 = iy1 < 0 ? 0 : (iy1 > h - 1 ? h - 1 : iy1);
+        const uint32_t r0 = (uint32_t)iy0 * tw, r1 = (uint32_t)iy1 * tw;
+        t[0] = fetch(r0 + (uint32_t)ix0);
+        t[1] = fetch(r0 + (uint32_t)ix1);
+        t[2] = fetch(r1 + (uint32_t)ix0);
+        t[3] = fetch(r1 + (uint32_t)ix1);
+    }
+};
+
+// The padded copy of a tw x th equirect the device samples: (tw + 2) x (th + 2)
+// texels, texel (x, y) of the texture at padded (x + 1, y + 1), column -1 =
+// column tw - 1 and column tw = column 0 (U wraps), row -1 = row 0 and row th =
+// row th - 1 (V clamps).  Every quad WrapClampQuad reads for U, V in [0, 1] is
+// then the plain 2 x 2 block at padded index (iy0 + 1) (tw + 2) + ix0 + 1: no
+// wrap or clamp logic, and on the device the four loads share one offset.
+GEO_HD void pad_sky(const uint32_t* src, uint32_t tw, uint32_t th, uint32_t* dst) {
+    const uint32_t pw = tw + 2u;
+    for (uint32_t py = 0; py < th + 2u; ++py) {
+        const uint32_t y = py == 0u ? 0u : (py > th ? th - 1u : py - 1u);
+        const uint32_t* row = src + (size_t)y * tw;
+        uint32_t* out = dst + (size_t)py * pw;
+        out[0] = row[tw - 1u];
+        for (uint32_t x = 0; x < tw; ++x) out[x + 1u] = row[x];
+        out[tw + 1u] = row[0];
+    }
+}
+
+// LOD-0 bilinear sample of an RGBA8 equirect (U wraps, V clamps) with 8-bit
+// sub-texel weights, as texture units do, on packed channel pairs; quad(ix0,
+// iy0, t) supplies the texel quad (WrapClampQuad, or a padded-copy reader).
+template <typename Quad>
+GEO_HD uint32_t sample_sky_quad(const Quad& quad, uint32_t tw, uint32_t th, float U, float V) {
     const float x = fmaf_(U, (float)tw, -0.5f);
     const float y = fmaf_(V, (float)th, -0.5f);
     const float fx0 = __builtin_floorf(x);
     const float fy0 = __builtin_floorf(y);
     const uint32_t wx = (uint32_t)((x - fx0) * 256.0f);  // 0..255
     const uint32_t wy = (uint32_t)((y - fy0) * 256.0f);
-    int ix0 = (int)fx0;
-    int iy0 = (int)fy0;
-    const int w = (int)tw, h = (int)th;
-    if (ix0 < 0) ix0 += w;
-    if (ix0 >= w) ix0 -= w;
-    const int ix1 = (ix0 + 1 == w) ? 0 : ix0 + 1;
-    int iy1 = iy0 + 1;
-    iy0 = iy0 < 0 ? 0 : (iy0 > h - 1 ? h - 1 : iy0);
-    iy1 = iy1 < 0 ? 0 : (iy1 > h - 1 ? h - 1 : iy1);
-    const uint32_t r0 = (uint32_t)iy0 * tw, r1 = (uint32_t)iy1 * tw;
-    const uint32_t t00 = fetch(r0 + (uint32_t)ix0);
-    const uint32_t t10 = fetch(r0 + (uint32_t)ix1);
-    const uint32_t t01 = fetch(r1 + (uint32_t)ix0);
-    const uint32_t t11 = fetch(r1 + (uint32_t)ix1);
+    uint32_t t[4];
+    quad((int)fx0, (int)fy0, t);
+    const uint32_t t00 = t[0], t10 = t[1], t01 = t[2], t11 = t[3];
     const uint32_t iwx = 256u - wx, iwy = 256u - wy;
     // horizontal (fields <= 255*256), truncated to 8 bits, then vertical, rounded
     const uint32_t trb = (lerp2_(rb_(t00), rb_(t10), iwx, wx) >> 8) & 0x00FF00FFu;
@@ -673,6 +705,11 @@ GEO_HD uint32_t sample_sky_raw(Fetch fetch, uint32_t tw, uint32_t th, float U, f
     const uint32_t crb = ((lerp2_(trb, brb, iwy, wy) + 0x00800080u) >> 8) & 0x00FF00FFu;
     const uint32_t cga = ((lerp2_(tga, bga, iwy, wy) + 0x00800080u) >> 8) & 0x00FF00FFu;
     return crb | (cga << 8);
+}
+
+template <typename Fetch>
+GEO_HD uint32_t sample_sky_raw(Fetch fetch, uint32_t tw, uint32_t th, float U, float V) {
+    return sample_sky_quad(WrapClampQuad<Fetch>{fetch, tw, th}, tw, th, U, V);
 }
 
 // The reference's alpha blend (BlendState::ALPHA_BLENDING, pipeline.rs:49) in
@@ -690,13 +727,17 @@ GEO_HD uint32_t composite_(uint32_t s, uint32_t d) {
 // A sample over the cleared target (0,0,0,1) (renderer.rs:233-238): rgb*a/255,
 // alpha 1.  `opaque` (every texel alpha 255, checked on upload) skips the
 // blend, which is exact there.
-template <typename Fetch>
-GEO_HD uint32_t sample_sky(Fetch fetch, uint32_t tw, uint32_t th, bool opaque, float U, float V) {
-    const uint32_t s = sample_sky_raw(fetch, tw, th, U, V);
+template <typename Quad>
+GEO_HD uint32_t sample_sky_q(const Quad& quad, uint32_t tw, uint32_t th, bool opaque, float U, float V) {
+    const uint32_t s = sample_sky_quad(quad, tw, th, U, V);
     if (opaque) return s | 0xFF000000u;
     const uint32_t a = s >> 24;
     return blend255_(s & 0xFFu, a) | (blend255_((s >> 8) & 0xFFu, a) << 8) |
            (blend255_((s >> 16) & 0xFFu, a) << 16) | 0xFF000000u;
+}
+template <typename Fetch>
+GEO_HD uint32_t sample_sky(Fetch fetch, uint32_t tw, uint32_t th, bool opaque, float U, float V) {
+    return sample_sky_q(WrapClampQuad<Fetch>{fetch, tw, th}, tw, th, opaque, U, V);
 }
 
 constexpr uint32_t kBlackRGBA = 0xFF000000u;  // clear colour (0,0,0,1), renderer.rs:233-238

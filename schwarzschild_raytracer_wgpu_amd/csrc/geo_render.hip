@@ -19,6 +19,7 @@
 #include <cstring>
 #include <new>
 #include <type_traits>
+#include <vector>
 
 #include "../../include/geo/geo.h"
 #include "geo_ctx.h"
@@ -51,8 +52,9 @@ struct RenderArgs {
     uint32_t sky_opaque;
     uint32_t composite;  // GEO_FLAG_COMPOSITE
     float inv_w, inv_h, kt;
-    const uint32_t* sky;
+    const uint32_t* sky;  // padded (geo::pad_sky): (sky_w + 2) x (sky_h + 2) texels
     uint32_t sky_w, sky_h;
+    uint32_t sky_pitch_b, sky_bytes;
     const float* fan;
     uint32_t n_fan;
     uint32_t* out_rgba;
@@ -75,6 +77,26 @@ __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
     v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);  // row_bcast:31
     return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
 }
+
+// The texel quad from the context's padded sky (geo::pad_sky): the 2 x 2 block
+// at padded texel (ix0 + 1, iy0 + 1), by four buffer loads from one 32-bit
+// byte offset (one v_mad_u32_u24): +4 B for the right column as the immediate
+// offset, +pitch for the lower row as the scalar offset.  Against the wrap/clamp
+// quad on the unpadded texture this drops the wrap and clamp selects, the
+// quarter-rate v_mul_lo_u32 row products and the 64-bit address adds; the
+// texels are the same (geo_set_sky limits the padded sky to < 2^31 bytes).
+constexpr int kBufferRsrcWord3 = 0x00020000;  // gfx9 buffer resource: raw 32-bit dwords
+struct PaddedSkyQuad {
+    __amdgpu_buffer_rsrc_t rsrc;
+    uint32_t pitch_b;  // bytes per padded row, (sky_w + 2) * 4
+    __device__ __forceinline__ void operator()(int ix0, int iy0, uint32_t (&t)[4]) const {
+        const uint32_t off = __umul24((uint32_t)(iy0 + 1), pitch_b) + ((uint32_t)(ix0 + 1) << 2);
+        t[0] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rsrc, off, 0, 0);
+        t[1] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rsrc, off + 4u, 0, 0);
+        t[2] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rsrc, off, (int)pitch_b, 0);
+        t[3] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rsrc, off + 4u, (int)pitch_b, 0);
+    }
+};
 
 template <int MODE, int KIND>
 __global__ __launch_bounds__(kBlock) void geo_render_kernel(const RenderArgs a) {
@@ -116,17 +138,18 @@ __global__ __launch_bounds__(kBlock) void geo_render_kernel(const RenderArgs a) 
         if (!bh || a.out_uv)
 #endif
             geo::sky_uv(a.frame.central_to_uv, c2x, c2y, ct, lam, &U, &V);
-        const uint32_t* sky = a.sky;
-        auto fetch = [sky](uint32_t i) { return sky[i]; };
+        const PaddedSkyQuad quad{__builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(a.sky), 0,
+                                                                   (int)a.sky_bytes, kBufferRsrcWord3),
+                                 a.sky_pitch_b};
         const size_t o = (size_t)ly * a.width + px;
         if (a.composite) {
             // over the previous spheres; a discarded pixel keeps the target
             if (!bh) {
-                const uint32_t s = geo::sample_sky_raw(fetch, a.sky_w, a.sky_h, U, V);
+                const uint32_t s = geo::sample_sky_quad(quad, a.sky_w, a.sky_h, U, V);
                 a.out_rgba[o] = a.sky_opaque ? s : geo::composite_(s, a.out_rgba[o]);
             }
         } else {
-            a.out_rgba[o] = bh ? geo::kBlackRGBA : geo::sample_sky(fetch, a.sky_w, a.sky_h, a.sky_opaque != 0, U, V);
+            a.out_rgba[o] = bh ? geo::kBlackRGBA : geo::sample_sky_q(quad, a.sky_w, a.sky_h, a.sky_opaque != 0, U, V);
         }
         if (a.out_mask) a.out_mask[o] = bh ? 1 : 0;
         if (a.out_uv) a.out_uv[o] = make_float2(U, V);
@@ -434,19 +457,26 @@ void geo_ctx_destroy(geo_ctx* c) {
 }
 
 int geo_set_sky(geo_ctx* c, const uint8_t* rgba8, uint32_t w, uint32_t h) {
-    if (!c || !rgba8 || w == 0 || h == 0 || (uint64_t)w * h > (1ull << 31)) return GEO_EINVAL;
+    // the padded copy must stay below 2^31 bytes (32-bit buffer offsets, PaddedSkyQuad)
+    if (!c || !rgba8 || w == 0 || h == 0 || w > (1u << 20) || h > (1u << 20) ||
+        ((uint64_t)w + 2u) * ((uint64_t)h + 2u) * 4u >= (1ull << 31))
+        return GEO_EINVAL;
     DeviceGuard g(c->device);
     if (!g.ok) return GEO_EHIP;
     const size_t bytes = (size_t)w * h * 4;
-    if (c->sky && (uint64_t)c->sky_w * c->sky_h != (uint64_t)w * h) {
+    const size_t padded = ((size_t)w + 2u) * ((size_t)h + 2u);
+    if (c->sky && ((size_t)c->sky_w + 2u) * ((size_t)c->sky_h + 2u) != padded) {
         (void)hipFree(c->sky);
         c->sky = nullptr;
     }
-    if (!c->sky && hipMalloc(&c->sky, bytes) != hipSuccess) {
+    if (!c->sky && hipMalloc(&c->sky, padded * 4u) != hipSuccess) {
         c->sky = nullptr;
         return GEO_ENOMEM;
     }
-    if (hipMemcpy(c->sky, rgba8, bytes, hipMemcpyHostToDevice) != hipSuccess) return GEO_EHIP;
+    std::vector<uint32_t> src((size_t)w * h), pad(padded);
+    std::memcpy(src.data(), rgba8, bytes);
+    geo::pad_sky(src.data(), w, h, pad.data());
+    if (hipMemcpy(c->sky, pad.data(), padded * 4u, hipMemcpyHostToDevice) != hipSuccess) return GEO_EHIP;
     c->sky_w = w;
     c->sky_h = h;
     bool opaque = true;
@@ -537,6 +567,8 @@ static int render_impl(geo_ctx* c, const geo_frame* frame, const geo_scene* scen
     a.sky = c->sky;
     a.sky_w = c->sky_w;
     a.sky_h = c->sky_h;
+    a.sky_pitch_b = (c->sky_w + 2u) * 4u;
+    a.sky_bytes = a.sky_pitch_b * (c->sky_h + 2u);
     a.fan = c->fan;
     a.n_fan = c->n_fan;
     a.out_rgba = reinterpret_cast<uint32_t*>(out_rgba8);

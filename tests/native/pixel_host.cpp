@@ -69,3 +69,27 @@ extern "C" int host_render(const geo_frame* f, const geo_scene* s, const float* 
     }
     return 0;
 }
+
+// geo::pad_sky + the padded 2 x 2 block (what the device's PaddedSkyQuad reads)
+// against WrapClampQuad on the unpadded texture: the sampled RGBA of n (U, V)
+// pairs both ways.
+extern "C" int host_sample_padded(const uint32_t* sky, uint32_t sw, uint32_t sh, const float* U, const float* V,
+                                  uint32_t n, uint32_t* out_wrap, uint32_t* out_pad) {
+    uint32_t* pad = new uint32_t[((size_t)sw + 2) * ((size_t)sh + 2)];
+    geo::pad_sky(sky, sw, sh, pad);
+    const uint32_t pitch = sw + 2u;
+    auto padded = [pad, pitch](int ix0, int iy0, uint32_t (&t)[4]) {
+        const size_t i = (size_t)(iy0 + 1) * pitch + (size_t)(ix0 + 1);
+        t[0] = pad[i];
+        t[1] = pad[i + 1];
+        t[2] = pad[i + pitch];
+        t[3] = pad[i + pitch + 1];
+    };
+    auto fetch = [sky](uint32_t i) { return sky[i]; };
+    for (uint32_t i = 0; i < n; ++i) {
+        out_wrap[i] = geo::sample_sky_raw(fetch, sw, sh, U[i], V[i]);
+        out_pad[i] = geo::sample_sky_quad(padded, sw, sh, U[i], V[i]);
+    }
+    delete[] pad;
+    return 0;
+}

@@ -329,6 +329,10 @@ def test_invalid_arguments(geo, torch_mod):
     st = _lib.lib.geo_render_rows(ctx._h, ctypes.byref(frame), ctypes.byref(scene), 8, 8, 0, 8, out.data_ptr(),
                                   None, None, None, None, None)
     assert st == _lib.GEO_ESTATE
+    # a sky whose padded device copy would reach 2^31 bytes, or wider than 2^20
+    dummy = np.zeros(4, np.uint8)
+    for w, h in ((1 << 20) + 1, 1), (1, (1 << 20) + 1), (32766, 16384):
+        assert _lib.lib.geo_set_sky(ctx._h, dummy.ctypes.data, w, h) == _lib.GEO_EINVAL
     ctx.set_sky(np.zeros((1, 1, 4), np.uint8))
     # rows out of range
     st = _lib.lib.geo_render_rows(ctx._h, ctypes.byref(frame), ctypes.byref(scene), 8, 8, 4, 5, out.data_ptr(),

@@ -189,3 +189,22 @@ def test_composite_over_clear_equals_plain_draw():
     comp = O.render_f32(frame, make_scene(1.0, 50.0, r, math.pi / 100, 512, flags=GEO_FLAG_COMPOSITE), sky, w, h,
                         target=clear)
     assert np.array_equal(plain["rgba"], comp["rgba"])
+
+
+@pytest.mark.parametrize("sw,sh", [(1, 1), (2, 1), (7, 5), (64, 32), (513, 257)])
+def test_padded_sky_quad_equals_wrap_clamp(host, sw, sh):
+    """The device's sky sampling reads a padded copy (geo::pad_sky, 2 x 2 block
+    at (ix0 + 1, iy0 + 1)); it must sample exactly what the wrap/clamp quad on
+    the unpadded texture does: random (U, V), the edges and corners, and the
+    texel centres next to them."""
+    rng = np.random.default_rng(sw * 1000 + sh)
+    sky = rng.integers(0, 2**32, size=(sh, sw), dtype=np.uint64).astype(np.uint32)
+    edge = np.array([0.0, 1.0, 0.5 / sw, 1 - 0.5 / sw, 1e-7, 1 - 1e-7, 0.5, np.nextafter(1.0, 0.0)], np.float32)
+    U = np.concatenate([rng.random(4000, dtype=np.float32), np.repeat(edge, edge.size)]).astype(np.float32)
+    V = np.concatenate([rng.random(4000, dtype=np.float32), np.tile(edge, edge.size)]).astype(np.float32)
+    a = np.empty(U.size, np.uint32)
+    b = np.empty(U.size, np.uint32)
+    vp = ctypes.c_void_p
+    host.host_sample_padded(vp(sky.ctypes.data), ctypes.c_uint32(sw), ctypes.c_uint32(sh), vp(U.ctypes.data),
+                            vp(V.ctypes.data), ctypes.c_uint32(U.size), vp(a.ctypes.data), vp(b.ctypes.data))
+    assert np.array_equal(a, b)

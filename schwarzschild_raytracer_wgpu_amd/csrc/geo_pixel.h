@@ -24,6 +24,12 @@
 #define GEO_ABSORBING_TEST 1
 #endif
 
+// 1: the RK4 loop's frame constants held in VGPRs (geodesic_angle_v);
+// 0: left to the compiler, which keeps them in SGPRs (A/B switch)
+#ifndef GEO_VGPR_CONSTS
+#define GEO_VGPR_CONSTS 1
+#endif
+
 namespace geo {
 
 constexpr float kNoValue = 15.0f;          // SphereRayTracer::NO_VALUE, sphere_ray_tracer.rs:22
@@ -358,11 +364,24 @@ GEO_HD float geodesic_angle_v(const PixelConsts& k, float st, float ct, uint32_t
     float U, UB, early;
     if (!geodesic_init(k, st, ct, &early, &U, &UB)) return early;
     const float SU = k.SU;
-    const float h = k.step, hh = k.hh, hh2 = k.hh2, hhh = k.hhh, h6 = k.h6, h2_6 = k.h2_6;
+    float h = k.step, hh = k.hh, hh2 = k.hh2, hhh = k.hhh, h6 = k.h6, h2_6 = k.h2_6;
     // Main loop (:134-191), restructured for the wave64 VALU: per step the
     // lane-exit flag is StopTest (crossing | escape | horizon); the budget
     // (:135) is wave-uniform.
-    const StopTest<KIND> stop_at(k);
+    StopTest<KIND> stop_at(k);
+#if GEO_VGPR_CONSTS
+    // The loop's frame constants in VGPRs: on gfx950 a VALU op that reads an
+    // SGPR issues at about half the rate of an all-VGPR one
+    // (tools/ubench/op_rates.hip), and 6 of the step's 14 ops read one.
+    GEO_OPAQUE(h);
+    GEO_OPAQUE(hh);
+    GEO_OPAQUE(hh2);
+    GEO_OPAQUE(hhh);
+    GEO_OPAQUE(h6);
+    GEO_OPAQUE(h2_6);
+    GEO_OPAQUE(stop_at.lo);
+    GEO_OPAQUE(stop_at.hi);
+#endif
     // LOOP = G: G RK4 steps per exit test (the budget in whole groups is a
     // wave-uniform bound); a lane that stops inside a group discards the rest
     // of it.  Results equal the literal loop's (the oracle keeps that form;

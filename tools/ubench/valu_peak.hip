@@ -1,6 +1,9 @@
 // Microbenchmark: sustained FP32 VALU throughput on gfx950 for
 //   v_fma_f32 (scalar), v_pk_fma_f32 (2 x f32 per lane), and the
 // dependent-chain latency, to calibrate the roofline of geo_render_kernel.
+// CAUTION: built without -fno-slp-vectorize, hipcc packs fma_scalar's
+// independent chains into v_pk_fma_f32 too, so both kernels measure packed
+// code; tools/ubench/op_rates.hip pins the opcodes with inline asm.
 #include <hip/hip_runtime.h>
 #include <cstdio>
 

@@ -252,6 +252,17 @@ __global__ __launch_bounds__(256) void k_pkfma2(float* out, int iters, float a) 
     for (int c = 0; c < 8; ++c) s += x[c].x + x[c].y;
     if (s == 12345.f) out[threadIdx.x] = s;
 }
+__global__ __launch_bounds__(256) void k_fma_alt(float* out, int iters, float a) {
+    float x[16];
+#pragma unroll
+    for (int c = 0; c < 16; ++c) x[c] = threadIdx.x * 1e-3f + c + 1.0f;
+    for (int i = 0; i < iters; ++i)
+        asm volatile("v_fma_f32 %0, %0, %16, %0\nv_fma_f32 %1, %2, %2, %1\nv_fma_f32 %2, %2, %16, %2\nv_fma_f32 %3, %4, %4, %3\nv_fma_f32 %4, %4, %16, %4\nv_fma_f32 %5, %6, %6, %5\nv_fma_f32 %6, %6, %16, %6\nv_fma_f32 %7, %8, %8, %7\nv_fma_f32 %8, %8, %16, %8\nv_fma_f32 %9, %10, %10, %9\nv_fma_f32 %10, %10, %16, %10\nv_fma_f32 %11, %12, %12, %11\nv_fma_f32 %12, %12, %16, %12\nv_fma_f32 %13, %14, %14, %13\nv_fma_f32 %14, %14, %16, %14\nv_fma_f32 %15, %0, %0, %15" : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(x[4]), "+v"(x[5]), "+v"(x[6]), "+v"(x[7]), "+v"(x[8]), "+v"(x[9]), "+v"(x[10]), "+v"(x[11]), "+v"(x[12]), "+v"(x[13]), "+v"(x[14]), "+v"(x[15]) : "s"(a) : "vcc");
+    float s = 0;
+#pragma unroll
+    for (int c = 0; c < 16; ++c) s += x[c];
+    if (s == 12345.f) out[threadIdx.x] = s;
+}
 template <typename K>
 float run(K k, int blocks, int iters) {
     float* out;
@@ -292,6 +303,7 @@ int main() {
         {"v_fma_f32 d, s, v_other, d", k_fma2, 16},
         {"v_fma_f32 d, v_o, v_o, d", k_fma3, 16},
         {"v_pk_fma_f32 d, v_o, v_o, d", k_pkfma2, 8},
+        {"alternating SGPR / all-VGPR fma", k_fma_alt, 16},
         {"v_fmac_f32", k_fmac, 16},
         {"v_add_f32", k_add, 16},
         {"v_mul_f32", k_mul, 16},

@@ -689,15 +689,16 @@ struct WrapClampQuad {
 // row th - 1 (V clamps).  Every quad WrapClampQuad reads for U, V in [0, 1] is
 // then the plain 2 x 2 block at padded index (iy0 + 1) (tw + 2) + ix0 + 1: no
 // wrap or clamp logic, and on the device the four loads share one offset.
-GEO_HD void pad_sky(const uint32_t* src, uint32_t tw, uint32_t th, uint32_t* dst) {
+// rgba8: the row-major texture, 4 bytes per texel (any alignment).
+GEO_HD void pad_sky(const uint8_t* rgba8, uint32_t tw, uint32_t th, uint32_t* dst) {
     const uint32_t pw = tw + 2u;
     for (uint32_t py = 0; py < th + 2u; ++py) {
         const uint32_t y = py == 0u ? 0u : (py > th ? th - 1u : py - 1u);
-        const uint32_t* row = src + (size_t)y * tw;
+        const uint8_t* row = rgba8 + (size_t)y * tw * 4u;
         uint32_t* out = dst + (size_t)py * pw;
-        out[0] = row[tw - 1u];
-        for (uint32_t x = 0; x < tw; ++x) out[x + 1u] = row[x];
-        out[tw + 1u] = row[0];
+        __builtin_memcpy(out + 1, row, (size_t)tw * 4u);
+        out[0] = out[tw];       // column tw - 1
+        out[tw + 1u] = out[1];  // column 0
     }
 }
 

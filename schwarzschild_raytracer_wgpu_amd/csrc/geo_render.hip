@@ -473,9 +473,8 @@ int geo_set_sky(geo_ctx* c, const uint8_t* rgba8, uint32_t w, uint32_t h) {
         c->sky = nullptr;
         return GEO_ENOMEM;
     }
-    std::vector<uint32_t> src((size_t)w * h), pad(padded);
-    std::memcpy(src.data(), rgba8, bytes);
-    geo::pad_sky(src.data(), w, h, pad.data());
+    std::vector<uint32_t> pad(padded);
+    geo::pad_sky(rgba8, w, h, pad.data());
     if (hipMemcpy(c->sky, pad.data(), padded * 4u, hipMemcpyHostToDevice) != hipSuccess) return GEO_EHIP;
     c->sky_w = w;
     c->sky_h = h;

@@ -76,7 +76,7 @@ extern "C" int host_render(const geo_frame* f, const geo_scene* s, const float* 
 extern "C" int host_sample_padded(const uint32_t* sky, uint32_t sw, uint32_t sh, const float* U, const float* V,
                                   uint32_t n, uint32_t* out_wrap, uint32_t* out_pad) {
     uint32_t* pad = new uint32_t[((size_t)sw + 2) * ((size_t)sh + 2)];
-    geo::pad_sky(sky, sw, sh, pad);
+    geo::pad_sky(reinterpret_cast<const uint8_t*>(sky), sw, sh, pad);
     const uint32_t pitch = sw + 2u;
     auto padded = [pad, pitch](int ix0, int iy0, uint32_t (&t)[4]) {
         const size_t i = (size_t)(iy0 + 1) * pitch + (size_t)(ix0 + 1);

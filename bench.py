@@ -56,10 +56,10 @@ def parse():
     p.add_argument("--frames-per-gather", type=int, default=4,
                    help="N > 1: frames per RCCL gather to rank 0 (amortises the ~34 us host cost of a gather; "
                         "rank 0 reassembles each batch with one geo_assemble_lead launch)")
-    p.add_argument("--rank0-lead", default="auto", choices=["auto", "1", "2", "4"],
+    p.add_argument("--rank0-lead", default="auto", choices=["auto", "1", "2", "3", "4", "6"],
                    help="N > 1: rank 0's band height in 8-row bands per cycle (it renders rows that never cross "
-                        "an xGMI link, so a link-bound present wants it larger); auto = the fastest of 1, 2, 4 "
-                        "measured on the whole pipeline before the timed region")
+                        "an xGMI link, so a link-bound present wants it larger); auto = the fastest of 1, 2, 3, 4, "
+                        "6 measured on the whole pipeline before the timed region")
     p.add_argument("--lead-trial-frames", type=int, default=120,
                    help="frames per --rank0-lead auto trial (after a quarter as many warm-up frames)")
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -132,7 +132,7 @@ def main():
     if world == 1:
         leads = [1]
     elif args.rank0_lead == "auto":
-        leads = [1, 2, 4]
+        leads = [1, 2, 3, 4, 6]
     else:
         leads = [int(args.rank0_lead)]
     sf = make_sf(leads[0])

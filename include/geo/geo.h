@@ -181,7 +181,8 @@ int geo_assemble_bands(geo_ctx* ctx, const uint8_t* src, size_t rank_stride, siz
                        uint8_t* dst, void* stream);
 
 /* The general strided band set: bands starting at rows row0, row0+row_stride,
- * ..., nbands of them, each band_rows tall (a power of two >= 8) and clipped
+ * ..., nbands of them, each band_rows tall (a multiple of 8; at most 4096
+ * unless a power of two) and clipped
  * to height; row_stride >= band_rows.  Outputs packed band after band as in
  * geo_render_bands (which is the case row0 = band0*band_rows,
  * row_stride = band_step*band_rows).  Used for the lead layout below, where

@@ -48,7 +48,9 @@ struct RenderArgs {
     geo_frame frame;
     geo::PixelConsts k;  // frame constants, evaluated once on the host (IEEE f32, same bits)
     uint32_t width, height, row0, nrows;
-    uint32_t band_shift, band_stride;  // local row lr -> row0 + (lr>>shift)*band_stride + lr%(1<<shift)
+    // local row lr -> row0 + b*band_stride + (lr - b*band_rows), b = lr / band_rows
+    // = umulhi(lr, band_magic) (band_rows_magic)
+    uint32_t band_rows, band_magic, band_stride;
     uint32_t sky_opaque;
     uint32_t composite;  // GEO_FLAG_COMPOSITE
     float inv_w, inv_h, kt;
@@ -107,12 +109,13 @@ __global__ __launch_bounds__(kBlock) void geo_render_kernel(const RenderArgs a) 
     }
     const uint32_t px = blockIdx.x * kTileW + (threadIdx.x % kTileW);
     const uint32_t ly = blockIdx.y * kTileH + (threadIdx.x / kTileW);
-    // local row -> frame row.  band_rows is a power of two >= 8 (checked on the
-    // host): each 8-row wave lies in one band and the mapping is wave-uniform.
+    // local row -> frame row.  band_rows is a multiple of 8 (checked on the
+    // host): each 8-row wave lies in one band and the mapping is wave-uniform
+    // (scalar ops; the band index by a multiply-high, band_rows_magic).
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x) >> 6;
     const uint32_t wl0 = blockIdx.y * kTileH + wave * kWaveRows;
-    const uint32_t py = a.row0 + (wl0 >> a.band_shift) * a.band_stride + (wl0 & ((1u << a.band_shift) - 1u)) +
-                        (ly - wl0);
+    const uint32_t band = __umulhi(wl0, a.band_magic);
+    const uint32_t py = a.row0 + band * a.band_stride + (wl0 - band * a.band_rows) + (ly - wl0);
     uint32_t steps = 0;
     if (px < a.width && ly < a.nrows && py < a.height) {
         float c2x, c2y, c2z;
@@ -526,8 +529,16 @@ int geo_solve_ray_fan(geo_ctx* c, double sphere_r, double schwarz_r, uint32_t ma
     return GEO_OK;
 }
 
+// floor(lr / d) == umulhi(lr, m) for every local row lr < 2^20: d a power of
+// two, m = 2^32 / d exactly; otherwise m = floor(2^32 / d) + 1, whose error
+// lr (m - 2^32/d) / 2^32 < lr / 2^32 stays below 1/d while lr d < 2^32
+// (d <= 4096, checked by the caller).
+static uint32_t band_rows_magic(uint32_t d) {
+    return (d & (d - 1u)) == 0u ? (uint32_t)((1ull << 32) / d) : (uint32_t)((1ull << 32) / d + 1u);
+}
+
 static int render_impl(geo_ctx* c, const geo_frame* frame, const geo_scene* scene, uint32_t width,
-                       uint32_t height, uint32_t row0, uint32_t nrows, uint32_t band_shift,
+                       uint32_t height, uint32_t row0, uint32_t nrows, uint32_t band_rows,
                        uint32_t band_stride, uint8_t* out_rgba8, uint8_t* out_mask, float* out_uv,
                        uint32_t* out_steps, unsigned long long* steps_total, void* stream) {
     if (scene->mode != GEO_MODE_DIRECT && scene->mode != GEO_MODE_FAN && scene->mode != GEO_MODE_ADAPTIVE)
@@ -554,7 +565,8 @@ static int render_impl(geo_ctx* c, const geo_frame* frame, const geo_scene* scen
     a.height = height;
     a.row0 = row0;
     a.nrows = nrows;
-    a.band_shift = band_shift;
+    a.band_rows = band_rows;
+    a.band_magic = band_rows_magic(band_rows);
     a.band_stride = band_stride;
     a.sky_opaque = c->sky_opaque ? 1u : 0u;
     a.composite = (scene->flags & GEO_FLAG_COMPOSITE) ? 1u : 0u;
@@ -718,7 +730,7 @@ int geo_render_rows(geo_ctx* c, const geo_frame* frame, const geo_scene* scene, 
     if ((uint64_t)row0 + nrows > height || width > (1u << 20) || height > (1u << 20))
         return GEO_EINVAL;
     // one band covering every row (2^21 >= nrows)
-    return render_impl(c, frame, scene, width, height, row0, nrows, 21u, 1u << 21, out_rgba8, out_mask,
+    return render_impl(c, frame, scene, width, height, row0, nrows, 1u << 21, 1u << 21, out_rgba8, out_mask,
                        out_uv, out_steps, steps_total, stream);
 }
 
@@ -735,7 +747,7 @@ int geo_render_bands(geo_ctx* c, const geo_frame* frame, const geo_scene* scene,
     const uint64_t nrows = (uint64_t)nbands * band_rows;
     if (first >= height || last >= height || nrows > (1u << 20)) return GEO_EINVAL;
     return render_impl(c, frame, scene, width, height, (uint32_t)first, (uint32_t)nrows,
-                       (uint32_t)__builtin_ctz(band_rows), band_step * band_rows, out_rgba8, out_mask, out_uv,
+                       band_rows, band_step * band_rows, out_rgba8, out_mask, out_uv,
                        out_steps, steps_total, stream);
 }
 
@@ -743,15 +755,17 @@ int geo_render_band_set(geo_ctx* c, const geo_frame* frame, const geo_scene* sce
                         uint32_t height, uint32_t band_rows, uint32_t row0, uint32_t row_stride, uint32_t nbands,
                         uint8_t* out_rgba8, uint8_t* out_mask, float* out_uv, uint32_t* out_steps,
                         unsigned long long* steps_total, void* stream) {
+    // band_rows: a multiple of 8, at most 4096 unless a power of two (band_rows_magic)
     if (!c || !frame || !scene || !out_rgba8 || width == 0 || height == 0 || band_rows == 0 || nbands == 0 ||
-        row_stride < band_rows || band_rows < (uint32_t)kWaveRows || (band_rows & (band_rows - 1)) != 0)
+        row_stride < band_rows || band_rows % (uint32_t)kWaveRows != 0 ||
+        ((band_rows & (band_rows - 1)) != 0 && band_rows > 4096u))
         return GEO_EINVAL;
     if (width > (1u << 20) || height > (1u << 20)) return GEO_EINVAL;
     const uint64_t last = (uint64_t)row0 + (uint64_t)(nbands - 1) * row_stride;
     const uint64_t nrows = (uint64_t)nbands * band_rows;
     if (row0 >= height || last >= height || nrows > (1u << 20)) return GEO_EINVAL;
-    return render_impl(c, frame, scene, width, height, row0, (uint32_t)nrows, (uint32_t)__builtin_ctz(band_rows),
-                       row_stride, out_rgba8, out_mask, out_uv, out_steps, steps_total, stream);
+    return render_impl(c, frame, scene, width, height, row0, (uint32_t)nrows, band_rows, row_stride, out_rgba8,
+                       out_mask, out_uv, out_steps, steps_total, stream);
 }
 
 }  // extern "C"

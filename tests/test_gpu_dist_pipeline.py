@@ -67,7 +67,7 @@ def _peer_bands(ctx, torch, frame, scene, W, H, B, r, world, lead, dev, bpp):
 @pytest.mark.parametrize("S", [1, 2])
 @pytest.mark.parametrize("world,K,nframes,lead", [(2, 4, 41, 1), (3, 3, 10, 1), (8, 4, 16, 1), (8, 1, 5, 1),
                                                   (2, 4, 13, 2), (2, 2, 7, 4), (4, 3, 10, 2), (8, 4, 9, 2),
-                                                  (8, 2, 6, 4)])
+                                                  (8, 2, 6, 4), (2, 3, 8, 3), (8, 4, 9, 3), (4, 2, 5, 6)])
 def test_rank0_pipeline_assembles_frames(world, K, nframes, lead, S, rgb):
     import torch
 
@@ -105,7 +105,7 @@ def test_rank0_pipeline_assembles_frames(world, K, nframes, lead, S, rgb):
         assert torch.equal(sf.frame_rgba(k), ref), k
 
 
-@pytest.mark.parametrize("lead", [1, 2])
+@pytest.mark.parametrize("lead", [1, 2, 3])
 @pytest.mark.parametrize("S", [1, 2])
 def test_peer_rank_pipeline_runs_batches(S, lead):
     """A peer rank (rank 3 of 4): batches of K frames, each sent with one
@@ -159,7 +159,7 @@ def test_peer_rank_pipeline_runs_batches(S, lead):
 
 @pytest.mark.parametrize("W,H,B,world,lead,bpp,nframes", [
     (320, 180, 8, 2, 2, 3, 3), (320, 180, 8, 8, 4, 4, 2), (36, 50, 8, 3, 2, 3, 1), (33, 27, 8, 2, 4, 4, 2),
-    (64, 64, 16, 4, 1, 3, 2), (20, 8, 8, 3, 2, 4, 1)])
+    (64, 64, 16, 4, 1, 3, 2), (20, 8, 8, 3, 2, 4, 1), (320, 180, 8, 8, 3, 3, 2), (36, 50, 8, 2, 6, 4, 1)])
 def test_assemble_lead_matches_host_assembly(W, H, B, world, lead, bpp, nframes):
     """geo_assemble_lead on random bytes == dist.assemble (the host reassembly
     the gloo tests check against the oracle), RGB24 and RGBA8 peers, widths

@@ -263,6 +263,39 @@ __global__ __launch_bounds__(256) void k_fma_alt(float* out, int iters, float a)
     for (int c = 0; c < 16; ++c) s += x[c];
     if (s == 12345.f) out[threadIdx.x] = s;
 }
+__global__ __launch_bounds__(256) void k_lit(float* out, int iters, float a) {
+    float x[16];
+#pragma unroll
+    for (int c = 0; c < 16; ++c) x[c] = threadIdx.x * 1e-3f + c + 1.0f;
+    for (int i = 0; i < iters; ++i)
+        asm volatile("v_fmac_f32 %0, 0x3e99999a, %1\nv_fmac_f32 %1, 0x3f4ccccd, %2\nv_fmac_f32 %2, 0x3e99999a, %3\nv_fmac_f32 %3, 0x3f4ccccd, %4\nv_fmac_f32 %4, 0x3e99999a, %5\nv_fmac_f32 %5, 0x3f4ccccd, %6\nv_fmac_f32 %6, 0x3e99999a, %7\nv_fmac_f32 %7, 0x3f4ccccd, %8\nv_fmac_f32 %8, 0x3e99999a, %9\nv_fmac_f32 %9, 0x3f4ccccd, %10\nv_fmac_f32 %10, 0x3e99999a, %11\nv_fmac_f32 %11, 0x3f4ccccd, %12\nv_fmac_f32 %12, 0x3e99999a, %13\nv_fmac_f32 %13, 0x3f4ccccd, %14\nv_fmac_f32 %14, 0x3e99999a, %15\nv_fmac_f32 %15, 0x3f4ccccd, %0" : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(x[4]), "+v"(x[5]), "+v"(x[6]), "+v"(x[7]), "+v"(x[8]), "+v"(x[9]), "+v"(x[10]), "+v"(x[11]), "+v"(x[12]), "+v"(x[13]), "+v"(x[14]), "+v"(x[15]) : "s"(a) : "vcc");
+    float s = 0;
+#pragma unroll
+    for (int c = 0; c < 16; ++c) s += x[c];
+    if (s == 12345.f) out[threadIdx.x] = s;
+}
+__global__ __launch_bounds__(256) void k_lit_alt(float* out, int iters, float a) {
+    float x[16];
+#pragma unroll
+    for (int c = 0; c < 16; ++c) x[c] = threadIdx.x * 1e-3f + c + 1.0f;
+    for (int i = 0; i < iters; ++i)
+        asm volatile("v_fmac_f32 %0, 0x3e99999a, %1\nv_fma_f32 %1, %2, %2, %1\nv_fmac_f32 %2, 0x3e99999a, %3\nv_fma_f32 %3, %4, %4, %3\nv_fmac_f32 %4, 0x3e99999a, %5\nv_fma_f32 %5, %6, %6, %5\nv_fmac_f32 %6, 0x3e99999a, %7\nv_fma_f32 %7, %8, %8, %7\nv_fmac_f32 %8, 0x3e99999a, %9\nv_fma_f32 %9, %10, %10, %9\nv_fmac_f32 %10, 0x3e99999a, %11\nv_fma_f32 %11, %12, %12, %11\nv_fmac_f32 %12, 0x3e99999a, %13\nv_fma_f32 %13, %14, %14, %13\nv_fmac_f32 %14, 0x3e99999a, %15\nv_fma_f32 %15, %0, %0, %15" : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(x[4]), "+v"(x[5]), "+v"(x[6]), "+v"(x[7]), "+v"(x[8]), "+v"(x[9]), "+v"(x[10]), "+v"(x[11]), "+v"(x[12]), "+v"(x[13]), "+v"(x[14]), "+v"(x[15]) : "s"(a) : "vcc");
+    float s = 0;
+#pragma unroll
+    for (int c = 0; c < 16; ++c) s += x[c];
+    if (s == 12345.f) out[threadIdx.x] = s;
+}
+__global__ __launch_bounds__(256) void k_inl(float* out, int iters, float a) {
+    float x[16];
+#pragma unroll
+    for (int c = 0; c < 16; ++c) x[c] = threadIdx.x * 1e-3f + c + 1.0f;
+    for (int i = 0; i < iters; ++i)
+        asm volatile("v_fmac_f32 %0, 0.5, %1\nv_fmac_f32 %1, 2.0, %2\nv_fmac_f32 %2, 0.5, %3\nv_fmac_f32 %3, 2.0, %4\nv_fmac_f32 %4, 0.5, %5\nv_fmac_f32 %5, 2.0, %6\nv_fmac_f32 %6, 0.5, %7\nv_fmac_f32 %7, 2.0, %8\nv_fmac_f32 %8, 0.5, %9\nv_fmac_f32 %9, 2.0, %10\nv_fmac_f32 %10, 0.5, %11\nv_fmac_f32 %11, 2.0, %12\nv_fmac_f32 %12, 0.5, %13\nv_fmac_f32 %13, 2.0, %14\nv_fmac_f32 %14, 0.5, %15\nv_fmac_f32 %15, 2.0, %0" : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(x[4]), "+v"(x[5]), "+v"(x[6]), "+v"(x[7]), "+v"(x[8]), "+v"(x[9]), "+v"(x[10]), "+v"(x[11]), "+v"(x[12]), "+v"(x[13]), "+v"(x[14]), "+v"(x[15]) : "s"(a) : "vcc");
+    float s = 0;
+#pragma unroll
+    for (int c = 0; c < 16; ++c) s += x[c];
+    if (s == 12345.f) out[threadIdx.x] = s;
+}
 template <typename K>
 float run(K k, int blocks, int iters) {
     float* out;
@@ -304,6 +337,9 @@ int main() {
         {"v_fma_f32 d, v_o, v_o, d", k_fma3, 16},
         {"v_pk_fma_f32 d, v_o, v_o, d", k_pkfma2, 8},
         {"alternating SGPR / all-VGPR fma", k_fma_alt, 16},
+        {"v_fmac_f32 d, literal, v", k_lit, 16},
+        {"alternating literal / all-VGPR", k_lit_alt, 16},
+        {"v_fmac_f32 d, inline const, v", k_inl, 16},
         {"v_fmac_f32", k_fmac, 16},
         {"v_add_f32", k_add, 16},
         {"v_mul_f32", k_mul, 16},

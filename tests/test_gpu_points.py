@@ -150,3 +150,25 @@ def test_draw_points_bitexact(geo, ctx, torch_mod):
     assert np.array_equal(xy_h, ref_xy)
     assert np.array_equal(got, ref)
     assert (xy_h[:, 0] >= 0).sum() > 1000  # the disk is in view
+
+
+def test_point_cloud_draw_equals_two_mesh_draws(geo, ctx, torch_mod):
+    """PointCloud.draw (geo_points_draw: the near mesh, then the far mesh,
+    event-ordered after the cloud's update) == two geo_draw_points calls, frame
+    and per-vertex pixels (out_xy: near side first)."""
+    w, h = 320, 180
+    frame = default_frame(w, h, pos=(25.0, 0.0, 1.0))
+    pc = geo.PointCloud(ctx, accretion_disk(3000, seed=4), 1.0, (25.0, 0.0, 1.0), True, False)
+    pc.update((25.0, 0.0, 1.0), 0.0)
+    dev = torch_mod.device("cuda:0")
+    a = geo.RenderTarget(w, h, torch_mod.zeros(w * h * 4, dtype=torch_mod.uint8, device=dev))
+    b = geo.RenderTarget(w, h, torch_mod.zeros(w * h * 4, dtype=torch_mod.uint8, device=dev))
+    xy = torch_mod.empty((2 * 3000, 2), dtype=torch_mod.int32, device=dev)
+    pc.draw(frame, a, out_xy=xy)
+    xn = torch_mod.empty((3000, 2), dtype=torch_mod.int32, device=dev)
+    xf = torch_mod.empty((3000, 2), dtype=torch_mod.int32, device=dev)
+    geo.draw_points(ctx, frame, pc.vertices_ptr(False), 3000, b, out_xy=xn)
+    geo.draw_points(ctx, frame, pc.vertices_ptr(True), 3000, b, out_xy=xf)
+    assert np.array_equal(host(a.rgba, torch_mod), host(b.rgba, torch_mod))
+    assert np.array_equal(host(xy, torch_mod), np.concatenate([host(xn, torch_mod), host(xf, torch_mod)]))
+    assert (host(xy, torch_mod)[:, 0] >= 0).sum() > 500

@@ -13,6 +13,7 @@ the present-side exchange the north star asks for.
 """
 from __future__ import annotations
 
+import ctypes
 from dataclasses import dataclass
 
 
@@ -128,6 +129,40 @@ def assemble(full, recv, layout: BandLayout, row_bytes: int, frame: int = 0, fra
         fv[rt[keep]] = src[keep]
 
 
+class _RawEvent:
+    """A HIP event without timing or system-scope release, recorded and waited
+    on by stream handle (ctypes): the per-frame ordering of ShardedFrame at
+    ~1 us per call instead of torch.cuda.Event's construction + record."""
+
+    def __init__(self):
+        from .timing import _hip, hipEventDisableSystemFence
+
+        self._hip = _hip
+        self.h = ctypes.c_void_p()
+        if _hip.hipEventCreateWithFlags(ctypes.byref(self.h), hipEventDisableSystemFence | 0x2) != 0:
+            raise RuntimeError("hipEventCreateWithFlags")
+        self.recorded = False
+
+    def record(self, stream: int) -> None:
+        if self._hip.hipEventRecord(self.h, ctypes.c_void_p(stream)) != 0:
+            raise RuntimeError("hipEventRecord")
+        self.recorded = True
+
+    def wait(self, stream: int) -> None:
+        """`stream` waits for the last record (no-op before the first)."""
+        if self.recorded and self._hip.hipStreamWaitEvent(ctypes.c_void_p(stream), self.h, 0) != 0:
+            raise RuntimeError("hipStreamWaitEvent")
+
+    def __del__(self):
+        h = getattr(self, "h", None)
+        if h is not None and h.value:
+            try:
+                self._hip.hipEventDestroy(h)
+            except Exception:  # interpreter shutdown
+                pass
+            self.h = None
+
+
 class ShardedFrame:
     """Render-then-gather pipeline for one rank, K frames per gather.
 
@@ -147,6 +182,12 @@ class ShardedFrame:
     re-rendered only after its gather completed, rank 0's only after the
     reassembly that reads it, and rank 0's receive buffer is re-filled only
     after its reassembly completed.
+
+    The per-frame path is host-bound at N = 8 unless it is lean (a peer's share
+    of a 4K frame is ~26 us of GPU time): step() calls the C-ABI directly with
+    pointers, stream handles and ctypes references computed once, and orders
+    streams with pre-created raw HIP events (tools/host_bound_probe.py).
+    Stream 0 is the caller's current stream when the object is built.
     """
 
     def __init__(self, ctx, frame, scene, width: int, height: int, band_rows: int, rank: int, world: int, device,
@@ -160,7 +201,10 @@ class ShardedFrame:
         (geo_assemble_lead)."""
         import torch
 
+        from ._lib import lib
+
         self.torch = torch
+        self.lib = lib
         self.host_gather = host_gather
         self.ctx, self.frame, self.scene = ctx, frame, scene
         self.width, self.height = width, height
@@ -187,14 +231,12 @@ class ShardedFrame:
             self.sbufs = self.bufs if self.bpp == 4 else [
                 torch.empty(self.K * self.tslice, dtype=torch.uint8, device=device) for _ in range(2)]
         self.frame_bytes = height * self.row_bytes  # assembled frames, back to back
+        self.stream0 = torch.cuda.current_stream(device)
         self.extra = [torch.cuda.Stream(device) for _ in range(self.S - 1)]
         self.recv = None
         self.frames = None
         self.side = None
         self.gstream = None
-        self.ev_free = [None, None]       # batch buffer b may be re-rendered after this event
-        self.ev_assembled = [None, None]  # rank 0: recv[b] may be re-filled after this event
-        self.ev_rendered = [[None] * self.S for _ in range(2)]  # last render per stream into batch b
         if world > 1 and not host_gather:
             self.gstream = torch.cuda.Stream(device)
         if world > 1 and rank == 0:
@@ -204,7 +246,22 @@ class ShardedFrame:
             if not host_gather:
                 # reassembly (HBM-bound) on its own stream, overlapping the next renders (VALU-bound)
                 self.side = torch.cuda.Stream(device)
-        self.pending = [None, None]  # (work, nframes, batch number) per batch buffer
+        # raw events: a batch buffer may be re-rendered after ev_free[b]; rank
+        # 0's recv[b] may be re-filled after ev_assembled[b]; ev_rendered[b][k]
+        # = the last render (and pack) of stream k into batch buffer b
+        self.ev_free = [_RawEvent(), _RawEvent()]
+        self.ev_assembled = [_RawEvent(), _RawEvent()]
+        self.ev_rendered = [[_RawEvent() for _ in range(self.S)] for _ in range(2)]
+        self.rendered_in = [[False] * self.S for _ in range(2)]  # stream k rendered into batch b since its launch
+        # the per-frame C-ABI arguments, computed once
+        self._sh = [self.stream0.cuda_stream] + [st.cuda_stream for st in self.extra]
+        self._ctx_h = ctx._h
+        self._frame_ref = ctypes.byref(frame)
+        self._scene_ref = ctypes.byref(scene)
+        self._band = (L.band_height(), L.row0(), L.cycle_rows, L.nbands())
+        self._lv = [[self.bufs[b].data_ptr() + sub * self.slice for sub in range(self.K)] for b in range(2)]
+        self._sv = [[self.sbufs[b].data_ptr() + sub * self.tslice for sub in range(self.K)] for b in range(2)]
+        self.pending = [None, None]  # (work, nframes, batch number, streams that rendered) per batch buffer
         self.rendered = 0            # frames rendered into the open batch
         self.open = 0                # batch buffer being filled
         self.batches = 0             # batches launched
@@ -222,28 +279,32 @@ class ShardedFrame:
         self.ctx.render_band_set(self.frame, self.scene if scene is None else scene, self.width, self.height,
                                  L.band_height(), L.row0(), L.cycle_rows, L.nbands(), buf, **outs)
 
-    def _assemble(self, b: int, src, n: int) -> None:
+    def _assemble(self, b: int, src, n: int, stream=None) -> None:
         """Rank 0: frames of batch b from its own bands (bufs[b]) and the peers' gathered blocks."""
         self.ctx.assemble_lead(self.bufs[b], self.slice, self.layout.lead, src, self.K * self.tslice, self.tslice,
                                self.world, self.layout.band_rows, self.width, self.height, n, self.frames,
-                               src_bpp=self.bpp)
+                               src_bpp=self.bpp, stream=stream)
 
     def _render_stream(self, i: int):
         k = i % self.S
-        return self.torch.cuda.current_stream() if k == 0 else self.extra[k - 1]
+        return self.stream0 if k == 0 else self.extra[k - 1]
 
     def _join(self) -> None:
         """The current stream waits for every render stream."""
         cur = self.torch.cuda.current_stream()
-        for st in self.extra:
+        for st in [self.stream0] + self.extra:
+            if st.cuda_stream == cur.cuda_stream:
+                continue
             ev = self.torch.cuda.Event()
             ev.record(st)
             cur.wait_event(ev)
 
     def _launch(self, b: int, n: int) -> None:
         self.batches += 1
+        rendered = [k for k in range(self.S) if self.rendered_in[b][k]]
+        self.rendered_in[b] = [False] * self.S
         if self.world == 1:
-            self.pending[b] = (None, n, self.batches, [])
+            self.pending[b] = (None, n, self.batches, rendered)
             return
         torch = self.torch
         gl = list(self.recv[b].chunk(self.world)) if self.rank == 0 else None
@@ -251,19 +312,16 @@ class ShardedFrame:
             self._join()
             work = self.dist.gather(self.sbufs[b].cpu(), gather_list=gl, dst=0, async_op=True)
         else:
+            gsh = self.gstream.cuda_stream
             with torch.cuda.stream(self.gstream):
                 # a peer sends after its renders; rank 0 sends nothing it
                 # renders, so its receives are posted at once (its reassembly
                 # waits for its renders instead)
                 if self.rank != 0:
-                    for ev in self.ev_rendered[b]:
-                        if ev is not None:
-                            self.gstream.wait_event(ev)
-                if self.ev_assembled[b] is not None:
-                    self.gstream.wait_event(self.ev_assembled[b])  # recv[b] is still being reassembled
+                    for k in rendered:
+                        self.ev_rendered[b][k].wait(gsh)
+                self.ev_assembled[b].wait(gsh)  # recv[b] is still being reassembled
                 work = self.dist.gather(self.sbufs[b], gather_list=gl, dst=0, async_op=True)
-        rendered = [ev for ev in self.ev_rendered[b] if ev is not None]
-        self.ev_rendered[b] = [None] * self.S
         self.pending[b] = (work, n, self.batches, rendered)
 
     def _retire(self, b: int) -> None:
@@ -277,18 +335,13 @@ class ShardedFrame:
             st = self.side if self.side is not None else self.gstream
             with torch.cuda.stream(st):
                 work.wait()  # this stream waits for the gather
-                if self.side is not None:
-                    for ev in rendered:  # rank 0's own bands of the batch
-                        st.wait_event(ev)
-                    self._assemble(b, self.recv[b], n)
-                    ea = torch.cuda.Event()
-                    ea.record(st)
-                    self.ev_assembled[b] = ea
-                    self.ev_free[b] = ea  # the reassembly read bufs[b]
-                else:
-                    ev = torch.cuda.Event()
-                    ev.record(st)
-                    self.ev_free[b] = ev
+            sh = st.cuda_stream
+            if self.side is not None:
+                for k in rendered:  # rank 0's own bands of the batch
+                    self.ev_rendered[b][k].wait(sh)
+                self._assemble(b, self.recv[b], n, stream=sh)
+                self.ev_assembled[b].record(sh)
+            self.ev_free[b].record(sh)  # the gather (peer) or the reassembly (rank 0) read bufs[b]
         elif work is not None:
             work.wait()
             if self.rank == 0:
@@ -300,28 +353,37 @@ class ShardedFrame:
             self.last = (seq, b, n - 1)
 
     def step(self, i: int, steps_total=None, events=None, scene=None) -> None:
-        torch = self.torch
         b, sub = (i // self.K) % 2, i % self.K
         if sub == 0:
             self._retire(b)  # the batch that used this buffer two batches ago
-        st = self._render_stream(i)
-        if sub < self.S and self.ev_free[b] is not None:
-            st.wait_event(self.ev_free[b])  # first render of this stream into the batch buffer
-            if sub == min(self.S, self.K) - 1:
-                self.ev_free[b] = None
-        with torch.cuda.stream(st):
-            if events is not None:
-                events[0].record()
-            self.render_local(self.local_view(i), scene=scene, steps_total=steps_total)
-            if events is not None:
-                events[1].record()
-            if self.bpp == 3 and self.rank != 0:
-                self.ctx.pack_rgb(self.local_view(i), self.slice // 4,
-                                  self.sbufs[b][sub * self.tslice:(sub + 1) * self.tslice])
-            if self.world > 1:
-                ev = torch.cuda.Event()
-                ev.record(st)
-                self.ev_rendered[b][i % self.S] = ev
+        k = i % self.S
+        sh = self._sh[k]
+        if sub < self.S:
+            self.ev_free[b].wait(sh)  # first render of this stream into the batch buffer
+        if events is not None:
+            events[0].record(sh)
+        band_h, row0, cycle, nb = self._band
+        lib = self.lib
+        if nb:
+            st = lib.geo_render_band_set(
+                self._ctx_h, self._frame_ref, self._scene_ref if scene is None else ctypes.byref(scene), self.width,
+                self.height, band_h, row0, cycle, nb, self._lv[b][sub], None, None, None,
+                None if steps_total is None else steps_total.data_ptr(), sh)
+            if st != 0:
+                from ._lib import check
+
+                check("geo_render_band_set", st)
+        if events is not None:
+            events[1].record(sh)
+        if self.bpp == 3 and self.rank != 0:
+            st = lib.geo_pack_rgb(self._ctx_h, self._lv[b][sub], self.slice // 4, self._sv[b][sub], sh)
+            if st != 0:
+                from ._lib import check
+
+                check("geo_pack_rgb", st)
+        if self.world > 1:
+            self.ev_rendered[b][k].record(sh)
+            self.rendered_in[b][k] = True
         self.rendered = sub + 1
         self.open = b
         if sub == self.K - 1:

@@ -17,6 +17,7 @@ _hip.hipEventRecord.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
 _hip.hipEventSynchronize.argtypes = [ctypes.c_void_p]
 _hip.hipEventElapsedTime.argtypes = [ctypes.POINTER(ctypes.c_float), ctypes.c_void_p, ctypes.c_void_p]
 _hip.hipEventDestroy.argtypes = [ctypes.c_void_p]
+_hip.hipStreamWaitEvent.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint]
 
 hipEventDefault = 0x0
 hipEventDisableSystemFence = 0x20000000

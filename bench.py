@@ -53,7 +53,7 @@ def parse():
     p.add_argument("--render-streams", type=int, default=None,
                    help="render streams (1 or 2; default 1 at N = 1, 2 at N > 1: the next frame's waves fill "
                         "the tail of a rank's small share)")
-    p.add_argument("--frames-per-gather", type=int, default=4,
+    p.add_argument("--frames-per-gather", type=int, default=8,
                    help="N > 1: frames per RCCL gather to rank 0 (amortises the ~34 us host cost of a gather; "
                         "rank 0 reassembles each batch with one geo_assemble_lead launch)")
     p.add_argument("--rank0-lead", default="auto", choices=["auto", "1", "2", "3", "4", "6"],

@@ -261,7 +261,18 @@ def main():
         raise SystemExit(f"step counter mismatch: {steps_done} vs {steps_diag} x {args.steps}")
     stats = torch.tensor([elapsed, kernel_ms_avg, elapsed_compute], dtype=torch.float64, device=rdev)
     tot = torch.tensor([steps_done, rows_mine * W * args.steps, evals_per_launch], dtype=torch.int64, device=rdev)
+    per_rank = None
     if world > 1:
+        # per-rank diagnostics for the scaling analysis: each rank's wall and
+        # compute-only time, isolated-launch kernel time and rows
+        mine = torch.tensor([elapsed, elapsed_compute, kernel_ms_avg, float(rows_mine)], dtype=torch.float64,
+                            device=rdev)
+        every = [torch.empty_like(mine) for _ in range(world)]
+        dist.all_gather(every, mine)
+        per_rank = {"ms_per_step": [round(float(t[0]) / args.steps * 1e3, 5) for t in every],
+                    "compute_only_ms_per_step": [round(float(t[1]) / args.steps * 1e3, 5) for t in every],
+                    "kernel_ms_avg": [round(float(t[2]), 5) for t in every],
+                    "rows": [int(t[3]) for t in every]}
         dist.all_reduce(stats, op=dist.ReduceOp.MAX)
         dist.all_reduce(tot, op=dist.ReduceOp.SUM)
     elapsed_max, kernel_ms_max, compute_max = float(stats[0]), float(stats[1]), float(stats[2])
@@ -319,6 +330,7 @@ def main():
             "render_streams": sf.S,
         },
         "per_gpu": value / world,
+        "per_rank": per_rank,
         "pixels_per_s": total_pixels / elapsed_max,
         "frames_per_s": args.steps / elapsed_max,
         "steps_per_frame": total_steps // args.steps,

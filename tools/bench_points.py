@@ -30,6 +30,18 @@ PEAK_HBM_GBS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md)
 BYTES_PER_CONNECTOR = 2 * 48 * 4 + 2 + 6 + 16
 
 
+def pmc_traffic(n_conn, orbits):
+    """HBM bytes per launch of geo_rays_kernel from the committed rocprofv3 PMC
+    summary (profiles/r01_points_pmc.json: FETCH_SIZE doubled for 16-B/lane
+    streaming reads, WRITE_SIZE), for the workload it was taken on, else None."""
+    path = os.path.join(ROOT, "profiles", "r01_points_pmc.json")
+    if orbits or not os.path.exists(path):
+        return None
+    with open(path) as f:
+        d = json.load(f)
+    return d["derived"]["traffic_bytes"] if d["workload"].startswith(f"{n_conn} connectors") else None
+
+
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("--points", type=int, default=1 << 21)
@@ -102,7 +114,7 @@ def main():
                    "orbits": bool(args.orbits)},
         "kernel_ms": {"avg": ms_avg, "median": ms[len(ms) // 2], "min": ms[0]},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                     "frac": achieved / PEAK_HBM_GBS, "traffic": None,
+                     "frac": achieved / PEAK_HBM_GBS, "traffic": pmc_traffic(n_conn, args.orbits),
                      "algorithmic_bytes_per_connector": BYTES_PER_CONNECTOR},
         "cpu_baseline": {"value": 2 * m * k / cdt, "unit": "connector-updates/s", "cores": 1, "kind": "port",
                          "sample": f"{k} updates of {2 * m} connectors in {cdt:.2f} s (oracle, libm)"},

@@ -129,6 +129,9 @@ def main():
                             host_gather=args.dist_backend == "gloo", frames_per_gather=args.frames_per_gather,
                             render_streams=args.render_streams or (1 if world == 1 else 2), lead=lead)
 
+    # everything that syncs or reads back (lead trials, the diagnostic pass)
+    # runs before the clock spin-up below, which flows straight into the
+    # warmup and the timed region
     if world == 1:
         leads = [1]
     elif args.rank0_lead == "auto":
@@ -138,23 +141,13 @@ def main():
     sf = make_sf(leads[0])
     steps_ctr = torch.zeros(1, dtype=torch.int64, device=dev)
 
-    # GPU clock spin-up (untimed, not counted as warmup): from idle the first
-    # frames run up to 5x slower while the clock ramps (tools/ubench/gap_probe2.py)
-    spin = args.spinup_frames * world
-    for i in range(spin):
-        sf.step(i)
-        if i % 50 == 49:
-            sf.drain()
-            torch.cuda.synchronize()
-    sf.drain()
-    torch.cuda.synchronize()
-
     # rank 0's share (--rank0-lead auto): every layout runs the whole pipeline
     # (render, pack, gather, reassembly) for the same frames, untimed for the
     # metric; the fastest by max-over-ranks wall time is used for the timed
     # region.  Every rank holds the same all-reduced times, so all pick alike.
     lead_trials = None
     if len(leads) > 1:
+        spin_up(sf, args.spinup_frames * world)  # the trials compare layouts at the settled clock
         times = []
         for ld in leads:
             t_sf = sf if ld == sf.layout.lead else make_sf(ld)
@@ -198,11 +191,6 @@ def main():
     else:
         flops_per_launch = FLOPS_PER_EVAL * evals_per_launch
 
-    for i in range(args.warmup):
-        sf.step(i)
-    sf.drain()
-    torch.cuda.synchronize()
-
     # timed region: K frames; steps counted in the context (GEO_FLAG_DEFER_STEPS)
     # and flushed once at the end; fence-free event pairs on every k-th frame
     from schwarzschild_raytracer_wgpu_amd.timing import HipEvent
@@ -215,6 +203,23 @@ def main():
     timed = set(range(0, args.steps, max(1, args.event_every))) if sf.S == 1 else set()
     evs = {i: (HipEvent(), HipEvent()) for i in timed}
     steps_ctr.zero_()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+
+    # GPU clock spin-up (untimed, not counted as warmup), then the warmup,
+    # then the timed region, with no host work in between: the clock falls
+    # back within ~1 ms of an idle queue and the next ~100 4K frames run
+    # 10-30 % slower (tools/ubench/clock_probe.py), so everything that syncs
+    # or reads back (the diagnostic pass, the lead trials) comes before this.
+    # The short syncs every 50 frames keep the host within reach of the GPU
+    # and cost nothing (clock_probe: no ramp after them).
+    spin = args.spinup_frames * world
+    spin_up(sf, spin)
+    for i in range(args.warmup):
+        sf.step(i)
+    sf.drain()
+    torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -350,7 +355,7 @@ def main():
             "peak": PEAK_FP32_TFLOPS,
             "unit": "TFLOP/s",
             "frac": achieved_tflops / PEAK_FP32_TFLOPS,
-            "traffic": pmc_traffic(args.config, args.mode),
+            "traffic": pmc_traffic(args.config, args.mode, world),
             "kernel": f"geo_render_kernel<{mode}>",
             "algorithmic_flops_per_launch": flops_per_launch,
             "evals_per_launch": evals_per_launch,
@@ -364,19 +369,37 @@ def main():
         dist.destroy_process_group()
 
 
-def pmc_traffic(config, mode):
+def spin_up(sf, n):
+    """n untimed frames back to back (a short sync every 50 keeps the host
+    within reach of the GPU without idling it)."""
+    import torch
+
+    for i in range(n):
+        sf.step(i)
+        if i % 50 == 49:
+            sf.drain()
+            torch.cuda.synchronize()
+    sf.drain()
+
+
+def pmc_traffic(config, mode, world):
     """HBM bytes per launch of the render kernel from the committed rocprofv3
     PMC summary of this workload (profiles/*_<config>_pmc.json, made by
-    tools/gpu_pmc.sh + tools/pmc_to_profile.py), or None."""
+    tools/gpu_pmc.sh + tools/pmc_to_profile.py), or None.  Only a profile
+    taken on this exact workload counts: same config, same mode (its
+    workload string ends in ", <mode>)"), one GPU (the profiles hold
+    full-frame bytes; at N > 1 a launch renders a partial share)."""
     import glob
 
-    if mode == "fan":
+    if world != 1:
         return None
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_{config}_pmc.json")))
-    if not files:
-        return None
-    with open(files[-1]) as f:
-        return json.load(f)["derived"]["traffic_bytes"]
+    for path in reversed(files):
+        with open(path) as f:
+            d = json.load(f)
+        if d.get("workload", "").startswith(config) and d["workload"].endswith(f", {mode})"):
+            return d["derived"]["traffic_bytes"]
+    return None
 
 
 def reference_fan_cost(ctx, cfg, r):

@@ -125,13 +125,16 @@ int geo_ctx_create(int device, geo_ctx** out);
 void geo_ctx_destroy(geo_ctx* ctx);
 
 /* Uploads an equirect RGBA8 sky (row-major, w*h*4 bytes, host memory; the
- * bytes are copied, synchronously).  U wraps, V clamps, LOD-0 bilinear with
+ * bytes are copied, synchronously, after every render in flight on the
+ * context's device has finished, so no frame samples a half-written sky).
+ * On failure the context has no sky (renders return GEO_ESTATE).  U wraps, V clamps, LOD-0 bilinear with
  * 8-bit sub-texel weights.  The device keeps a copy padded by one texel on
  * every side, which must stay below 2^31 bytes: (w + 2) * (h + 2) * 4 < 2^31,
  * w, h <= 2^20 (GEO_EINVAL otherwise). */
 int geo_set_sky(geo_ctx* ctx, const uint8_t* rgba8, uint32_t w, uint32_t h);
 
-/* Uploads a ray fan of n >= 2 nodes (host memory, copied synchronously):
+/* Uploads a ray fan of n >= 2 nodes (host memory, copied synchronously after
+ * the device's work in flight; geo_solve_ray_fan replaces it stream-ordered):
  * node i is PI/2 - traveled angle of the ray at theta_i = PI/2 - PI*i/(n-1). */
 int geo_set_fan(geo_ctx* ctx, const float* fan, uint32_t n);
 
@@ -263,7 +266,8 @@ void geo_points_destroy(geo_points* pts);
 int geo_points_count(const geo_points* pts);
 /* PointCloud::update (point_cloud.rs:117-148): orbit step by dt seconds and
  * respawn (orbits), then update_ray(observer, 1) for every connector.
- * Asynchronous on `stream`. */
+ * Asynchronous on `stream`; it waits for the cloud's previous update and for
+ * every geo_points_draw before it, whichever streams they ran on. */
 int geo_points_update(geo_points* pts, const float* observer_xyz, double dt, void* stream);
 /* get_vertices / get_vertices_farside: device pointer, 4 floats per point
  * (NULL for the far side of a cloud without one). */
@@ -285,8 +289,8 @@ int geo_draw_points(geo_ctx* ctx, const geo_frame* frame, const float* vertices,
  * far-side ones; lib.rs:415-418, renderer.rs:256-264) drawn as by
  * geo_draw_points.  out_xy (device, optional): 2 ints per connector, near
  * side first.  Stream order: the draw waits for the cloud's last
- * geo_points_update and the next update waits for this draw (events owned by
- * the cloud), whichever streams they run on, so a caller may put the update
+ * geo_points_update and the next update waits for this draw and every draw
+ * before it (events owned by the cloud), whichever streams they run on, so a caller may put the update
  * on a side stream where it overlaps the sphere draws.  Async on `stream`. */
 int geo_points_draw(geo_points* pts, const geo_frame* frame, uint32_t width, uint32_t height, uint32_t row0,
                     uint32_t nrows, uint8_t* out_rgba8, int* out_xy, void* stream);

@@ -171,10 +171,7 @@ class Context:
     def render_rows(self, frame: GeoFrame, scene: GeoScene, width: int, height: int, row0: int, nrows: int,
                     out_rgba, out_mask=None, out_uv=None, out_steps=None, steps_total=None, stream=None) -> None:
         """geo_render_rows; outputs are device tensors (rgba: nrows*width*4 u8)."""
-        for t, n in ((out_rgba, nrows * width * 4), (out_mask, nrows * width), (out_uv, nrows * width * 2),
-                     (out_steps, nrows * width), (steps_total, 1)):
-            if t is not None and (not t.is_cuda or not t.is_contiguous() or t.numel() < n):
-                raise ValueError("outputs must be contiguous device tensors of sufficient size")
+        _check_outputs(nrows, width, out_rgba, out_mask, out_uv, out_steps, steps_total)
         check("geo_render_rows", lib.geo_render_rows(
             self._h, ctypes.byref(frame), ctypes.byref(scene), width, height, row0, nrows,
             _ptr(out_rgba), _ptr(out_mask), _ptr(out_uv), _ptr(out_steps), _ptr(steps_total),
@@ -186,10 +183,7 @@ class Context:
                      steps_total=None, stream=None) -> None:
         """geo_render_bands; outputs packed band after band (nbands*band_rows rows)."""
         nrows = nbands * band_rows
-        for t, n in ((out_rgba, nrows * width * 4), (out_mask, nrows * width), (out_uv, nrows * width * 2),
-                     (out_steps, nrows * width), (steps_total, 1)):
-            if t is not None and (not t.is_cuda or not t.is_contiguous() or t.numel() < n):
-                raise ValueError("outputs must be contiguous device tensors of sufficient size")
+        _check_outputs(nrows, width, out_rgba, out_mask, out_uv, out_steps, steps_total)
         check("geo_render_bands", lib.geo_render_bands(
             self._h, ctypes.byref(frame), ctypes.byref(scene), width, height, band_rows, band0, band_step, nbands,
             _ptr(out_rgba), _ptr(out_mask), _ptr(out_uv), _ptr(out_steps), _ptr(steps_total),
@@ -200,14 +194,34 @@ class Context:
                         steps_total=None, stream=None) -> None:
         """geo_render_band_set: bands at rows row0 + j*row_stride (j < nbands), band_rows tall, packed."""
         nrows = nbands * band_rows
-        for t, n in ((out_rgba, nrows * width * 4), (out_mask, nrows * width), (out_uv, nrows * width * 2),
-                     (out_steps, nrows * width), (steps_total, 1)):
-            if t is not None and (not t.is_cuda or not t.is_contiguous() or t.numel() < n):
-                raise ValueError("outputs must be contiguous device tensors of sufficient size")
+        _check_outputs(nrows, width, out_rgba, out_mask, out_uv, out_steps, steps_total)
         check("geo_render_band_set", lib.geo_render_band_set(
             self._h, ctypes.byref(frame), ctypes.byref(scene), width, height, band_rows, row0, row_stride, nbands,
             _ptr(out_rgba), _ptr(out_mask), _ptr(out_uv), _ptr(out_steps), _ptr(steps_total),
             _stream_handle(stream)))
+
+
+def _check_outputs(nrows: int, width: int, rgba, mask, uv, steps, steps_total) -> None:
+    """The kernel writes 4 B of RGBA8, 1 B of mask, 2 f32 of UV and one u32 of
+    steps per pixel, and adds into one u64 total: every output must be a
+    contiguous device tensor holding at least that many BYTES (a tensor of
+    the right element count but a narrower dtype would be overrun), and the
+    typed ones must carry their type (f32 UV, 4-byte steps, 64-bit total)."""
+    import torch
+
+    n = nrows * width
+    for name, t, nbytes, dtypes in (("out_rgba", rgba, 4 * n, None), ("out_mask", mask, n, None),
+                                    ("out_uv", uv, 8 * n, (torch.float32,)),
+                                    ("out_steps", steps, 4 * n, (torch.int32, torch.uint32)),
+                                    ("steps_total", steps_total, 8, (torch.int64, torch.uint64))):
+        if t is None:
+            continue
+        if not t.is_cuda or not t.is_contiguous():
+            raise ValueError(f"{name} must be a contiguous device tensor")
+        if dtypes is not None and t.dtype not in dtypes:
+            raise ValueError(f"{name} must be one of {dtypes}, got {t.dtype}")
+        if t.numel() * t.element_size() < nbytes:
+            raise ValueError(f"{name} holds {t.numel() * t.element_size()} bytes, the rows need {nbytes}")
 
 
 def make_scene(rs: float, sphere_r: float, r_obs: float, step: float = math.pi / 100.0, max_steps: int = 1000,

@@ -361,9 +361,13 @@ struct geo_points {
     geo_rays rays;
     bool has_orbits;
     // Cross-stream order of the update and the draw (geo_points_draw): the
-    // draw waits for the last update, the next update for the last draw, so
-    // a caller may run the update on a side stream, overlapping the
-    // VALU-bound sphere draw with this latency-bound work.
+    // draw waits for the last update, the next update for the last update
+    // and every draw before it, so a caller may run the update on a side
+    // stream, overlapping the VALU-bound sphere draw with this latency-bound
+    // work.  `drawn` is a chain: each draw records it only after waiting for
+    // the previous draw's `drawn` (behind its own launches, so the draws
+    // themselves still overlap), so it completes after every draw so far,
+    // on whatever streams they ran.
     hipEvent_t updated = nullptr, drawn = nullptr;
     bool updated_rec = false, drawn_rec = false;
 };
@@ -576,7 +580,10 @@ int geo_points_update(geo_points* p, const float* observer_xyz, double dt, void*
     DeviceGuard g(r->device);
     if (!g.ok) return GEO_EHIP;
     hipStream_t s = (hipStream_t)stream;
-    if (p->drawn_rec && hipStreamWaitEvent(s, p->drawn, 0) != hipSuccess) return GEO_EHIP;  // last draw read the vertices
+    // every draw so far read the vertices (the chained `drawn`); the last
+    // update, on whatever stream, wrote the state this one reads
+    if (p->drawn_rec && hipStreamWaitEvent(s, p->drawn, 0) != hipSuccess) return GEO_EHIP;
+    if (p->updated_rec && hipStreamWaitEvent(s, p->updated, 0) != hipSuccess) return GEO_EHIP;
     if (p->has_orbits) {
         hipLaunchKernelGGL(geo_orbits_kernel, dim3((r->n_points + kOrbitBlock - 1) / kOrbitBlock), dim3(kOrbitBlock),
                            0, s, r->n_points, dt, r->rs, r->orbits, r->rng, r->pos, r->respawn, r->respawn_pos);
@@ -666,6 +673,7 @@ int geo_points_draw(geo_points* p, const geo_frame* frame, uint32_t width, uint3
                                    out_xy ? out_xy + 2 * (size_t)far * r->n_points : nullptr, s);
         if (st) return st;
     }
+    if (p->drawn_rec && hipStreamWaitEvent(s, p->drawn, 0) != hipSuccess) return GEO_EHIP;  // chain the draws
     if (hipEventRecord(p->drawn, s) != hipSuccess) return GEO_EHIP;
     p->drawn_rec = true;
     return GEO_OK;

@@ -468,17 +468,32 @@ int geo_set_sky(geo_ctx* c, const uint8_t* rgba8, uint32_t w, uint32_t h) {
     if (!g.ok) return GEO_EHIP;
     const size_t bytes = (size_t)w * h * 4;
     const size_t padded = ((size_t)w + 2u) * ((size_t)h + 2u);
+    std::vector<uint32_t> pad(padded);
+    geo::pad_sky(rgba8, w, h, pad.data());
+    // Renders still running on any of the caller's streams (non-blocking ones
+    // do not order against a blocking copy) may be reading the current sky:
+    // let them finish before it is overwritten or freed.  A sky change is a
+    // set-up call (the reference builds its texture once,
+    // basic_sphere_buffer.rs:29-36), so the device-wide wait costs nothing
+    // per frame.
+    if (hipDeviceSynchronize() != hipSuccess) return GEO_EHIP;
     if (c->sky && ((size_t)c->sky_w + 2u) * ((size_t)c->sky_h + 2u) != padded) {
         (void)hipFree(c->sky);
         c->sky = nullptr;
+        c->sky_w = c->sky_h = 0;
     }
     if (!c->sky && hipMalloc(&c->sky, padded * 4u) != hipSuccess) {
         c->sky = nullptr;
+        c->sky_w = c->sky_h = 0;
         return GEO_ENOMEM;
     }
-    std::vector<uint32_t> pad(padded);
-    geo::pad_sky(rgba8, w, h, pad.data());
-    if (hipMemcpy(c->sky, pad.data(), padded * 4u, hipMemcpyHostToDevice) != hipSuccess) return GEO_EHIP;
+    if (hipMemcpy(c->sky, pad.data(), padded * 4u, hipMemcpyHostToDevice) != hipSuccess) {
+        // the buffer's contents are unknown now: no sky (renders return GEO_ESTATE until the next upload)
+        (void)hipFree(c->sky);
+        c->sky = nullptr;
+        c->sky_w = c->sky_h = 0;
+        return GEO_EHIP;
+    }
     c->sky_w = w;
     c->sky_h = h;
     bool opaque = true;
@@ -501,9 +516,18 @@ int geo_set_fan(geo_ctx* c, const float* fan, uint32_t n) {
     if (!c || !fan || n < 2 || n > kMaxFan) return GEO_EINVAL;
     DeviceGuard g(c->device);
     if (!g.ok) return GEO_EHIP;
+    // as geo_set_sky: fan-mode renders in flight on any stream read the fan
+    // (geo_solve_ray_fan is the stream-ordered way to replace it per frame)
+    if (hipDeviceSynchronize() != hipSuccess) return GEO_EHIP;
     int st = ensure_fan(c, n);
-    if (st) return st;
-    if (hipMemcpy(c->fan, fan, sizeof(float) * n, hipMemcpyHostToDevice) != hipSuccess) return GEO_EHIP;
+    if (st) {
+        c->n_fan = 0;
+        return st;
+    }
+    if (hipMemcpy(c->fan, fan, sizeof(float) * n, hipMemcpyHostToDevice) != hipSuccess) {
+        c->n_fan = 0;
+        return GEO_EHIP;
+    }
     c->n_fan = n;
     return GEO_OK;
 }

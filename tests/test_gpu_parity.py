@@ -367,6 +367,39 @@ def test_invalid_arguments(geo, torch_mod):
         geo.Context(99)
 
 
+def test_output_buffers_checked_by_bytes_and_type(geo, torch_mod):
+    """The Python wrappers refuse outputs that would be overrun: the right
+    element count in a narrower dtype (u8 steps, f16 UV, i32 total), the
+    wrong type, too few bytes or host memory.  Nothing is launched."""
+    torch = torch_mod
+    ctx = geo.Context(0)
+    ctx.set_sky(np.zeros((1, 1, 4), np.uint8))
+    frame, scene = default_frame(8, 8), default_scene(16)
+    dev = torch.device("cuda:0")
+    n = 64
+    rgba = torch.zeros(n * 4, dtype=torch.uint8, device=dev)
+    bad = [dict(out_steps=torch.zeros(n, dtype=torch.uint8, device=dev)),
+           dict(out_uv=torch.zeros(2 * n, dtype=torch.float16, device=dev)),
+           dict(out_uv=torch.zeros(n, dtype=torch.float64, device=dev)),
+           dict(steps_total=torch.zeros(1, dtype=torch.int32, device=dev)),
+           dict(out_mask=torch.zeros(n - 1, dtype=torch.uint8, device=dev)),
+           dict(out_steps=torch.zeros(n, dtype=torch.int32))]
+    for kw in bad:
+        with pytest.raises(ValueError):
+            ctx.render_rows(frame, scene, 8, 8, 0, 8, rgba, **kw)
+        with pytest.raises(ValueError):
+            ctx.render_bands(frame, scene, 8, 8, 8, 0, 1, 1, rgba, **kw)
+        with pytest.raises(ValueError):
+            ctx.render_band_set(frame, scene, 8, 8, 8, 0, 8, 1, rgba, **kw)
+    with pytest.raises(ValueError):  # 4 B per pixel: an RGBA8 buffer of n elements is too short
+        ctx.render_rows(frame, scene, 8, 8, 0, 8, torch.zeros(n, dtype=torch.uint8, device=dev))
+    # the RGBA8 target may be any dtype of enough bytes (an int32 view of the frame)
+    ok = torch.zeros(n, dtype=torch.int32, device=dev)
+    ctx.render_rows(frame, scene, 8, 8, 0, 8, ok, out_steps=torch.zeros(n, dtype=torch.int32, device=dev),
+                    steps_total=torch.zeros(1, dtype=torch.int64, device=dev))
+    torch.cuda.synchronize()
+
+
 def test_maximum_step_budget_bitexact(geo, torch_mod):
     """The largest budget the ABI accepts (2^24 steps): every ray still stops on its own
     (crossing, escape or horizon), so the frame equals the oracle's and the 2048-step frame's."""
@@ -464,6 +497,46 @@ def test_points_update_on_side_stream_matches_one_stream(geo, torch_mod):
     assert np.array_equal(one[1], two[1]) and np.array_equal(one[2], two[2])
     red = [int((f.reshape(h, w, 4)[..., :3] == np.array([255, 0, 0], np.uint8)).all(-1).sum()) for f in one[0]]
     assert min(red) > 100  # the disk is drawn in every frame
+
+
+def test_points_updates_and_draws_across_streams(geo, torch_mod):
+    """Back-to-back updates on alternating streams with no draw between them,
+    and several draws on different streams before the next update: every
+    update waits for the previous update and for all draws before it (the
+    chained `drawn` event), so the vertices and frames equal the one-stream
+    sequence.  Long dt: particles fall and respawn."""
+    torch = torch_mod
+    w, h = 320, 180
+    dev = torch.device("cuda:0")
+
+    def run(streams):
+        ctx = geo.Context(0)
+        obs = geo.Observer(1.0, math.pi / 2, w, h)
+        obs.set_position(2.5, 0.0, 0.1)
+        disk = geo.PointCloud.new_accretion_disk(ctx, 1.0, obs.get_position(), True, seed=11, n=20000)
+        tgts = [geo.RenderTarget(w, h, torch.zeros(w * h * 4, dtype=torch.uint8, device=dev)) for _ in range(3)]
+        frames = []
+        for k in range(6):
+            for j in range(3):  # three updates, no draw between them
+                obs.update_position((0.0, 0.0, 0.0), 1 / 60)
+                disk.update(obs.get_position(), 0.3, stream=streams[(k + j) % len(streams)])
+            frame = obs.calc_transformation_pipeline()
+            for j, t in enumerate(tgts):  # three draws, on different streams
+                t.rgba.zero_()
+                torch.cuda.synchronize()
+                disk.draw(frame, t, stream=streams[(k + j + 1) % len(streams)])
+            obs.update_position((0.0, 0.0, 0.0), 1 / 60)
+            disk.update(obs.get_position(), 0.3, stream=streams[k % len(streams)])  # must wait for all 3 draws
+            torch.cuda.synchronize()
+            frames.append([t.rgba.cpu().numpy() for t in tgts])
+        return frames, disk.get_vertices(False), disk.get_vertices(True)
+
+    one = run([None])
+    many = run([torch.cuda.Stream(dev), torch.cuda.Stream(dev), None])
+    for fa, fb in zip(one[0], many[0]):
+        for a, b in zip(fa, fb):
+            assert np.array_equal(a, b)
+    assert np.array_equal(one[1], many[1]) and np.array_equal(one[2], many[2])
 
 
 @pytest.mark.parametrize("rotation,nframes", [(3.2, 120), (2.0, 200)])

@@ -16,4 +16,4 @@ SETS=("GRBM_GUI_ACTIVE SQ_INSTS_SALU SQ_INSTS_VALU" "SQ_INSTS_VALU_TRANS_F32 SQ_
 CONFIG=cfg3_4k bash tools/gpu_pmc.sh pmc3_$TAG "${SETS[@]}" || exit $?
 CONFIG=cfg5_8k_adaptive bash tools/gpu_pmc.sh pmc5_$TAG "${SETS[@]}" || exit $?
 python tools/pmc_to_profile.py pmc3_$TAG gpurun_out/${TAG}_cfg3_4k_pmc.json "cfg3_4k (3840x2160, 2048 steps, direct)" > /dev/null
-python tools/pmc_to_profile.py pmc5_$TAG gpurun_out/${TAG}_cfg5_8k_adaptive_pmc.json "cfg5_8k_adaptive (7680x4320, RK5(4) tol 1e-6)" "geo_render_kernel<GEO_MODE_ADAPTIVE, kCurvedOut>"
+python tools/pmc_to_profile.py pmc5_$TAG gpurun_out/${TAG}_cfg5_8k_adaptive_pmc.json "cfg5_8k_adaptive (7680x4320, RK5(4) tol 1e-6, adaptive)" "geo_render_kernel<GEO_MODE_ADAPTIVE, kCurvedOut>"

@@ -286,7 +286,7 @@ float geo_oracle_atan2f(float y, float x) {
     } else {
         num = ay; den = ax; y0 = 0.0f;
     }
-    float t = den > 0.0f ? num / den : 0.0f;
+    float t = den > 0.0f ? num * (1.0f / den) : 0.0f; /* divf_ */
     float z = t * t;
     float p = fmaf(fmaf(fmaf(8.05374449538e-2f, z, -1.38776856032e-1f), z, 1.99777106478e-1f), z,
                    -3.33329491539e-1f);
@@ -442,7 +442,7 @@ static float adaptive_f32(const fconsts* k, float U, float V, int flat, uint32_t
                 ns = h; wu = NU; wv = NV;
             }
             for (int n = 0; n < 3; ++n) {
-                ns = ns - (wu - k->SU) / wv;
+                ns = ns - (wu - k->SU) * (1.0f / wv); /* divf_ */
                 dp5f(U, V, ns, flat, &wu, &wv, &se);
             }
             *steps = it;
@@ -482,7 +482,7 @@ static float geodesic_f32(const fconsts* k, float st, float ct, int adaptive, ui
         }
         return (k->sphere_outside && falling) ? 0.0f : 15.0f;
     }
-    float inv_b2 = (energy * energy) / (rotation * rotation); /* 1/b^2, b = L/E */
+    float inv_b2 = (energy * energy) * (1.0f / (rotation * rotation)); /* 1/b^2, b = L/E (divf_) */
     int barrier = k->rs > 0.0f && inv_b2 < k->barrier;
     if ((k->inside_sphere && !k->sphere_outside) || (!k->outside && k->sphere_outside && energy < 0.0f) ||
         (barrier && k->diff_sides) || (k->r < k->r3_2 && k->inside_sphere && falling) ||
@@ -508,7 +508,7 @@ static float geodesic_f32(const fconsts* k, float st, float ct, int adaptive, ui
                 ns = k->step; wu = NU; wub = NUB;
             }
             for (int n = 0; n < 3; ++n) {
-                ns = ns - (wu - k->SU) / wub;
+                ns = ns - (wu - k->SU) * (1.0f / wub); /* divf_ */
                 float n2 = ns * ns;
                 float n6 = ns * (1.0f / 6.0f);
                 rk4f(U, UB, ns, ns * 0.5f, n2 * 0.25f, n2 * 0.5f, n6, ns * n6, flat, &wu, &wub);
@@ -583,7 +583,7 @@ static void pixel_f32(const geo_frame* f, const fconsts* k, int mode, const floa
     geo_oracle_sincosf(lam, &sl, &cll);
     float ex = cll, ey = 0.0f;
     if (rho2 > 0.0f) {
-        float w = cll / rho2;
+        float w = cll * (1.0f / rho2); /* divf_ */
         ex = c2[0] * w;
         ey = c2[1] * w;
     }

@@ -88,6 +88,20 @@ GEO_HD float rcpf_(float x) {
 #endif
     return 1.0f / x;
 }
+// The quotient of the specification: a times the correctly rounded
+// reciprocal of b (two IEEE roundings, within 1 ulp of a / b).  On gfx950
+// that is rcpf_'s 5 VALU plus one multiply instead of the ≈ 11 of a
+// correctly rounded division; the oracle mirrors it as a * (1.0f / b).
+#ifndef GEO_DIVF
+#define GEO_DIVF 1  // 0: a / b (timing A/B only: not the specification the oracle mirrors)
+#endif
+GEO_HD float divf_(float a, float b) {
+#if GEO_DIVF
+    return a * rcpf_(b);
+#else
+    return a / b;
+#endif
+}
 GEO_HD float clampf_(float x, float lo, float hi) { return x < lo ? lo : (x > hi ? hi : x); }
 // max(a, b) with a NaN `a` mapped to b (used to clamp radicands at 0).
 GEO_HD float fmaxf_(float a, float b) { return a > b ? a : b; }
@@ -135,7 +149,7 @@ GEO_HD float atan2f_(float y, float x) {
     const float num = big ? -ax : (mid ? ay - ax : ay);
     const float den = big ? ay : (mid ? ay + ax : ax);
     const float y0 = big ? kPi2 : (mid ? kPi4 : 0.0f);
-    const float t = den > 0.0f ? num / den : 0.0f;
+    const float t = den > 0.0f ? divf_(num, den) : 0.0f;
     const float z = t * t;
     const float p = fmaf_(fmaf_(fmaf_(8.05374449538e-2f, z, -1.38776856032e-1f), z,
                                 1.99777106478e-1f), z, -3.33329491539e-1f);

@@ -235,7 +235,7 @@ GEO_HD float newton_angle(const PixelConsts& k, float U, float UB, float NU, flo
         wub = NUB;
     }
     for (int n = 0; n < kNewtonIters; ++n) {
-        ns = ns - (wu - k.SU) / wub;
+        ns = ns - divf_(wu - k.SU, wub);
         const float n2 = ns * ns;
         const float n6 = ns * kSixth;
         rk4_step<KIND>(U, UB, ns, ns * 0.5f, n2 * 0.25f, n2 * 0.5f, n6, ns * n6, &wu, &wub);
@@ -265,8 +265,8 @@ GEO_HD bool geodesic_init(const PixelConsts& k, float st, float ct, float* early
                                     : (falling ? k.radial_falling : k.radial_outgoing);
         return false;
     }
-    // 1/b^2 with b = rotation/energy (:61): one division
-    const float inv_b2 = (energy * energy) / (rotation * rotation);
+    // 1/b^2 with b = rotation/energy (:61): one quotient (divf_)
+    const float inv_b2 = divf_(energy * energy, rotation * rotation);
     // pre-filters (:106-119), frame-uniform terms precomputed
     if (k.pf_always | (k.pf_eneg & (energy < 0.0f)) | (k.pf_barrier & (inv_b2 < k.barrier_thresh)) |
         (k.pf_falling & falling) | (k.pf_outgoing & !falling)) {
@@ -355,6 +355,169 @@ GEO_HD uint32_t run_groups(const StopTest<KIND>& stop_at, uint32_t ngroups, uint
     return all;
 }
 
+// run_groups without copies (GEO_PINGPONG): the loop alternates two register
+// sets, group A stepping from X into a_1..a_G and group B from a_G into
+// b_1..b_{G-1}, X, so neither ends with the start-state move of run_groups.
+// Its exit is wave-uniform (every lane done, or the budget): a lane that stops
+// is masked off (`done`) and keeps its stopping group's states in whichever
+// set that group wrote; after the loop one select per state puts them in
+// su_/sb_.  Results equal run_groups' bit for bit.
+#ifndef GEO_PINGPONG
+#define GEO_PINGPONG 1
+#endif
+// The lanes of the wave for which p holds (a uniform SGPR mask), and the
+// rarely taken arm of a branch that must stay a branch: a volatile asm cannot
+// be speculated, so the compiler cannot turn the arm into a select that every
+// group would pay for.
+#if defined(__HIP_DEVICE_COMPILE__)
+GEO_HD uint64_t ballot_(bool p) { return __builtin_amdgcn_ballot_w64(p); }
+#define GEO_RARE() asm volatile("")
+#else
+GEO_HD uint64_t ballot_(bool p) { return p ? 1u : 0u; }
+#define GEO_RARE() ((void)0)
+#endif
+
+template <int G, int KIND>
+GEO_HD void group_steps_(float u, float b, float h, float hh, float hh2, float hhh, float h6, float h2_6,
+                         float (&ou)[G], float (&ob)[G]) {
+#pragma unroll
+    for (int j = 0; j < G; ++j)
+        rk4_step<KIND>(j ? ou[j - 1] : u, j ? ob[j - 1] : b, h, hh, hh2, hhh, h6, h2_6, &ou[j], &ob[j]);
+}
+// The stop flag of a group (its last state where the stop set is absorbing).
+template <int G, int KIND, bool LAST_ONLY>
+GEO_HD bool group_stop_(const StopTest<KIND>& stop_at, const float (&ou)[G], const float (&ob)[G]) {
+    if constexpr (LAST_ONLY) return stop_at(ou[G - 1], ob[G - 1]);
+    bool s = false;
+#pragma unroll
+    for (int j = 0; j < G; ++j) s = s | stop_at(ou[j], ob[j]);
+    return s;
+}
+
+template <int G, int KIND, bool LAST_ONLY>
+GEO_HD uint32_t run_groups_pp(const StopTest<KIND>& stop_at, uint32_t ngroups, uint32_t all, float h, float hh,
+                              float hh2, float hhh, float h6, float h2_6, float (&su_)[G + 1], float (&sb_)[G + 1]) {
+    float xu = su_[0], xb = sb_[0];  // X: group A's start, group B's end
+    float au[G], ab[G], bu[G], bb[G];  // a_1..a_G; b_1..b_{G-1} (b_G is X)
+#pragma unroll
+    for (int j = 0; j < G; ++j) {
+        au[j] = bu[j] = xu;
+        ab[j] = bb[j] = xb;
+    }
+    bool done = false, in_b = false;  // in_b: stopped in a B group
+    bool last_b = false;              // wave-uniform: the last group run was a B group
+    uint64_t live = ballot_(true);    // wave-uniform: the lanes still integrating
+    uint32_t it = all;
+    // The stop test runs outside the `if (!done)` regions, on every lane: its
+    // ballot is then the compare mask itself (a flag merged out of the region
+    // would be rematerialised by two VALU ops per group).  A finished lane's
+    // flag is garbage but harmless: `live` only ever loses bits.
+    for (uint32_t q = 0; q < ngroups;) {
+        if (!done) group_steps_<G, KIND>(xu, xb, h, hh, hh2, hhh, h6, h2_6, au, ab);
+        bool hit = group_stop_<G, KIND, LAST_ONLY>(stop_at, au, ab);
+        live &= ~ballot_(hit);
+        if (hit && !done) {
+            GEO_RARE();
+            done = true;
+            it = q * (uint32_t)G;
+        }
+        last_b = false;
+        if (++q >= ngroups || live == 0) break;
+        if (!done) {
+            float ou[G], ob[G];
+            group_steps_<G, KIND>(au[G - 1], ab[G - 1], h, hh, hh2, hhh, h6, h2_6, ou, ob);
+#pragma unroll
+            for (int j = 0; j < G - 1; ++j) {
+                bu[j] = ou[j];
+                bb[j] = ob[j];
+            }
+            xu = ou[G - 1];
+            xb = ob[G - 1];
+        }
+        float tu[G], tb[G];
+#pragma unroll
+        for (int j = 0; j < G - 1; ++j) {
+            tu[j] = bu[j];
+            tb[j] = bb[j];
+        }
+        tu[G - 1] = xu;
+        tb[G - 1] = xb;
+        hit = group_stop_<G, KIND, LAST_ONLY>(stop_at, tu, tb);
+        live &= ~ballot_(hit);
+        if (hit && !done) {
+            GEO_RARE();
+            done = true;
+            in_b = true;
+            it = q * (uint32_t)G;
+        }
+        last_b = true;
+        if (++q >= ngroups || live == 0) break;
+    }
+    // a lane on the budget continues from the last group's end state, which
+    // sits where a B group's start state (a_G) or an A group's (X) does
+    if (!done) in_b = !last_b;
+    su_[0] = in_b ? au[G - 1] : xu;
+    sb_[0] = in_b ? ab[G - 1] : xb;
+#pragma unroll
+    for (int j = 0; j < G - 1; ++j) {
+        su_[j + 1] = in_b ? bu[j] : au[j];
+        sb_[j + 1] = in_b ? bb[j] : ab[j];
+    }
+    su_[G] = in_b ? xu : au[G - 1];
+    sb_[G] = in_b ? xb : ab[G - 1];
+    return it;
+}
+
+// After the group loop (run_groups): from the G + 1 states of the lane's
+// stopping group and `it` = the steps before it (or the whole-group budget),
+// the first stopping step, the budget tail of fewer than G steps, the
+// crossing test and Newton (sphere_ray_tracer.rs:150-191).  *steps =
+// executed main-loop RK4 steps.
+template <int G, int KIND>
+GEO_HD float geodesic_finish(const PixelConsts& k, const StopTest<KIND>& stop_at, uint32_t it, float (&su_)[G + 1],
+                             float (&sb_)[G + 1], uint32_t* steps) {
+    const uint32_t ms = k.max_steps;
+    // Opaque copies: the per-step flags are recomputed from the state rather
+    // than carried out of the loop as lane masks.
+#pragma unroll
+    for (int j = 0; j <= G; ++j) {
+        GEO_OPAQUE(su_[j]);
+        GEO_OPAQUE(sb_[j]);
+    }
+    GEO_OPAQUE(it);
+    float ou = su_[0], oub = sb_[0], nu = su_[0], nub = sb_[0];
+    if (it + (uint32_t)G <= ms) {
+        // stopped inside the group: the first step j whose flag holds
+        bool found = false;
+#pragma unroll
+        for (int j = 0; j < G; ++j) {
+            const bool sj = !found && stop_at(su_[j + 1], sb_[j + 1]);
+            if (sj) {
+                ou = su_[j]; oub = sb_[j]; nu = su_[j + 1]; nub = sb_[j + 1];
+                it += (uint32_t)j + 1u;
+            }
+            found = found | sj;
+        }
+    } else {
+        // budget exit: fewer than G steps left, one test per step
+        float cu = su_[0], cb = sb_[0];
+        for (uint32_t r = it; r < ms; ++r) {
+            rk4_step<KIND>(cu, cb, k.step, k.hh, k.hh2, k.hhh, k.h6, k.h2_6, &nu, &nub);
+            ou = cu;
+            oub = cb;
+            ++it;
+            if (stop_at(nu, nub)) break;
+            cu = nu;
+            cb = nub;
+            ou = nu;  // no crossing if the budget ends here
+            oub = nub;
+        }
+    }
+    *steps = it;
+    if ((nu > k.SU) == (ou > k.SU)) return kNoValue;  // stopped without a crossing
+    return newton_angle<KIND>(k, ou, oub, nu, nub, it);
+}
+
 // Traveled angle of the ray at angle theta to the black hole, or kNoValue.
 // *steps = executed main-loop RK4 steps.  LOOP = RK4 steps per exit test
 // (tools/ubench/loop_ab.hip), KIND the integration kind (geodesic_kind).
@@ -363,7 +526,6 @@ GEO_HD float geodesic_angle_v(const PixelConsts& k, float st, float ct, uint32_t
     *steps = 0;
     float U, UB, early;
     if (!geodesic_init(k, st, ct, &early, &U, &UB)) return early;
-    const float SU = k.SU;
     float h = k.step, hh = k.hh, hh2 = k.hh2, hhh = k.hhh, h6 = k.h6, h2_6 = k.h2_6;
     // Main loop (:134-191), restructured for the wave64 VALU: per step the
     // lane-exit flag is StopTest (crossing | escape | horizon); the budget
@@ -399,51 +561,22 @@ GEO_HD float geodesic_angle_v(const PixelConsts& k, float st, float ct, uint32_t
     }
     // per lane: steps before its stopping group (budget: all)
     uint32_t it;
+#if GEO_PINGPONG
+    if (stop_at.absorbing)  // frame-uniform
+        it = run_groups_pp<G, KIND, GEO_ABSORBING_TEST != 0>(stop_at, ngroups, ngroups * (uint32_t)G, h, hh, hh2,
+                                                             hhh, h6, h2_6, su_, sb_);
+    else
+        it = run_groups_pp<G, KIND, false>(stop_at, ngroups, ngroups * (uint32_t)G, h, hh, hh2, hhh, h6, h2_6,
+                                           su_, sb_);
+#else
     if (stop_at.absorbing)  // frame-uniform
         it = run_groups<G, KIND, GEO_ABSORBING_TEST != 0>(stop_at, ngroups, ngroups * (uint32_t)G, h, hh, hh2, hhh,
                                                           h6, h2_6, su_, sb_);
     else
         it = run_groups<G, KIND, false>(stop_at, ngroups, ngroups * (uint32_t)G, h, hh, hh2, hhh, h6, h2_6, su_,
                                         sb_);
-    // Opaque copies: the per-step flags are recomputed from the state rather
-    // than carried out of the loop as lane masks.
-#pragma unroll
-    for (int j = 0; j <= G; ++j) {
-        GEO_OPAQUE(su_[j]);
-        GEO_OPAQUE(sb_[j]);
-    }
-    GEO_OPAQUE(it);
-    float ou = su_[0], oub = sb_[0], nu = su_[0], nub = sb_[0];
-    if (it + (uint32_t)G <= ms) {
-        // stopped inside the group: the first step j whose flag holds
-        bool found = false;
-#pragma unroll
-        for (int j = 0; j < G; ++j) {
-            const bool sj = !found && stop_at(su_[j + 1], sb_[j + 1]);
-            if (sj) {
-                ou = su_[j]; oub = sb_[j]; nu = su_[j + 1]; nub = sb_[j + 1];
-                it += (uint32_t)j + 1u;
-            }
-            found = found | sj;
-        }
-    } else {
-        // budget exit: fewer than G steps left, one test per step
-        float cu = su_[0], cb = sb_[0];
-        for (uint32_t r = it; r < ms; ++r) {
-            rk4_step<KIND>(cu, cb, h, hh, hh2, hhh, h6, h2_6, &nu, &nub);
-            ou = cu;
-            oub = cb;
-            ++it;
-            if (stop_at(nu, nub)) break;
-            cu = nu;
-            cb = nub;
-            ou = nu;  // no crossing if the budget ends here
-            oub = nub;
-        }
-    }
-    *steps = it;
-    if ((nu > SU) == (ou > SU)) return kNoValue;  // stopped without a crossing
-    return newton_angle<KIND>(k, ou, oub, nu, nub, it);
+#endif
+    return geodesic_finish<G, KIND>(k, stop_at, it, su_, sb_, steps);
 }
 
 #ifndef GEO_LOOP_VARIANT
@@ -557,7 +690,7 @@ GEO_HD float geodesic_angle_adaptive(const PixelConsts& k, float st, float ct, u
         ns = h; wu = NU; wv = NV;
     }
     for (int n = 0; n < kNewtonIters; ++n) {
-        ns = ns - (wu - k.SU) / wv;
+        ns = ns - divf_(wu - k.SU, wv);
         float se;
         dp5_step<KIND>(U, V, ns, ns * ns, &wu, &wv, &se);
     }
@@ -621,7 +754,7 @@ GEO_HD void sky_uv(const float* m2, float c2x, float c2y, float rho, float lam, 
     // to_cart(phi, lam) with (cos phi, sin phi) = (c2x, c2y)/rho
     float ex = cl, ey = 0.0f;
     if (rho > 0.0f) {
-        const float w = cl / rho;
+        const float w = divf_(cl, rho);
         ex = c2x * w;
         ey = c2y * w;
     }

@@ -100,6 +100,36 @@ struct PaddedSkyQuad {
     }
 };
 
+// Epilogue of one pixel (shader.wgsl:88-105): black-hole test, sky UV,
+// bilinear sample, blend and the optional outputs at index o.
+__device__ __forceinline__ void shade_pixel(const RenderArgs& a, float c2x, float c2y, float ct, float lam,
+                                            uint32_t steps, size_t o) {
+    const bool bh = lam < geo::kBlackHoleLambda;
+    // A black-hole pixel is discarded (shader.wgsl:88): it needs its UV
+    // only when the caller asks for it, so a wave inside the shadow skips
+    // the sincos/atan2/asin and the sample (GEO_BH_SKIP_UV 0: always compute)
+    float U = 0.0f, V = 0.0f;
+#if GEO_BH_SKIP_UV
+    if (!bh || a.out_uv)
+#endif
+        geo::sky_uv(a.frame.central_to_uv, c2x, c2y, ct, lam, &U, &V);
+    const PaddedSkyQuad quad{__builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(a.sky), 0,
+                                                               (int)a.sky_bytes, kBufferRsrcWord3),
+                             a.sky_pitch_b};
+    if (a.composite) {
+        // over the previous spheres; a discarded pixel keeps the target
+        if (!bh) {
+            const uint32_t s = geo::sample_sky_quad(quad, a.sky_w, a.sky_h, U, V);
+            a.out_rgba[o] = a.sky_opaque ? s : geo::composite_(s, a.out_rgba[o]);
+        }
+    } else {
+        a.out_rgba[o] = bh ? geo::kBlackRGBA : geo::sample_sky_q(quad, a.sky_w, a.sky_h, a.sky_opaque != 0, U, V);
+    }
+    if (a.out_mask) a.out_mask[o] = bh ? 1 : 0;
+    if (a.out_uv) a.out_uv[o] = make_float2(U, V);
+    if (a.out_steps) a.out_steps[o] = steps;
+}
+
 template <int MODE, int KIND>
 __global__ __launch_bounds__(kBlock) void geo_render_kernel(const RenderArgs a) {
     __shared__ float s_fan[MODE == GEO_MODE_FAN ? kMaxFan : 1];
@@ -132,31 +162,7 @@ __global__ __launch_bounds__(kBlock) void geo_render_kernel(const RenderArgs a) 
         } else {
             lam = geo::kPi2 - geo::geodesic_angle_v<GEO_LOOP_VARIANT, KIND>(a.k, st, ct, &steps);
         }
-        const bool bh = lam < geo::kBlackHoleLambda;
-        // A black-hole pixel is discarded (shader.wgsl:88): it needs its UV
-        // only when the caller asks for it, so a wave inside the shadow skips
-        // the sincos/atan2/asin and the sample (GEO_BH_SKIP_UV 0: always compute)
-        float U = 0.0f, V = 0.0f;
-#if GEO_BH_SKIP_UV
-        if (!bh || a.out_uv)
-#endif
-            geo::sky_uv(a.frame.central_to_uv, c2x, c2y, ct, lam, &U, &V);
-        const PaddedSkyQuad quad{__builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(a.sky), 0,
-                                                                   (int)a.sky_bytes, kBufferRsrcWord3),
-                                 a.sky_pitch_b};
-        const size_t o = (size_t)ly * a.width + px;
-        if (a.composite) {
-            // over the previous spheres; a discarded pixel keeps the target
-            if (!bh) {
-                const uint32_t s = geo::sample_sky_quad(quad, a.sky_w, a.sky_h, U, V);
-                a.out_rgba[o] = a.sky_opaque ? s : geo::composite_(s, a.out_rgba[o]);
-            }
-        } else {
-            a.out_rgba[o] = bh ? geo::kBlackRGBA : geo::sample_sky_q(quad, a.sky_w, a.sky_h, a.sky_opaque != 0, U, V);
-        }
-        if (a.out_mask) a.out_mask[o] = bh ? 1 : 0;
-        if (a.out_uv) a.out_uv[o] = make_float2(U, V);
-        if (a.out_steps) a.out_steps[o] = steps;
+        shade_pixel(a, c2x, c2y, ct, lam, steps, (size_t)ly * a.width + px);
     }
     if constexpr (MODE != GEO_MODE_FAN) {
         if (a.step_slots) {

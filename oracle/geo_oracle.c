@@ -544,15 +544,40 @@ static inline void m3vf(const float* m, float x, float y, float z, float* o) {
 }
 
 
-static void pixel_f32(const geo_frame* f, const fconsts* k, int mode, const float* fan, uint32_t n_fan,
+typedef struct {
+    float a[3], b[3], c[3]; /* d = py a + px b + c */
+    int m1_identity;
+} cam_f32;
+
+static cam_f32 camera_f32(const geo_frame* f, uint32_t width, uint32_t height) {
+    const float* m0 = f->display_to_movement;
+    const float* m1 = f->movement_to_central;
+    cam_f32 cc;
+    double w = (double)width, h = (double)height;
+    double sx = 2.0 / w, ox = (1.0 - w) / w, sy = -2.0 / h, oy = (h - 1.0) / h;
+    for (int i = 0; i < 3; ++i) {
+        double p = -(double)m0[12] * (double)m0[i];
+        double q = -(double)m0[13] * (double)m0[4 + i];
+        double r = (double)m0[14] * (double)m0[8 + i];
+        cc.a[i] = (float)(sy * p);
+        cc.b[i] = (float)(sx * q);
+        cc.c[i] = (float)((oy * p + ox * q) + r);
+    }
+    cc.m1_identity = m1[0] == 1.0f && m1[1] == 0.0f && m1[2] == 0.0f && m1[4] == 0.0f && m1[5] == 1.0f &&
+                     m1[6] == 0.0f && m1[8] == 0.0f && m1[9] == 0.0f && m1[10] == 1.0f;
+    return cc;
+}
+
+static void pixel_f32(const geo_frame* f, const cam_f32* cam, const fconsts* k, int mode, const float* fan, uint32_t n_fan,
                       const uint32_t* sky, uint32_t sw, uint32_t sh, int opaque, int composite, uint32_t width,
                       uint32_t height, uint32_t px, uint32_t py, uint32_t* rgba, uint8_t* bh_out, float* uv,
                       uint32_t* steps) {
-    const float* m0 = f->display_to_movement;
-    float nx = ((float)(2u * px + 1u) - (float)width) * (1.0f / (float)width);
-    float ny = ((float)height - (float)(2u * py + 1u)) * (1.0f / (float)height);
+    /* camera ray (shader.wgsl:60-64): d = M0 (-ny M0[12], -nx M0[13], M0[14]) with the pixel-centre NDC
+     * nx = (2 px + 1 - W)/W, ny = (H - 2 py - 1)/H, affine in (px, py): d = py A + px B + C, the frame
+     * constants in f64 rounded once to f32 (cam_f32) */
+    const cam_f32* cc = cam;
     float d[3];
-    m3vf(m0, -ny * m0[12], -nx * m0[13], m0[14], d);
+    for (int i = 0; i < 3; ++i) d[i] = fmaf((float)py, cc->a[i], fmaf((float)px, cc->b[i], cc->c[i]));
     /* aberration (shader.wgsl:69-70) as a boost along z on the unnormalised ray */
     float kk = f->psi_factor_and_position[0];
     float kt = sqrtf(fmaf(-kk, kk, 1.0f));
@@ -560,7 +585,12 @@ static void pixel_f32(const geo_frame* f, const fconsts* k, int mode, const floa
     float id = 1.0f / fmaf(-kk, d[2], len);
     float g = kt * id;
     float c2[3];
-    m3vf(f->movement_to_central, d[0] * g, d[1] * g, fmaf(-kk, len, d[2]) * id, c2);
+    float e[3] = {d[0] * g, d[1] * g, fmaf(-kk, len, d[2]) * id};
+    if (cc->m1_identity) { /* movement_to_central = I (observer.rs:243-246): skipped, -0 stays -0 */
+        c2[0] = e[0]; c2[1] = e[1]; c2[2] = e[2];
+    } else {
+        m3vf(f->movement_to_central, e[0], e[1], e[2], c2);
+    }
     float st = clampf(c2[2], -1.0f, 1.0f);
     float rho2 = sqrtf(fmaf(c2[1], c2[1], c2[0] * c2[0])); /* cos theta */
     float lam;
@@ -648,6 +678,7 @@ typedef struct {
     const geo_frame* f;
     const geo_scene* s;
     fconsts k;
+    cam_f32 cam;
     const float* fan;
     uint32_t n_fan;
     const uint32_t* sky;
@@ -673,7 +704,7 @@ static void* job_f32(void* arg) {
             uint8_t bh;
             float uv[2];
             memcpy(&rgba, j->rgba + 4 * o, 4); /* the target, for GEO_FLAG_COMPOSITE */
-            pixel_f32(j->f, &j->k, (int)j->s->mode, j->fan, j->n_fan, j->sky, j->sw, j->sh, j->opaque,
+            pixel_f32(j->f, &j->cam, &j->k, (int)j->s->mode, j->fan, j->n_fan, j->sky, j->sw, j->sh, j->opaque,
                       (j->s->flags & GEO_FLAG_COMPOSITE) != 0, j->width, j->height, px, py, &rgba, &bh, uv, &st);
             memcpy(j->rgba + 4 * o, &rgba, 4);
             if (j->mask) j->mask[o] = bh;
@@ -757,6 +788,7 @@ int geo_oracle_render_f32(const geo_frame* f, const geo_scene* s, const float* f
     j.f = f;
     j.s = s;
     j.k = make_fconsts(s);
+    j.cam = camera_f32(f, width, height);
     j.fan = fan;
     j.n_fan = n_fan;
     j.sky = (const uint32_t*)sky;

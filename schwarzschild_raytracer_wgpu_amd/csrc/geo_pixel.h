@@ -706,30 +706,67 @@ GEO_HD void mat3_mul(const float* m, float x, float y, float z, float* ox, float
 
 // shader.wgsl:60-75 — pixel (px, py) of a width x height frame to the
 // direction in the black-hole-central frame (unit up to rounding).
+//
+// Camera ray (:60-64): the pixel centre's NDC, nx = (2 px + 1 - W)/W and
+// ny = (H - 2 py - 1)/H (full-screen quad, basic_sphere_buffer.rs:63-83),
+// scaled by the FOV column w and rotated by display_to_movement's 3 x 3 part:
+//   d = M0 (-ny M0[12], -nx M0[13], M0[14]) = py A + px B + C,
+// affine in the integer pixel coordinates.  A, B, C are frame constants
+// (CameraConsts, evaluated in f64 and rounded once to f32, on the host), so
+// a pixel's ray is two FMAs per component.
+//
 // The aberration (:69-70), sin(l') = (s - k)/(1 - s k) with phi kept, is
 // applied as the boost along z it is: for the unnormalised ray d, |d| = L,
 //   e_z = (d_z - k L)/(L - k d_z),   e_xy = d_xy sqrt(1 - k^2)/(L - k d_z),
-// (|e| = 1), so steps 2-5 need one sqrt, one division and no
+// (|e| = 1), so steps 2-5 need one sqrt, one reciprocal and no
 // transcendental.  kt = sqrt(1 - k^2) is a frame constant (aberration_kt).
-// inv_w = 1/width, inv_h = 1/height (f32, rounded once).
+// movement_to_central (:72-74) is skipped where it is exactly the identity
+// (the Unmoving and FrozenFall states, observer.rs:243-246): a product with
+// it can turn -0 into +0, so the skip is part of the specification.
 GEO_HD float aberration_kt(float psi_k) { return __builtin_sqrtf(fmaf_(-psi_k, psi_k, 1.0f)); }
 
-GEO_HD void pixel_central_dir(const float* m0, const float* m1, float psi_k, float kt, uint32_t width,
-                              uint32_t height, float inv_w, float inv_h, uint32_t px, uint32_t py,
-                              float* c2x, float* c2y, float* c2z) {
-    const float nx = ((float)(2u * px + 1u) - (float)width) * inv_w;
-    const float ny = ((float)height - (float)(2u * py + 1u)) * inv_h;
-    // carthesic = (-pos.y, -pos.x, 1, 0) * screen_to_movement.w (:60-63)
-    const float cx = -ny * m0[12];
-    const float cy = -nx * m0[13];
-    const float cz = m0[14];
-    float dx, dy, dz;
-    mat3_mul(m0, cx, cy, cz, &dx, &dy, &dz);
+struct CameraConsts {
+    float a[3], b[3], c[3];  // d = py a + px b + c
+    bool m1_identity;        // movement_to_central's 3 x 3 part is exactly the identity
+};
+
+// Host (f64, then one rounding per constant; the oracle evaluates the same
+// expressions).  m0 = display_to_movement, m1 = movement_to_central.
+GEO_HD CameraConsts camera_consts(const float* m0, const float* m1, uint32_t width, uint32_t height) {
+    CameraConsts cc;
+    const double w = (double)width, h = (double)height;
+    const double sx = 2.0 / w, ox = (1.0 - w) / w;   // nx = px sx + ox
+    const double sy = -2.0 / h, oy = (h - 1.0) / h;  // ny = py sy + oy
+    for (int i = 0; i < 3; ++i) {
+        const double p = -(double)m0[12] * (double)m0[i];     // d_i's ny coefficient
+        const double q = -(double)m0[13] * (double)m0[4 + i]; // d_i's nx coefficient
+        const double r = (double)m0[14] * (double)m0[8 + i];
+        cc.a[i] = (float)(sy * p);
+        cc.b[i] = (float)(sx * q);
+        cc.c[i] = (float)((oy * p + ox * q) + r);
+    }
+    cc.m1_identity = m1[0] == 1.0f && m1[1] == 0.0f && m1[2] == 0.0f && m1[4] == 0.0f && m1[5] == 1.0f &&
+                     m1[6] == 0.0f && m1[8] == 0.0f && m1[9] == 0.0f && m1[10] == 1.0f;
+    return cc;
+}
+
+GEO_HD void pixel_central_dir(const CameraConsts& cc, const float* m1, float psi_k, float kt, uint32_t px,
+                              uint32_t py, float* c2x, float* c2y, float* c2z) {
+    const float fx = (float)px, fy = (float)py;
+    const float dx = fmaf_(fy, cc.a[0], fmaf_(fx, cc.b[0], cc.c[0]));
+    const float dy = fmaf_(fy, cc.a[1], fmaf_(fx, cc.b[1], cc.c[1]));
+    const float dz = fmaf_(fy, cc.a[2], fmaf_(fx, cc.b[2], cc.c[2]));
     const float len = sqrtf_(fmaf_(dz, dz, fmaf_(dy, dy, dx * dx)));
     const float id = rcpf_(fmaf_(-psi_k, dz, len));
     const float g = kt * id;
-    // to_cart, then movement_to_central (:72-74)
-    mat3_mul(m1, dx * g, dy * g, fmaf_(-psi_k, len, dz) * id, c2x, c2y, c2z);
+    const float ex = dx * g, ey = dy * g, ez = fmaf_(-psi_k, len, dz) * id;
+    if (cc.m1_identity) {
+        *c2x = ex;
+        *c2y = ey;
+        *c2z = ez;
+    } else {
+        mat3_mul(m1, ex, ey, ez, c2x, c2y, c2z);  // to_cart, then movement_to_central (:72-74)
+    }
 }
 
 // Fan lookup (shader.wgsl:77-84); i+1 clamped to n-1 (weight 0 there).

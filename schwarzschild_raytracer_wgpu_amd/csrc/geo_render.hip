@@ -53,7 +53,8 @@ struct RenderArgs {
     uint32_t band_rows, band_magic, band_stride;
     uint32_t sky_opaque;
     uint32_t composite;  // GEO_FLAG_COMPOSITE
-    float inv_w, inv_h, kt;
+    geo::CameraConsts cam;  // the pixel's camera ray, frame constants (geo::camera_consts)
+    float kt;
     const uint32_t* sky;  // padded (geo::pad_sky): (sky_w + 2) x (sky_h + 2) texels
     uint32_t sky_w, sky_h;
     uint32_t sky_pitch_b, sky_bytes;
@@ -149,9 +150,8 @@ __global__ __launch_bounds__(kBlock) void geo_render_kernel(const RenderArgs a) 
     uint32_t steps = 0;
     if (px < a.width && ly < a.nrows && py < a.height) {
         float c2x, c2y, c2z;
-        geo::pixel_central_dir(a.frame.display_to_movement, a.frame.movement_to_central,
-                               a.frame.psi_factor_and_position[0], a.kt, a.width, a.height, a.inv_w,
-                               a.inv_h, px, py, &c2x, &c2y, &c2z);
+        geo::pixel_central_dir(a.cam, a.frame.movement_to_central, a.frame.psi_factor_and_position[0], a.kt, px, py,
+                               &c2x, &c2y, &c2z);
         const float st = geo::clampf_(c2z, -1.0f, 1.0f);
         const float ct = geo::central_rho(c2x, c2y);
         float lam;
@@ -601,8 +601,7 @@ static int render_impl(geo_ctx* c, const geo_frame* frame, const geo_scene* scen
     a.sky_opaque = c->sky_opaque ? 1u : 0u;
     a.composite = (scene->flags & GEO_FLAG_COMPOSITE) ? 1u : 0u;
     const uint32_t tiles_x = (width + kTileW - 1) / kTileW;
-    a.inv_w = 1.0f / (float)width;
-    a.inv_h = 1.0f / (float)height;
+    a.cam = geo::camera_consts(frame->display_to_movement, frame->movement_to_central, width, height);
     a.kt = geo::aberration_kt(frame->psi_factor_and_position[0]);
     const uint32_t tiles_y = (nrows + kTileH - 1) / kTileH;
     a.sky = c->sky;

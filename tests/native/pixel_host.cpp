@@ -31,13 +31,13 @@ extern "C" int host_render(const geo_frame* f, const geo_scene* s, const float* 
     const geo::PixelConsts k = geo::make_consts(s->rs, s->sphere_r, s->r_obs, s->step, s->max_steps, s->tol);
     bool opaque = true;
     for (size_t i = 0; i < (size_t)sw * sh; ++i) opaque = opaque && (sky[i] >> 24) == 255u;
-    const float inv_w = 1.0f / (float)width, inv_h = 1.0f / (float)height;
+    const geo::CameraConsts cam = geo::camera_consts(f->display_to_movement, f->movement_to_central, width, height);
     for (uint32_t ly = 0; ly < nrows; ++ly) {
         const uint32_t py = row0 + ly;
         for (uint32_t px = 0; px < width; ++px) {
             float c2x, c2y, c2z;
-            geo::pixel_central_dir(f->display_to_movement, f->movement_to_central, f->psi_factor_and_position[0],
-                                   geo::aberration_kt(f->psi_factor_and_position[0]), width, height, inv_w, inv_h, px, py, &c2x, &c2y, &c2z);
+            geo::pixel_central_dir(cam, f->movement_to_central, f->psi_factor_and_position[0],
+                                   geo::aberration_kt(f->psi_factor_and_position[0]), px, py, &c2x, &c2y, &c2z);
             const float st = geo::clampf_(c2z, -1.0f, 1.0f);
             const float ct = geo::central_rho(c2x, c2y);
             uint32_t n = 0;

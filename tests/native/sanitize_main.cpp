@@ -50,12 +50,12 @@ static int render_check(double px_, double py_, double pz_, float rs, uint32_t m
     const geo::PixelConsts k = geo::make_consts(s.rs, s.sphere_r, s.r_obs, s.step, s.max_steps, s.tol);
     const uint32_t* skyp = reinterpret_cast<const uint32_t*>(sky.data());
     int bad = 0;
+    const geo::CameraConsts cam = geo::camera_consts(f.display_to_movement, f.movement_to_central, W, H);
     for (uint32_t py = 0; py < H; ++py)
         for (uint32_t px = 0; px < W; ++px) {
             float c2x, c2y, c2z;
-            geo::pixel_central_dir(f.display_to_movement, f.movement_to_central, f.psi_factor_and_position[0],
-                                   geo::aberration_kt(f.psi_factor_and_position[0]), W, H, 1.0f / W, 1.0f / H, px,
-                                   py, &c2x, &c2y, &c2z);
+            geo::pixel_central_dir(cam, f.movement_to_central, f.psi_factor_and_position[0],
+                                   geo::aberration_kt(f.psi_factor_and_position[0]), px, py, &c2x, &c2y, &c2z);
             const float st = geo::clampf_(c2z, -1.0f, 1.0f), ct = geo::central_rho(c2x, c2y);
             uint32_t n = 0;
             const float lam = geo::kPi2 - angle_for(k, mode, st, ct, &n);

@@ -32,6 +32,7 @@ res = {
     "derived": {
         "clock_ghz": xcd_cycles / dur_ns,
         "valu_issue_utilisation": c["SQ_INSTS_VALU"] * 2.0 / 1024.0 / xcd_cycles,
+        "valu_per_simd_cycle": c["SQ_INSTS_VALU"] / 1024.0 / xcd_cycles,
         "salu_per_cu_cycle": c["SQ_INSTS_SALU"] / 256.0 / xcd_cycles,
         "lane_utilisation": c.get("SQ_THREAD_CYCLES_VALU", 0) / (64.0 * c["SQ_INSTS_VALU"]),
         "hw_fp32_flops": c.get("SQ_INSTS_VALU_FLOPS_FP32", 0) * 64.0,

@@ -51,8 +51,11 @@ def parse():
     p.add_argument("--config", default="cfg3_4k")
     p.add_argument("--band-rows", type=int, default=8)
     p.add_argument("--render-streams", type=int, default=None,
-                   help="render streams (1 or 2; default 1 at N = 1, 2 at N > 1: the next frame's waves fill "
-                        "the tail of a rank's small share)")
+                   help="render streams (1 or 2; default 1 at N = 1, 2 at N > 1): with 2, frame i+1's waves fill "
+                        "frame i's tail (a rank's share at N = 8 is only ~2 waves per slot) and the per-launch "
+                        "kernel time is measured on 20 back-to-back launches on one stream after the timed region. "
+                        "N = 1 keeps one stream so that in-region launch times and rocprofv3's agree; the two-stream "
+                        "throughput is reported beside it (`pipelined`)")
     p.add_argument("--frames-per-gather", type=int, default=8,
                    help="N > 1: frames per RCCL gather to rank 0 (amortises the ~34 us host cost of a gather; "
                         "rank 0 reassembles each batch with one geo_assemble_lead launch)")
@@ -249,13 +252,35 @@ def main():
         dist.barrier()
     elapsed_compute = time.perf_counter() - c0
     ctx.steps_flush(torch.zeros(1, dtype=torch.int64, device=dev))  # discard this pass's steps
+    # N = 1, informational: the same K frames with two render streams, so
+    # that frame i+1's waves fill frame i's tail (what a frame loop gains
+    # from pipelining; not the metric's value, whose launches do not overlap)
+    pipelined = None
+    if world == 1 and sf.S == 1:
+        sf2 = ShardedFrame(ctx, frame, scene, W, H, args.band_rows, rank, world, dev, None, render_streams=2)
+        spin_up(sf2, max(100, args.warmup))  # its buffers' allocation idled the GPU
+        torch.cuda.synchronize()
+        p0 = time.perf_counter()
+        for i in range(args.steps):
+            sf2.step(i, scene=scene_defer)
+        sf2.drain()
+        torch.cuda.synchronize()
+        el2 = time.perf_counter() - p0
+        ctx.steps_flush(torch.zeros(1, dtype=torch.int64, device=dev))  # discard this pass's steps
+        pipelined = {"render_streams": 2, "ms_per_step": el2 / args.steps * 1e3,
+                     "value": steps_diag * args.steps / el2,
+                     "what": "the same K frames on two render streams (consecutive frames overlap); informational"}
+        del sf2
     if sf.S > 1:
+        # one launch at a time: 20 launches back to back on ONE stream (no
+        # overlap, and no idle gap between them that would let the clock
+        # drop), an event pair around each, one sync at the end
         iso = [(HipEvent(), HipEvent()) for _ in range(20)]
         for a, b in iso:
             a.record()
             sf.render_local(sf.bufs[0], scene=scene_defer)
             b.record()
-            torch.cuda.synchronize()
+        torch.cuda.synchronize()
         ctx.steps_flush(torch.zeros(1, dtype=torch.int64, device=dev))  # discard the isolated launches' steps
         evs = {i: ab for i, ab in enumerate(iso)}
     kernel_ms = sorted(a.elapsed_time(b) for a, b in evs.values())
@@ -343,8 +368,10 @@ def main():
         "kernel_ms": {"avg": kernel_ms_avg, "median": kernel_ms[len(kernel_ms) // 2], "min": kernel_ms[0],
                       "max_over_ranks_avg": kernel_ms_max, "frames_timed": len(kernel_ms),
                       "events": ("hipEventDisableSystemFence pairs on every %d-th timed frame" % args.event_every
-                                 if sf.S == 1 else "hipEventDisableSystemFence pairs on 20 isolated launches after "
-                                 "the timed region (%d render streams overlap launches inside it)" % sf.S)},
+                                 if sf.S == 1 else "hipEventDisableSystemFence pairs on 20 launches back to back on "
+                                 "one stream after the timed region (%d render streams overlap consecutive frames "
+                                 "inside it)" % sf.S)},
+        "pipelined": pipelined,
         "compute_only": {"value": total_steps / compute_max, "ms_per_step": compute_max / args.steps * 1e3,
                          "what": "the same K frames rendered on the same streams without pack, gather or "
                                  "reassembly (max over ranks)"},

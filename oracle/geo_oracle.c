@@ -298,7 +298,7 @@ float geo_oracle_atan2f(float y, float x) {
 typedef struct {
     float rs, sphere_r, r, step;
     uint32_t max_steps;
-    float hh, h6, hh2, hhh, h2_6, r3_2, sphere_u, schwarz_u, u0, h_over_r2, bound, e_out, e_in, barrier;
+    float hh, h6, hh2, hhh, h2_6, r3_2, sphere_u, schwarz_u, u0, h_over_r2, inv_r2, bound, e_out, e_in, barrier;
     int r_inside_h, outside, sphere_outside, inside_sphere, diff_sides, rs_nonzero;
     float scale, U0, SU, BD, HU; /* scaled state U = scale*u */
     float tolU, tolG, hmax;      /* GEO_MODE_ADAPTIVE step control */
@@ -321,6 +321,7 @@ static fconsts make_fconsts(const geo_scene* s) {
     k.schwarz_u = 1.0f / k.rs;
     k.u0 = 1.0f / k.r;
     k.h_over_r2 = (1.0f - k.rs / k.r) / (k.r * k.r);
+    k.inv_r2 = 1.0f / (k.r * k.r);
     float mx = k.sphere_r > k.r3_2 ? k.sphere_r : k.r3_2;
     float um = 1.0f / mx;
     k.bound = 0.9f * (k.u0 < um ? k.u0 : um);
@@ -459,7 +460,7 @@ static float adaptive_f32(const fconsts* k, float U, float V, int flat, uint32_t
     return 15.0f;
 }
 
-static float geodesic_f32(const fconsts* k, float st, float ct, int adaptive, uint32_t* steps) {
+static float geodesic_f32(const fconsts* k, float st, float ct, float rct, int adaptive, uint32_t* steps) {
     *steps = 0;
     float rotation = k->r * ct;
     int falling;
@@ -482,7 +483,8 @@ static float geodesic_f32(const fconsts* k, float st, float ct, int adaptive, ui
         }
         return (k->sphere_outside && falling) ? 0.0f : 15.0f;
     }
-    float inv_b2 = (energy * energy) * (1.0f / (rotation * rotation)); /* 1/b^2, b = L/E (divf_) */
+    /* 1/b^2, b = L/E = r ct/E, from the pixel's rct = 1/ct (shared with its sky direction) */
+    float inv_b2 = (energy * energy) * ((rct * rct) * k->inv_r2);
     int barrier = k->rs > 0.0f && inv_b2 < k->barrier;
     if ((k->inside_sphere && !k->sphere_outside) || (!k->outside && k->sphere_outside && energy < 0.0f) ||
         (barrier && k->diff_sides) || (k->r < k->r3_2 && k->inside_sphere && falling) ||
@@ -532,7 +534,7 @@ static float geodesic_f32(const fconsts* k, float st, float ct, int adaptive, ui
 float geo_oracle_geodesic_f32(const geo_scene* s, float st, float ct, uint32_t* steps) {
     fconsts k = make_fconsts(s);
     uint32_t n = 0;
-    float a = geodesic_f32(&k, st, ct, s->mode == GEO_MODE_ADAPTIVE, &n);
+    float a = geodesic_f32(&k, st, ct, 1.0f / ct, s->mode == GEO_MODE_ADAPTIVE, &n);
     if (steps) *steps = n;
     return a;
 }
@@ -593,6 +595,7 @@ static void pixel_f32(const geo_frame* f, const cam_f32* cam, const fconsts* k, 
     }
     float st = clampf(c2[2], -1.0f, 1.0f);
     float rho2 = sqrtf(fmaf(c2[1], c2[1], c2[0] * c2[0])); /* cos theta */
+    float rrho = 1.0f / rho2;
     float lam;
     *steps = 0;
     if (mode == (int)GEO_MODE_FAN) {
@@ -605,7 +608,7 @@ static void pixel_f32(const geo_frame* f, const cam_f32* cam, const fconsts* k, 
         uint32_t i1 = (i + 1u < n_fan) ? i + 1u : n_fan - 1u;
         lam = fan[i] * (1.0f - w) + fan[i1] * w;
     } else {
-        lam = F_PI2 - geodesic_f32(k, st, rho2, mode == (int)GEO_MODE_ADAPTIVE, steps);
+        lam = F_PI2 - geodesic_f32(k, st, rho2, rrho, mode == (int)GEO_MODE_ADAPTIVE, steps);
     }
     int bh = lam < -7.0f;
     /* sky_uv */
@@ -613,7 +616,7 @@ static void pixel_f32(const geo_frame* f, const cam_f32* cam, const fconsts* k, 
     geo_oracle_sincosf(lam, &sl, &cll);
     float ex = cll, ey = 0.0f;
     if (rho2 > 0.0f) {
-        float w = cll * (1.0f / rho2); /* divf_ */
+        float w = cll * rrho;
         ex = c2[0] * w;
         ey = c2[1] * w;
     }

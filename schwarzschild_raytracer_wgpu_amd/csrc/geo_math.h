@@ -42,6 +42,15 @@ constexpr float kInvTwoPi = 0.159154943091895335769f;
 
 GEO_HD float fmaf_(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
 
+// In an arm of a lane-divergent branch that must stay a branch (a volatile
+// asm cannot be speculated, so the arm is not if-converted into work every
+// lane would do).
+#if defined(__HIP_DEVICE_COMPILE__)
+#define GEO_COLD_ARM() asm volatile("")
+#else
+#define GEO_COLD_ARM() ((void)0)
+#endif
+
 // Correctly rounded sqrt, equal to __builtin_sqrtf for every input.  On the
 // device, hipcc's correctly rounded sequence wraps the ±1-ulp correction of
 // v_sqrt_f32 in a 2^32 pre-scale for x < 2^-96 and a class fix-up for
@@ -131,7 +140,13 @@ GEO_HD float asinf_(float x) {
     const float a = __builtin_fabsf(x);
     const bool big = a > 0.5f;
     const float z = big ? 0.5f * (1.0f - a) : a * a;
-    const float s = big ? sqrtf_(z) : a;
+    // the square root only where it is used: a wave with no |x| > 1/2 lane
+    // branches over it (the compiler would otherwise take it on every lane)
+    float s = a;
+    if (big) {
+        GEO_COLD_ARM();
+        s = sqrtf_(z);
+    }
     const float p = fmaf_(fmaf_(fmaf_(fmaf_(4.2163199048e-2f, z, 2.4181311049e-2f), z,
                                       4.5470025998e-2f), z, 7.4953002686e-2f), z,
                           1.6666752422e-1f);

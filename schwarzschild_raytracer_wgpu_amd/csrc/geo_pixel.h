@@ -51,6 +51,7 @@ struct PixelConsts {
     float schwarz_u;       // 1/rs (:132)
     float u0;              // 1/r (:122)
     float h_over_r2;       // (1 - rs/r)/(r*r) (:123)
+    float inv_r2;          // 1/(r*r)
     float bound;           // 0.9*min(u0, 1/max(sphere_r, r3_2)) (:127)
     float e_out;           // sqrt(1 - rs/r) (solve_ray_fan :48)
     float e_in;            // sqrt(-1 + rs/r) (:44)
@@ -118,6 +119,7 @@ GEO_HD PixelConsts make_consts(float rs, float sphere_r, float r, float step, ui
     k.schwarz_u = 1.0f / rs;
     k.u0 = 1.0f / r;
     k.h_over_r2 = (1.0f - rs / r) / (r * r);
+    k.inv_r2 = 1.0f / (r * r);
     const float um = 1.0f / (sphere_r > k.r3_2 ? sphere_r : k.r3_2);
     k.bound = 0.9f * (k.u0 < um ? k.u0 : um);
     k.e_out = __builtin_sqrtf(1.0f - rs / r);
@@ -244,10 +246,12 @@ GEO_HD float newton_angle(const PixelConsts& k, float U, float UB, float NU, flo
 }
 
 // Ray set-up of solve_ray_fan + solve_geodesic (sphere_ray_tracer.rs:38-132)
-// for (st, ct) = (sin theta, cos theta >= 0) of the central-frame direction.
+// for (st, ct) = (sin theta, cos theta >= 0) of the central-frame direction
+// and rct = rcpf_(ct), which the pixel shares with its sky direction (sky_uv).
 // Returns false with the traveled angle in *early (radial case, pre-filter
 // or failed initial loop test); else the scaled initial state (U, UB).
-GEO_HD bool geodesic_init(const PixelConsts& k, float st, float ct, float* early, float* U0, float* UB0) {
+GEO_HD bool geodesic_init(const PixelConsts& k, float st, float ct, float rct, float* early, float* U0,
+                          float* UB0) {
     // solve_ray_fan per node (:38-49)
     const float rotation = k.r * ct;
     bool falling;
@@ -265,8 +269,8 @@ GEO_HD bool geodesic_init(const PixelConsts& k, float st, float ct, float* early
                                     : (falling ? k.radial_falling : k.radial_outgoing);
         return false;
     }
-    // 1/b^2 with b = rotation/energy (:61): one quotient (divf_)
-    const float inv_b2 = divf_(energy * energy, rotation * rotation);
+    // 1/b^2 with b = rotation/energy = r ct/energy (:61), from the pixel's 1/ct
+    const float inv_b2 = (energy * energy) * ((rct * rct) * k.inv_r2);
     // pre-filters (:106-119), frame-uniform terms precomputed
     if (k.pf_always | (k.pf_eneg & (energy < 0.0f)) | (k.pf_barrier & (inv_b2 < k.barrier_thresh)) |
         (k.pf_falling & falling) | (k.pf_outgoing & !falling)) {
@@ -522,10 +526,10 @@ GEO_HD float geodesic_finish(const PixelConsts& k, const StopTest<KIND>& stop_at
 // *steps = executed main-loop RK4 steps.  LOOP = RK4 steps per exit test
 // (tools/ubench/loop_ab.hip), KIND the integration kind (geodesic_kind).
 template <int LOOP, int KIND>
-GEO_HD float geodesic_angle_v(const PixelConsts& k, float st, float ct, uint32_t* steps) {
+GEO_HD float geodesic_angle_v(const PixelConsts& k, float st, float ct, float rct, uint32_t* steps) {
     *steps = 0;
     float U, UB, early;
-    if (!geodesic_init(k, st, ct, &early, &U, &UB)) return early;
+    if (!geodesic_init(k, st, ct, rct, &early, &U, &UB)) return early;
     float h = k.step, hh = k.hh, hh2 = k.hh2, hhh = k.hhh, h6 = k.h6, h2_6 = k.h2_6;
     // Main loop (:134-191), restructured for the wave64 VALU: per step the
     // lane-exit flag is StopTest (crossing | escape | horizon); the budget
@@ -584,10 +588,11 @@ GEO_HD float geodesic_angle_v(const PixelConsts& k, float st, float ct, uint32_t
 #endif
 // Runtime-dispatched form (host tests); the kernel instantiates per kind.
 GEO_HD float geodesic_angle(const PixelConsts& k, float st, float ct, uint32_t* steps) {
+    const float rct = rcpf_(ct);
     switch (geodesic_kind(k)) {
-        case kCurvedOut: return geodesic_angle_v<GEO_LOOP_VARIANT, kCurvedOut>(k, st, ct, steps);
-        case kCurvedIn: return geodesic_angle_v<GEO_LOOP_VARIANT, kCurvedIn>(k, st, ct, steps);
-        default: return geodesic_angle_v<GEO_LOOP_VARIANT, kFlat>(k, st, ct, steps);
+        case kCurvedOut: return geodesic_angle_v<GEO_LOOP_VARIANT, kCurvedOut>(k, st, ct, rct, steps);
+        case kCurvedIn: return geodesic_angle_v<GEO_LOOP_VARIANT, kCurvedIn>(k, st, ct, rct, steps);
+        default: return geodesic_angle_v<GEO_LOOP_VARIANT, kFlat>(k, st, ct, rct, steps);
     }
 }
 
@@ -648,10 +653,10 @@ GEO_HD void dp5_step(float U, float V, float h, float hh, float* NU, float* NV, 
 //   |SE| h^2 < tolU/64        accept, then h = min(2h, hmax)  (5th order: x32)
 //   otherwise                 accept, keep h
 template <int KIND>
-GEO_HD float geodesic_angle_adaptive(const PixelConsts& k, float st, float ct, uint32_t* steps) {
+GEO_HD float geodesic_angle_adaptive(const PixelConsts& k, float st, float ct, float rct, uint32_t* steps) {
     *steps = 0;
     float U, V, early;
-    if (!geodesic_init(k, st, ct, &early, &U, &V)) return early;
+    if (!geodesic_init(k, st, ct, rct, &early, &U, &V)) return early;
     const StopTest<KIND> stop_at(k);
     const uint32_t ms = k.max_steps;
     float h = k.step, ang = 0.0f;
@@ -784,14 +789,14 @@ GEO_HD float fan_lerp(const float* fan, uint32_t n, float st) {
 // |(c2x, c2y)| = cos theta of the central-frame direction (to_polar, :75).
 GEO_HD float central_rho(float c2x, float c2y) { return sqrtf_(fmaf_(c2y, c2y, c2x * c2x)); }
 
-// shader.wgsl:90-100 — (phi of c2, lambda') to sky-sphere (U, V); rho = central_rho.
-GEO_HD void sky_uv(const float* m2, float c2x, float c2y, float rho, float lam, float* U, float* V) {
+// shader.wgsl:90-100 — (phi of c2, lambda') to sky-sphere (U, V); rho = central_rho, rrho = rcpf_(rho).
+GEO_HD void sky_uv(const float* m2, float c2x, float c2y, float rho, float rrho, float lam, float* U, float* V) {
     float sl, cl;
     sincosf_(lam, &sl, &cl);
     // to_cart(phi, lam) with (cos phi, sin phi) = (c2x, c2y)/rho
     float ex = cl, ey = 0.0f;
     if (rho > 0.0f) {
-        const float w = divf_(cl, rho);
+        const float w = cl * rrho;
         ex = c2x * w;
         ey = c2y * w;
     }

@@ -103,8 +103,8 @@ struct PaddedSkyQuad {
 
 // Epilogue of one pixel (shader.wgsl:88-105): black-hole test, sky UV,
 // bilinear sample, blend and the optional outputs at index o.
-__device__ __forceinline__ void shade_pixel(const RenderArgs& a, float c2x, float c2y, float ct, float lam,
-                                            uint32_t steps, size_t o) {
+__device__ __forceinline__ void shade_pixel(const RenderArgs& a, float c2x, float c2y, float ct, float rct,
+                                            float lam, uint32_t steps, size_t o) {
     const bool bh = lam < geo::kBlackHoleLambda;
     // A black-hole pixel is discarded (shader.wgsl:88): it needs its UV
     // only when the caller asks for it, so a wave inside the shadow skips
@@ -113,7 +113,7 @@ __device__ __forceinline__ void shade_pixel(const RenderArgs& a, float c2x, floa
 #if GEO_BH_SKIP_UV
     if (!bh || a.out_uv)
 #endif
-        geo::sky_uv(a.frame.central_to_uv, c2x, c2y, ct, lam, &U, &V);
+        geo::sky_uv(a.frame.central_to_uv, c2x, c2y, ct, rct, lam, &U, &V);
     const PaddedSkyQuad quad{__builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(a.sky), 0,
                                                                (int)a.sky_bytes, kBufferRsrcWord3),
                              a.sky_pitch_b};
@@ -154,15 +154,16 @@ __global__ __launch_bounds__(kBlock) void geo_render_kernel(const RenderArgs a) 
                                &c2x, &c2y, &c2z);
         const float st = geo::clampf_(c2z, -1.0f, 1.0f);
         const float ct = geo::central_rho(c2x, c2y);
+        const float rct = geo::rcpf_(ct);  // shared by the ray's 1/b^2 and its sky direction
         float lam;
         if constexpr (MODE == GEO_MODE_FAN) {
             lam = geo::fan_lerp(s_fan, a.n_fan, st);
         } else if constexpr (MODE == GEO_MODE_ADAPTIVE) {
-            lam = geo::kPi2 - geo::geodesic_angle_adaptive<KIND>(a.k, st, ct, &steps);
+            lam = geo::kPi2 - geo::geodesic_angle_adaptive<KIND>(a.k, st, ct, rct, &steps);
         } else {
-            lam = geo::kPi2 - geo::geodesic_angle_v<GEO_LOOP_VARIANT, KIND>(a.k, st, ct, &steps);
+            lam = geo::kPi2 - geo::geodesic_angle_v<GEO_LOOP_VARIANT, KIND>(a.k, st, ct, rct, &steps);
         }
-        shade_pixel(a, c2x, c2y, ct, lam, steps, (size_t)ly * a.width + px);
+        shade_pixel(a, c2x, c2y, ct, rct, lam, steps, (size_t)ly * a.width + px);
     }
     if constexpr (MODE != GEO_MODE_FAN) {
         if (a.step_slots) {

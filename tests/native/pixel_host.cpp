@@ -8,19 +8,19 @@
 #include "../../schwarzschild_raytracer_wgpu_amd/csrc/geo_pixel.h"
 
 template <int LOOP>
-static float geo_v(const geo::PixelConsts& k, float st, float ct, uint32_t* n) {
+static float geo_v(const geo::PixelConsts& k, float st, float ct, float rct, uint32_t* n) {
     switch (geo::geodesic_kind(k)) {
-        case geo::kCurvedOut: return geo::geodesic_angle_v<LOOP, geo::kCurvedOut>(k, st, ct, n);
-        case geo::kCurvedIn: return geo::geodesic_angle_v<LOOP, geo::kCurvedIn>(k, st, ct, n);
-        default: return geo::geodesic_angle_v<LOOP, geo::kFlat>(k, st, ct, n);
+        case geo::kCurvedOut: return geo::geodesic_angle_v<LOOP, geo::kCurvedOut>(k, st, ct, rct, n);
+        case geo::kCurvedIn: return geo::geodesic_angle_v<LOOP, geo::kCurvedIn>(k, st, ct, rct, n);
+        default: return geo::geodesic_angle_v<LOOP, geo::kFlat>(k, st, ct, rct, n);
     }
 }
 
-static float geo_adaptive(const geo::PixelConsts& k, float st, float ct, uint32_t* n) {
+static float geo_adaptive(const geo::PixelConsts& k, float st, float ct, float rct, uint32_t* n) {
     switch (geo::geodesic_kind(k)) {
-        case geo::kCurvedOut: return geo::geodesic_angle_adaptive<geo::kCurvedOut>(k, st, ct, n);
-        case geo::kCurvedIn: return geo::geodesic_angle_adaptive<geo::kCurvedIn>(k, st, ct, n);
-        default: return geo::geodesic_angle_adaptive<geo::kFlat>(k, st, ct, n);
+        case geo::kCurvedOut: return geo::geodesic_angle_adaptive<geo::kCurvedOut>(k, st, ct, rct, n);
+        case geo::kCurvedIn: return geo::geodesic_angle_adaptive<geo::kCurvedIn>(k, st, ct, rct, n);
+        default: return geo::geodesic_angle_adaptive<geo::kFlat>(k, st, ct, rct, n);
     }
 }
 
@@ -40,17 +40,18 @@ extern "C" int host_render(const geo_frame* f, const geo_scene* s, const float* 
                                    geo::aberration_kt(f->psi_factor_and_position[0]), px, py, &c2x, &c2y, &c2z);
             const float st = geo::clampf_(c2z, -1.0f, 1.0f);
             const float ct = geo::central_rho(c2x, c2y);
+            const float rct = geo::rcpf_(ct);
             uint32_t n = 0;
             float lam;
             if (s->mode == GEO_MODE_FAN)
                 lam = geo::fan_lerp(fan, n_fan, st);
             else if (s->mode == GEO_MODE_ADAPTIVE)
-                lam = geo::kPi2 - geo_adaptive(k, st, ct, &n);
+                lam = geo::kPi2 - geo_adaptive(k, st, ct, rct, &n);
             else
-                lam = geo::kPi2 - (variant == 1 ? geo_v<1>(k, st, ct, &n) : variant == 2 ? geo_v<2>(k, st, ct, &n) : variant == 3 ? geo_v<3>(k, st, ct, &n) : geo_v<4>(k, st, ct, &n));
+                lam = geo::kPi2 - (variant == 1 ? geo_v<1>(k, st, ct, rct, &n) : variant == 2 ? geo_v<2>(k, st, ct, rct, &n) : variant == 3 ? geo_v<3>(k, st, ct, rct, &n) : geo_v<4>(k, st, ct, rct, &n));
             const bool bh = lam < geo::kBlackHoleLambda;
             float U, V;
-            geo::sky_uv(f->central_to_uv, c2x, c2y, ct, lam, &U, &V);
+            geo::sky_uv(f->central_to_uv, c2x, c2y, ct, rct, lam, &U, &V);
             const size_t o = (size_t)ly * width + px;
             auto fetch = [sky](uint32_t i) { return sky[i]; };
             if (s->flags & GEO_FLAG_COMPOSITE) {

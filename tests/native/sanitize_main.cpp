@@ -14,16 +14,17 @@
 #include "../../schwarzschild_raytracer_wgpu_amd/csrc/geo_rays.h"
 
 static float angle_for(const geo::PixelConsts& k, uint32_t mode, float st, float ct, uint32_t* n) {
+    const float rct = geo::rcpf_(ct);
     switch (geo::geodesic_kind(k)) {
         case geo::kCurvedOut:
-            return mode == GEO_MODE_ADAPTIVE ? geo::geodesic_angle_adaptive<geo::kCurvedOut>(k, st, ct, n)
-                                             : geo::geodesic_angle_v<4, geo::kCurvedOut>(k, st, ct, n);
+            return mode == GEO_MODE_ADAPTIVE ? geo::geodesic_angle_adaptive<geo::kCurvedOut>(k, st, ct, rct, n)
+                                             : geo::geodesic_angle_v<4, geo::kCurvedOut>(k, st, ct, rct, n);
         case geo::kCurvedIn:
-            return mode == GEO_MODE_ADAPTIVE ? geo::geodesic_angle_adaptive<geo::kCurvedIn>(k, st, ct, n)
-                                             : geo::geodesic_angle_v<4, geo::kCurvedIn>(k, st, ct, n);
+            return mode == GEO_MODE_ADAPTIVE ? geo::geodesic_angle_adaptive<geo::kCurvedIn>(k, st, ct, rct, n)
+                                             : geo::geodesic_angle_v<4, geo::kCurvedIn>(k, st, ct, rct, n);
         default:
-            return mode == GEO_MODE_ADAPTIVE ? geo::geodesic_angle_adaptive<geo::kFlat>(k, st, ct, n)
-                                             : geo::geodesic_angle_v<4, geo::kFlat>(k, st, ct, n);
+            return mode == GEO_MODE_ADAPTIVE ? geo::geodesic_angle_adaptive<geo::kFlat>(k, st, ct, rct, n)
+                                             : geo::geodesic_angle_v<4, geo::kFlat>(k, st, ct, rct, n);
     }
 }
 
@@ -60,7 +61,7 @@ static int render_check(double px_, double py_, double pz_, float rs, uint32_t m
             uint32_t n = 0;
             const float lam = geo::kPi2 - angle_for(k, mode, st, ct, &n);
             float U, V;
-            geo::sky_uv(f.central_to_uv, c2x, c2y, ct, lam, &U, &V);
+            geo::sky_uv(f.central_to_uv, c2x, c2y, ct, geo::rcpf_(ct), lam, &U, &V);
             const bool bh = lam < geo::kBlackHoleLambda;
             const uint32_t c = bh ? geo::kBlackRGBA
                                   : geo::sample_sky([skyp](uint32_t i) { return skyp[i]; }, 16, 8, false, U, V);

@@ -1,0 +1,58 @@
+"""bench.py's contract (the driver parses its one JSON line).
+
+CPU: the committed PMC traffic is attached only to the workload it was taken
+on.  GPU: a short run (the driver's own --steps/--warmup shape, fewer spin-up
+frames) prints one JSON line with every field the contract names, and its
+numbers are consistent with each other.
+"""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+import bench
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_pmc_traffic_only_for_the_profiled_workload():
+    t = bench.pmc_traffic("cfg3_4k", "direct", 1)
+    assert t is not None and 5e7 < t < 2e8  # ~90 MB per 4K frame
+    assert bench.pmc_traffic("cfg3_4k", "adaptive", 1) is None  # a direct-mode profile
+    assert bench.pmc_traffic("cfg3_4k", "fan", 1) is None
+    assert bench.pmc_traffic("cfg3_4k", "direct", 2) is None  # full-frame bytes vs a rank's share
+    assert bench.pmc_traffic("cfg5_8k_adaptive", "adaptive", 1) is not None
+    assert bench.pmc_traffic("cfg2_1080p", "direct", 1) is None  # never profiled
+
+
+@pytest.mark.gpu
+def test_bench_short_run_prints_the_contract_line():
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "20", "--warmup", "5",
+                        "--spinup-frames", "60", "--cpu-seconds", "0.2"],
+                       cwd=ROOT, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
+        assert k in d, k
+    assert d["n_gpus"] == 1 and d["steps"] == 20 and d["warmup"] == 5 and d["higher_is_better"] is True
+    assert d["dtype"] == "f32" and d["vs_baseline"] is None and "workload" in d["config"]
+    # value = executed RK4 steps of the timed frames / their wall time
+    assert abs(d["value"] - d["steps_per_frame"] / (d["ms_per_step"] * 1e-3)) < 1e-6 * d["value"]
+    assert 70 < d["mean_steps_per_pixel"] < 90  # the default scene: 78.0
+    rf = d["roofline"]
+    for k in ("bound", "achieved", "peak", "unit", "frac", "traffic"):
+        assert k in rf, k
+    assert abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-9
+    assert abs(rf["achieved"] - rf["algorithmic_flops_per_launch"] / (d["kernel_ms"]["avg"] * 1e-3) / 1e12) < 1e-6
+    assert 0.3 < rf["frac"] < 1.0
+    cb = d["cpu_baseline"]
+    assert cb["kind"] == "port" and cb["cores"] >= 1 and cb["value"] > 0

@@ -408,15 +408,20 @@ GEO_HD uint32_t run_groups_pp(const StopTest<KIND>& stop_at, uint32_t ngroups, u
         au[j] = bu[j] = xu;
         ab[j] = bb[j] = xb;
     }
-    bool done = false, in_b = false;  // in_b: stopped in a B group
-    bool last_b = false;              // wave-uniform: the last group run was a B group
-    uint64_t live = ballot_(true);    // wave-uniform: the lanes still integrating
+    // Groups q = 0, 2, 4, ... are A groups, 1, 3, ... B groups.  A lane that
+    // stops in group q records it = q G (a multiple of G below `all`), so the
+    // set its states sit in is (it / G) & 1 after the loop: the loop carries
+    // one lane flag (`done`), which keeps the lane-mask merges at its joins
+    // to a minimum.
+    bool done = false;
+    uint64_t live = ballot_(true);  // wave-uniform: the lanes still integrating
     uint32_t it = all;
+    uint32_t q = 0;                 // wave-uniform: groups run
     // The stop test runs outside the `if (!done)` regions, on every lane: its
     // ballot is then the compare mask itself (a flag merged out of the region
     // would be rematerialised by two VALU ops per group).  A finished lane's
     // flag is garbage but harmless: `live` only ever loses bits.
-    for (uint32_t q = 0; q < ngroups;) {
+    while (q < ngroups) {
         if (!done) group_steps_<G, KIND>(xu, xb, h, hh, hh2, hhh, h6, h2_6, au, ab);
         bool hit = group_stop_<G, KIND, LAST_ONLY>(stop_at, au, ab);
         live &= ~ballot_(hit);
@@ -425,7 +430,6 @@ GEO_HD uint32_t run_groups_pp(const StopTest<KIND>& stop_at, uint32_t ngroups, u
             done = true;
             it = q * (uint32_t)G;
         }
-        last_b = false;
         if (++q >= ngroups || live == 0) break;
         if (!done) {
             float ou[G], ob[G];
@@ -451,15 +455,16 @@ GEO_HD uint32_t run_groups_pp(const StopTest<KIND>& stop_at, uint32_t ngroups, u
         if (hit && !done) {
             GEO_RARE();
             done = true;
-            in_b = true;
             it = q * (uint32_t)G;
         }
-        last_b = true;
-        if (++q >= ngroups || live == 0) break;
+        ++q;
+        if (live == 0) break;
     }
+    // the set holding the stopping group (B: start a_G, then b_1..b_{G-1}, X);
     // a lane on the budget continues from the last group's end state, which
-    // sits where a B group's start state (a_G) or an A group's (X) does
-    if (!done) in_b = !last_b;
+    // sits where a B group's start state (a_G, after an A group) or an A
+    // group's (X, after a B group) does
+    const bool in_b = it < all ? ((it / (uint32_t)G) & 1u) != 0 : (q & 1u) != 0;
     su_[0] = in_b ? au[G - 1] : xu;
     sb_[0] = in_b ? ab[G - 1] : xb;
 #pragma unroll

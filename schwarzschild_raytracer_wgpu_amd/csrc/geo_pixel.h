@@ -430,7 +430,9 @@ GEO_HD uint32_t run_groups_pp(const StopTest<KIND>& stop_at, uint32_t ngroups, u
             done = true;
             it = q * (uint32_t)G;
         }
-        if (++q >= ngroups || live == 0) break;
+        // two uniform branches (one `||` is lowered through lane masks)
+        if (++q >= ngroups) break;
+        if (live == 0) break;
         if (!done) {
             float ou[G], ob[G];
             group_steps_<G, KIND>(au[G - 1], ab[G - 1], h, hh, hh2, hhh, h6, h2_6, ou, ob);

@@ -54,8 +54,8 @@ def parse():
                    help="render streams (1 or 2; default 1 at N = 1, 2 at N > 1): with 2, frame i+1's waves fill "
                         "frame i's tail (a rank's share at N = 8 is only ~2 waves per slot) and the per-launch "
                         "kernel time is measured on 20 back-to-back launches on one stream after the timed region. "
-                        "N = 1 keeps one stream so that in-region launch times and rocprofv3's agree; the two-stream "
-                        "throughput is reported beside it (`pipelined`)")
+                        "N = 1 keeps one stream so that in-region launch times and rocprofv3's agree (--pipelined "
+                        "reports the two-stream throughput beside it)")
     p.add_argument("--frames-per-gather", type=int, default=8,
                    help="N > 1: frames per RCCL gather to rank 0 (amortises the ~34 us host cost of a gather; "
                         "rank 0 reassembles each batch with one geo_assemble_lead launch)")
@@ -65,6 +65,10 @@ def parse():
                         "6 measured on the whole pipeline before the timed region")
     p.add_argument("--lead-trial-frames", type=int, default=120,
                    help="frames per --rank0-lead auto trial (after a quarter as many warm-up frames)")
+    p.add_argument("--pipelined", action="store_true",
+                   help="N = 1: also time the K frames on two render streams (consecutive frames overlap) and report "
+                        "it as `pipelined`; off by default, since rocprofv3 would average the overlapped launches "
+                        "into the kernel's duration")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-threads", type=int, default=16)
     p.add_argument("--cpu-row-step", type=int, default=None,
@@ -256,7 +260,7 @@ def main():
     # that frame i+1's waves fill frame i's tail (what a frame loop gains
     # from pipelining; not the metric's value, whose launches do not overlap)
     pipelined = None
-    if world == 1 and sf.S == 1:
+    if args.pipelined and world == 1 and sf.S == 1:
         sf2 = ShardedFrame(ctx, frame, scene, W, H, args.band_rows, rank, world, dev, None, render_streams=2)
         spin_up(sf2, max(100, args.warmup))  # its buffers' allocation idled the GPU
         torch.cuda.synchronize()

@@ -624,6 +624,7 @@ static void pixel_f32(const geo_frame* f, const cam_f32* cam, const fconsts* k, 
     m3vf(f->central_to_uv, ex, ey, sl, c3);
     float U = geo_oracle_atan2f(c3[1], c3[0]) * 0.159154943091895335769f;
     if (U < 0.0f) U += 1.0f;
+    U = U + 0.0f; /* -0 -> +0 (the kernel's med3 clamp) */
     float V = 0.5f - geo_oracle_asinf(c3[2]) * 0.318309886183790671538f;
     if (!(U == U)) U = 0.0f;
     if (!(V == V)) V = 0.0f;

@@ -811,11 +811,13 @@ GEO_HD void sky_uv(const float* m2, float c2x, float c2y, float rho, float rrho,
     mat3_mul(m2, ex, ey, sl, &x, &y, &z);
     float u = atan2f_(y, x) * kInvTwoPi;
     if (u < 0.0f) u += 1.0f;
-    float v = 0.5f - asinf_(z) * kInvPi;
-    if (!(u == u)) u = 0.0f;  // NaN guard
-    if (!(v == v)) v = 0.0f;
-    *U = clampf_(u, 0.0f, 1.0f);
-    *V = clampf_(v, 0.0f, 1.0f);
+    const float v = 0.5f - asinf_(z) * kInvPi;
+    // clamped to [0, 1] with NaN -> 0, one v_med3_f32 each (the med3 of a NaN
+    // is the IEEE min of the other two, 0); u + 0 first turns the -0 of an
+    // atan2(-0, x) into +0, the one signed zero the median could order either
+    // way (v = 1/2 - t is never -0)
+    *U = med3_(u + 0.0f, 0.0f, 1.0f);
+    *V = med3_(v, 0.0f, 1.0f);
 }
 
 // Packed channel pairs of the bilinear sample: R|B and G|A in the two 16-bit

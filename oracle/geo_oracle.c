@@ -593,7 +593,8 @@ static void pixel_f32(const geo_frame* f, const cam_f32* cam, const fconsts* k, 
     } else {
         m3vf(f->movement_to_central, e[0], e[1], e[2], c2);
     }
-    float st = clampf(c2[2], -1.0f, 1.0f);
+    float st = c2[2] > -1.0f ? c2[2] : -1.0f; /* med3(c2z, -1, 1): NaN -> -1 */
+    st = st < 1.0f ? st : 1.0f;
     float rho2 = sqrtf(fmaf(c2[1], c2[1], c2[0] * c2[0])); /* cos theta */
     float rrho = 1.0f / rho2;
     float lam;

@@ -793,6 +793,11 @@ GEO_HD float fan_lerp(const float* fan, uint32_t n, float st) {
     return fan[i] * (1.0f - w) + fan[i1] * w;
 }
 
+// sin theta of the central-frame direction, c2z clamped to [-1, 1] (to_polar's
+// asin argument, :75) by one v_med3_f32 (a NaN becomes -1, where a compare-
+// and-select clamp would keep it: 4 VALU for no case a frame produces).
+GEO_HD float central_sin(float c2z) { return med3_(c2z, -1.0f, 1.0f); }
+
 // |(c2x, c2y)| = cos theta of the central-frame direction (to_polar, :75).
 GEO_HD float central_rho(float c2x, float c2y) { return sqrtf_(fmaf_(c2y, c2y, c2x * c2x)); }
 

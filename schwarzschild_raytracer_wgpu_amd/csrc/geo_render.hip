@@ -152,7 +152,7 @@ __global__ __launch_bounds__(kBlock) void geo_render_kernel(const RenderArgs a) 
         float c2x, c2y, c2z;
         geo::pixel_central_dir(a.cam, a.frame.movement_to_central, a.frame.psi_factor_and_position[0], a.kt, px, py,
                                &c2x, &c2y, &c2z);
-        const float st = geo::clampf_(c2z, -1.0f, 1.0f);
+        const float st = geo::central_sin(c2z);
         const float ct = geo::central_rho(c2x, c2y);
         const float rct = geo::rcpf_(ct);  // shared by the ray's 1/b^2 and its sky direction
         float lam;

@@ -1,6 +1,6 @@
 // The sky UV clamp of the specification (geo_pixel.h sky_uv): y = x + 0, then
 // NaN -> 0 and [0, 1] clamping, as ONE v_med3_f32(y, 0, 1) on the device
-// (geo::med3_).  Checked for all 2^32 f32 bit patterns against the same rule
+// (geo::med3_); and sin theta's clamp (geo::central_sin: NaN -> -1, [-1, 1]).  Checked for all 2^32 f32 bit patterns against the same rule
 // evaluated on the IEEE bit pattern (no float compares the compiler could
 // fold back into a med3).  Prints "mismatches N"; exit status 0 iff N == 0.
 #include <hip/hip_runtime.h>
@@ -16,6 +16,13 @@ __device__ __forceinline__ uint32_t rule(uint32_t yb) {
     return yb;
 }
 
+// geo::central_sin: med3(x, -1, 1); NaN -> -1, else clamped (-0 stays -0)
+__device__ __forceinline__ uint32_t rule_sin(uint32_t xb) {
+    if ((xb & 0x7fffffffu) > 0x7f800000u) return 0xbf800000u;                    // NaN -> -1
+    if ((xb & 0x7fffffffu) > 0x3f800000u) return (xb & 0x80000000u) | 0x3f800000u;  // |x| > 1 -> +-1
+    return xb;
+}
+
 __global__ __launch_bounds__(256) void check(unsigned long long* bad, uint32_t* first) {
     const uint64_t stride = (uint64_t)gridDim.x * 256u;
     for (uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x; i < (1ull << 32); i += stride) {
@@ -24,7 +31,9 @@ __global__ __launch_bounds__(256) void check(unsigned long long* bad, uint32_t* 
         const float y = x + 0.0f;
         const uint32_t a = __builtin_bit_cast(uint32_t, geo::med3_(y, 0.0f, 1.0f));
         const uint32_t b = rule(__builtin_bit_cast(uint32_t, y));
-        if (a != b) {
+        const uint32_t c = __builtin_bit_cast(uint32_t, geo::central_sin(x));
+        const uint32_t d = rule_sin((uint32_t)i);
+        if (a != b || c != d) {
             const unsigned long long n = atomicAdd(bad, 1ull);
             if (n < 8) first[n] = (uint32_t)i;
         }

@@ -38,7 +38,7 @@ extern "C" int host_render(const geo_frame* f, const geo_scene* s, const float* 
             float c2x, c2y, c2z;
             geo::pixel_central_dir(cam, f->movement_to_central, f->psi_factor_and_position[0],
                                    geo::aberration_kt(f->psi_factor_and_position[0]), px, py, &c2x, &c2y, &c2z);
-            const float st = geo::clampf_(c2z, -1.0f, 1.0f);
+            const float st = geo::central_sin(c2z);
             const float ct = geo::central_rho(c2x, c2y);
             const float rct = geo::rcpf_(ct);
             uint32_t n = 0;

@@ -57,7 +57,7 @@ static int render_check(double px_, double py_, double pz_, float rs, uint32_t m
             float c2x, c2y, c2z;
             geo::pixel_central_dir(cam, f.movement_to_central, f.psi_factor_and_position[0],
                                    geo::aberration_kt(f.psi_factor_and_position[0]), px, py, &c2x, &c2y, &c2z);
-            const float st = geo::clampf_(c2z, -1.0f, 1.0f), ct = geo::central_rho(c2x, c2y);
+            const float st = geo::central_sin(c2z), ct = geo::central_rho(c2x, c2y);
             uint32_t n = 0;
             const float lam = geo::kPi2 - angle_for(k, mode, st, ct, &n);
             float U, V;

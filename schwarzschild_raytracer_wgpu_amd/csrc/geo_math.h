@@ -30,6 +30,14 @@
 #else
 #define GEO_OPAQUE(x) ((void)0)
 #endif
+// Gives a variable an arbitrary defined value at no cost (device: whatever
+// its VGPR holds; host: 0) — for registers that are always written before a
+// read that matters.
+#if defined(__HIP_DEVICE_COMPILE__)
+#define GEO_UNSET(x) asm volatile("" : "=v"(x))  // volatile: not CSEd into one value (copied 14 ways)
+#else
+#define GEO_UNSET(x) ((x) = 0)
+#endif
 
 namespace geo {
 

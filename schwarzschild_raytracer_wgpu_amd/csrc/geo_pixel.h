@@ -403,10 +403,16 @@ GEO_HD uint32_t run_groups_pp(const StopTest<KIND>& stop_at, uint32_t ngroups, u
                               float hh2, float hhh, float h6, float h2_6, float (&su_)[G + 1], float (&sb_)[G + 1]) {
     float xu = su_[0], xb = sb_[0];  // X: group A's start, group B's end
     float au[G], ab[G], bu[G], bb[G];  // a_1..a_G; b_1..b_{G-1} (b_G is X)
+    // Every element read after the loop as a state of the lane's stopping
+    // group was written by that group; the others are selected but unused
+    // (a lane on the budget continues from su_[0] alone).  Defined without
+    // instructions: an empty asm output (14 v_mov otherwise).
 #pragma unroll
     for (int j = 0; j < G; ++j) {
-        au[j] = bu[j] = xu;
-        ab[j] = bb[j] = xb;
+        GEO_UNSET(au[j]);
+        GEO_UNSET(ab[j]);
+        GEO_UNSET(bu[j]);
+        GEO_UNSET(bb[j]);
     }
     // Groups q = 0, 2, 4, ... are A groups, 1, 3, ... B groups.  A lane that
     // stops in group q records it = q G (a multiple of G below `all`), so the
@@ -795,7 +801,8 @@ GEO_HD float fan_lerp(const float* fan, uint32_t n, float st) {
 
 // sin theta of the central-frame direction, c2z clamped to [-1, 1] (to_polar's
 // asin argument, :75) by one v_med3_f32 (a NaN becomes -1, where a compare-
-// and-select clamp would keep it: 4 VALU for no case a frame produces).
+// and-select clamp would keep it: 4 VALU for no case a frame produces; c2z
+// is an arithmetic result, so never a signaling NaN, which med3 would quiet).
 GEO_HD float central_sin(float c2z) { return med3_(c2z, -1.0f, 1.0f); }
 
 // |(c2x, c2y)| = cos theta of the central-frame direction (to_polar, :75).

@@ -31,8 +31,14 @@ __global__ __launch_bounds__(256) void check(unsigned long long* bad, uint32_t* 
         const float y = x + 0.0f;
         const uint32_t a = __builtin_bit_cast(uint32_t, geo::med3_(y, 0.0f, 1.0f));
         const uint32_t b = rule(__builtin_bit_cast(uint32_t, y));
-        const uint32_t c = __builtin_bit_cast(uint32_t, geo::central_sin(x));
-        const uint32_t d = rule_sin((uint32_t)i);
+        // c2z is always an arithmetic result: a signaling NaN cannot reach the
+        // clamp (and v_med3_f32 would quiet one instead of returning -1), so
+        // the input passes a multiply first (x * 1 keeps -0; `one` is opaque)
+        float one = 1.0f;
+        GEO_OPAQUE(one);
+        const float z = x * one;
+        const uint32_t c = __builtin_bit_cast(uint32_t, geo::central_sin(z));
+        const uint32_t d = rule_sin(__builtin_bit_cast(uint32_t, z));
         if (a != b || c != d) {
             const unsigned long long n = atomicAdd(bad, 1ull);
             if (n < 8) first[n] = (uint32_t)i;

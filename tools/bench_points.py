@@ -32,12 +32,15 @@ BYTES_PER_CONNECTOR = 2 * 48 * 4 + 2 + 6 + 16
 
 def pmc_traffic(n_conn, orbits):
     """HBM bytes per launch of geo_rays_kernel from the committed rocprofv3 PMC
-    summary (profiles/r01_points_pmc.json: FETCH_SIZE doubled for 16-B/lane
-    streaming reads, WRITE_SIZE), for the workload it was taken on, else None."""
-    path = os.path.join(ROOT, "profiles", "r01_points_pmc.json")
-    if orbits or not os.path.exists(path):
+    summary (the newest profiles/*_points_pmc.json: FETCH_SIZE doubled for
+    16-B/lane streaming reads, WRITE_SIZE), for the workload it was taken on,
+    else None."""
+    import glob
+
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_points_pmc.json")))
+    if orbits or not files:
         return None
-    with open(path) as f:
+    with open(files[-1]) as f:
         d = json.load(f)
     return d["derived"]["traffic_bytes"] if d["workload"].startswith(f"{n_conn} connectors") else None
 
@@ -46,7 +49,10 @@ def main():
     p = argparse.ArgumentParser()
     p.add_argument("--points", type=int, default=1 << 21)
     p.add_argument("--steps", type=int, default=50)
-    p.add_argument("--warmup", type=int, default=10)
+    p.add_argument("--warmup", type=int, default=100,
+                   help="untimed updates first: the clock ramps for ~25 ms after the set-up's idle gap "
+                        "(10 warm-up updates timed 0.307 ms per update, 100 and 300 0.275-0.277; "
+                        "tools/gpu_points_warm.sh)")
     p.add_argument("--orbits", action="store_true", help="PointCloud::update with f64 orbits (and respawn)")
     p.add_argument("--cpu-connectors", type=int, default=20000)
     args = p.parse_args()

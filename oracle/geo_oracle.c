@@ -641,12 +641,13 @@ static void pixel_f32(const geo_frame* f, const cam_f32* cam, const fconsts* k, 
     /* bilinear LOD-0, U wraps, V clamps, 8-bit sub-texel weights; per
      * channel: horizontal lerp truncated to 8 bits, vertical lerp rounded;
      * then the alpha blend over (0,0,0,1): round(c*a/255), alpha 255. */
-    float x = fmaf(U, (float)sw, -0.5f);
-    float y = fmaf(V, (float)sh, -0.5f);
-    float fx0 = floorf(x), fy0 = floorf(y);
-    uint32_t wx = (uint32_t)((x - fx0) * 256.0f);
-    uint32_t wy = (uint32_t)((y - fy0) * 256.0f);
-    int ix0 = (int)fx0, iy0 = (int)fy0;
+    /* texel coordinates in 1/256 texel units: n = floor(256 (U sw - 1/2));
+     * texel floor(n / 256), 8-bit weight n mod 256 */
+    int nx = (int)floorf(fmaf(U, (float)sw * 256.0f, -128.0f));
+    int ny = (int)floorf(fmaf(V, (float)sh * 256.0f, -128.0f));
+    uint32_t wx = (uint32_t)nx & 255u;
+    uint32_t wy = (uint32_t)ny & 255u;
+    int ix0 = nx >> 8, iy0 = ny >> 8;
     int w = (int)sw, h = (int)sh;
     if (ix0 < 0) ix0 += w;
     if (ix0 >= w) ix0 -= w;

@@ -898,29 +898,48 @@ GEO_HD void pad_sky(const uint8_t* rgba8, uint32_t tw, uint32_t th, uint32_t* ds
     }
 }
 
+// floor(x) as an int32 (one v_cvt_flr_i32_f32 on the device).
+GEO_HD int32_t floor_i32_(float x) { return (int32_t)__builtin_floorf(x); }
+
+// The G|A channels of a texel into the two 16-bit halves (bytes 1 and 3 to
+// bytes 0 and 2): one v_perm_b32 on the device.
+GEO_HD uint32_t ga_perm_(uint32_t t) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_perm(0u, t, 0x0c030c01u);
+#else
+    return ga_(t);
+#endif
+}
+
 // LOD-0 bilinear sample of an RGBA8 equirect (U wraps, V clamps) with 8-bit
 // sub-texel weights, as texture units do, on packed channel pairs; quad(ix0,
 // iy0, t) supplies the texel quad (WrapClampQuad, or a padded-copy reader).
+// Texel coordinates in 1/256 texel units: n = floor(U tw 256 - 128) =
+// floor(256 x) for x = U tw - 1/2, so ix0 = n >> 8 (arithmetic, -1 for
+// x < 0) and the weight is n & 255 (one fma, one v_cvt_flr_i32_f32, two
+// integer ops per axis).  tw256 = tw * 256 as a float (exact, tw < 2^24).
 template <typename Quad>
-GEO_HD uint32_t sample_sky_quad(const Quad& quad, uint32_t tw, uint32_t th, float U, float V) {
-    const float x = fmaf_(U, (float)tw, -0.5f);
-    const float y = fmaf_(V, (float)th, -0.5f);
-    const float fx0 = __builtin_floorf(x);
-    const float fy0 = __builtin_floorf(y);
-    const uint32_t wx = (uint32_t)((x - fx0) * 256.0f);  // 0..255
-    const uint32_t wy = (uint32_t)((y - fy0) * 256.0f);
+GEO_HD uint32_t sample_sky_quad_f(const Quad& quad, float tw256, float th256, float U, float V) {
+    const int32_t nx = floor_i32_(fmaf_(U, tw256, -128.0f));
+    const int32_t ny = floor_i32_(fmaf_(V, th256, -128.0f));
+    const uint32_t wx = (uint32_t)nx & 255u;
+    const uint32_t wy = (uint32_t)ny & 255u;
     uint32_t t[4];
-    quad((int)fx0, (int)fy0, t);
+    quad(nx >> 8, ny >> 8, t);
     const uint32_t t00 = t[0], t10 = t[1], t01 = t[2], t11 = t[3];
     const uint32_t iwx = 256u - wx, iwy = 256u - wy;
     // horizontal (fields <= 255*256), truncated to 8 bits, then vertical, rounded
     const uint32_t trb = (lerp2_(rb_(t00), rb_(t10), iwx, wx) >> 8) & 0x00FF00FFu;
     const uint32_t brb = (lerp2_(rb_(t01), rb_(t11), iwx, wx) >> 8) & 0x00FF00FFu;
-    const uint32_t tga = (lerp2_(ga_(t00), ga_(t10), iwx, wx) >> 8) & 0x00FF00FFu;
-    const uint32_t bga = (lerp2_(ga_(t01), ga_(t11), iwx, wx) >> 8) & 0x00FF00FFu;
+    const uint32_t tga = (lerp2_(ga_perm_(t00), ga_perm_(t10), iwx, wx) >> 8) & 0x00FF00FFu;
+    const uint32_t bga = (lerp2_(ga_perm_(t01), ga_perm_(t11), iwx, wx) >> 8) & 0x00FF00FFu;
     const uint32_t crb = ((lerp2_(trb, brb, iwy, wy) + 0x00800080u) >> 8) & 0x00FF00FFu;
     const uint32_t cga = ((lerp2_(tga, bga, iwy, wy) + 0x00800080u) >> 8) & 0x00FF00FFu;
     return crb | (cga << 8);
+}
+template <typename Quad>
+GEO_HD uint32_t sample_sky_quad(const Quad& quad, uint32_t tw, uint32_t th, float U, float V) {
+    return sample_sky_quad_f(quad, (float)tw * 256.0f, (float)th * 256.0f, U, V);
 }
 
 template <typename Fetch>
@@ -944,12 +963,16 @@ GEO_HD uint32_t composite_(uint32_t s, uint32_t d) {
 // alpha 1.  `opaque` (every texel alpha 255, checked on upload) skips the
 // blend, which is exact there.
 template <typename Quad>
-GEO_HD uint32_t sample_sky_q(const Quad& quad, uint32_t tw, uint32_t th, bool opaque, float U, float V) {
-    const uint32_t s = sample_sky_quad(quad, tw, th, U, V);
+GEO_HD uint32_t sample_sky_qf(const Quad& quad, float tw256, float th256, bool opaque, float U, float V) {
+    const uint32_t s = sample_sky_quad_f(quad, tw256, th256, U, V);
     if (opaque) return s | 0xFF000000u;
     const uint32_t a = s >> 24;
     return blend255_(s & 0xFFu, a) | (blend255_((s >> 8) & 0xFFu, a) << 8) |
            (blend255_((s >> 16) & 0xFFu, a) << 16) | 0xFF000000u;
+}
+template <typename Quad>
+GEO_HD uint32_t sample_sky_q(const Quad& quad, uint32_t tw, uint32_t th, bool opaque, float U, float V) {
+    return sample_sky_qf(quad, (float)tw * 256.0f, (float)th * 256.0f, opaque, U, V);
 }
 template <typename Fetch>
 GEO_HD uint32_t sample_sky(Fetch fetch, uint32_t tw, uint32_t th, bool opaque, float U, float V) {

@@ -57,6 +57,7 @@ struct RenderArgs {
     float kt;
     const uint32_t* sky;  // padded (geo::pad_sky): (sky_w + 2) x (sky_h + 2) texels
     uint32_t sky_w, sky_h;
+    float sky_w256, sky_h256;  // sky_w * 256, sky_h * 256 (exact; geo::sample_sky_quad_f)
     uint32_t sky_pitch_b, sky_bytes;
     const float* fan;
     uint32_t n_fan;
@@ -120,11 +121,11 @@ __device__ __forceinline__ void shade_pixel(const RenderArgs& a, float c2x, floa
     if (a.composite) {
         // over the previous spheres; a discarded pixel keeps the target
         if (!bh) {
-            const uint32_t s = geo::sample_sky_quad(quad, a.sky_w, a.sky_h, U, V);
+            const uint32_t s = geo::sample_sky_quad_f(quad, a.sky_w256, a.sky_h256, U, V);
             a.out_rgba[o] = a.sky_opaque ? s : geo::composite_(s, a.out_rgba[o]);
         }
     } else {
-        a.out_rgba[o] = bh ? geo::kBlackRGBA : geo::sample_sky_q(quad, a.sky_w, a.sky_h, a.sky_opaque != 0, U, V);
+        a.out_rgba[o] = bh ? geo::kBlackRGBA : geo::sample_sky_qf(quad, a.sky_w256, a.sky_h256, a.sky_opaque != 0, U, V);
     }
     if (a.out_mask) a.out_mask[o] = bh ? 1 : 0;
     if (a.out_uv) a.out_uv[o] = make_float2(U, V);
@@ -608,6 +609,8 @@ static int render_impl(geo_ctx* c, const geo_frame* frame, const geo_scene* scen
     a.sky = c->sky;
     a.sky_w = c->sky_w;
     a.sky_h = c->sky_h;
+    a.sky_w256 = (float)c->sky_w * 256.0f;
+    a.sky_h256 = (float)c->sky_h * 256.0f;
     a.sky_pitch_b = (c->sky_w + 2u) * 4u;
     a.sky_bytes = a.sky_pitch_b * (c->sky_h + 2u);
     a.fan = c->fan;

@@ -66,6 +66,10 @@ struct PixelConsts {
     float radial_falling, radial_outgoing;  // result for rotation < 1e-10, by `falling`
     bool radial_by_energy;                  // radial result decided by energy > 0 instead
     bool pf_always, pf_falling, pf_outgoing, pf_eneg, pf_barrier;
+    // device forms of the same tests (geodesic_init): the barrier term as one
+    // compare, `inv_b2 < barrier_lim` (-inf when pf_barrier is off), and the
+    // squared outside-horizon energy
+    float barrier_lim, e_out2;
     // the integrator's scaled state U = scale*u (scale = 3 rs/2, or 1 for rs = 0)
     float scale, U0, SU, BD, HU;
     float SUp;  // next float above SU: (U > SU) == (U >= SUp) for every float U
@@ -99,6 +103,23 @@ GEO_HD float med3_(float x, float lo, float hi) {
     return m < hi ? m : hi;
 #endif
 }
+
+// c ? a : b for a lane condition c and frame-uniform a, b, as scalar lane-mask
+// ops: lane_mask_(c) is the wave's ballot of c (taken where c is computed: a
+// ballot of a condition from an earlier block costs two VALU to rebuild it),
+// lane_select_ picks by it with an inverse ballot.  hipcc otherwise selects
+// the flag bytes per lane in VGPRs.
+#if defined(__HIP_DEVICE_COMPILE__)
+typedef uint64_t LaneMask;
+GEO_HD LaneMask lane_mask_(bool c) { return __builtin_amdgcn_ballot_w64(c); }
+GEO_HD bool lane_select_(LaneMask m, bool a, bool b) {
+    return __builtin_amdgcn_inverse_ballot_w64((a ? m : 0ull) | (b ? ~m : 0ull));
+}
+#else
+typedef bool LaneMask;
+GEO_HD LaneMask lane_mask_(bool c) { return c; }
+GEO_HD bool lane_select_(LaneMask m, bool a, bool b) { return m ? a : b; }
+#endif
 
 // tol: GEO_MODE_ADAPTIVE local error tolerance in u (<= 0: the default 1e-6).
 GEO_HD PixelConsts make_consts(float rs, float sphere_r, float r, float step, uint32_t max_steps,
@@ -154,6 +175,8 @@ GEO_HD PixelConsts make_consts(float rs, float sphere_r, float r, float step, ui
     k.pf_barrier = k.rs > 0.0f && k.diff_sides;     // & 1/b^2 < 4/(27 rs^2)
     k.pf_falling = r < k.r3_2 && k.inside_sphere;   // & falling
     k.pf_outgoing = r > k.r3_2 && !k.inside_sphere; // & !falling
+    k.barrier_lim = k.pf_barrier ? k.barrier_thresh : -__builtin_inff();
+    k.e_out2 = k.e_out * k.e_out;
     k.scale = k.rs_nonzero ? k.r3_2 : 1.0f;
     k.U0 = k.scale * k.u0;
     k.SU = k.scale * k.sphere_u;
@@ -250,30 +273,40 @@ GEO_HD float newton_angle(const PixelConsts& k, float U, float UB, float NU, flo
 // and rct = rcpf_(ct), which the pixel shares with its sky direction (sky_uv).
 // Returns false with the traveled angle in *early (radial case, pre-filter
 // or failed initial loop test); else the scaled initial state (U, UB).
+//
+// KIND is the frame-uniform integration kind (geodesic_kind).  Outside the
+// horizon (kCurvedOut, kFlat) the energy is the frame constant e_out and the
+// pf_eneg term and the energy-decided radial case cannot occur (both need
+// r <= rs), so the per-lane tests are the compares on st and 1/b^2 alone
+// (their lane masks combine with the frame-uniform flags in scalar ops).
+template <int KIND>
 GEO_HD bool geodesic_init(const PixelConsts& k, float st, float ct, float rct, float* early, float* U0,
                           float* UB0) {
     // solve_ray_fan per node (:38-49)
     const float rotation = k.r * ct;
     bool falling;
-    float energy;
-    if (k.r_inside_h) {
+    float energy, e2;
+    if (KIND == kCurvedIn && k.r_inside_h) {
         falling = false;
         energy = (-st) * k.e_in;
+        e2 = energy * energy;
     } else {
         falling = st > 0.0f;
         energy = k.e_out;
+        e2 = k.e_out2;
     }
+    const LaneMask falling_m = lane_mask_(falling);
     // radial rays (:67-104), frame-uniform table
     if (rotation < 1e-10f) {
-        *early = k.radial_by_energy ? (energy > 0.0f ? 0.0f : kNoValue)
-                                    : (falling ? k.radial_falling : k.radial_outgoing);
+        *early = (KIND == kCurvedIn && k.radial_by_energy) ? (energy > 0.0f ? 0.0f : kNoValue)
+                                                           : (falling ? k.radial_falling : k.radial_outgoing);
         return false;
     }
     // 1/b^2 with b = rotation/energy = r ct/energy (:61), from the pixel's 1/ct
-    const float inv_b2 = (energy * energy) * ((rct * rct) * k.inv_r2);
+    const float inv_b2 = e2 * ((rct * rct) * k.inv_r2);
     // pre-filters (:106-119), frame-uniform terms precomputed
-    if (k.pf_always | (k.pf_eneg & (energy < 0.0f)) | (k.pf_barrier & (inv_b2 < k.barrier_thresh)) |
-        (k.pf_falling & falling) | (k.pf_outgoing & !falling)) {
+    const bool eneg = KIND == kCurvedIn && k.pf_eneg && energy < 0.0f;
+    if (k.pf_always || eneg || inv_b2 < k.barrier_lim || lane_select_(falling_m, k.pf_falling, k.pf_outgoing)) {
         *early = kNoValue;
         return false;
     }
@@ -281,8 +314,9 @@ GEO_HD bool geodesic_init(const PixelConsts& k, float st, float ct, float rct, f
     // NaN there only for |theta| < ~1e-8, never at a fan node).
     float ub = sqrtf_(fmaxf_(0.0f, inv_b2 - k.h_over_r2));
     if (!falling) ub = -ub;
-    // loop test of :134-135 on the initial state (schwarz_u = +inf for rs = 0)
-    if ((k.u0 > k.schwarz_u && ub > 0.0f) || k.max_steps == 0u || !(k.u0 > 0.0f)) {
+    // loop test of :134-135 on the initial state (schwarz_u = +inf for rs = 0;
+    // u0 > schwarz_u needs r < rs)
+    if ((KIND == kCurvedIn && k.u0 > k.schwarz_u && ub > 0.0f) || k.max_steps == 0u || !(k.u0 > 0.0f)) {
         *early = kNoValue;
         return false;
     }
@@ -375,9 +409,11 @@ GEO_HD uint32_t run_groups(const StopTest<KIND>& stop_at, uint32_t ngroups, uint
 // group would pay for.
 #if defined(__HIP_DEVICE_COMPILE__)
 GEO_HD uint64_t ballot_(bool p) { return __builtin_amdgcn_ballot_w64(p); }
+GEO_HD bool in_ballot_(uint64_t m) { return __builtin_amdgcn_inverse_ballot_w64(m); }
 #define GEO_RARE() asm volatile("")
 #else
 GEO_HD uint64_t ballot_(bool p) { return p ? 1u : 0u; }
+GEO_HD bool in_ballot_(uint64_t m) { return m != 0; }
 #define GEO_RARE() ((void)0)
 #endif
 
@@ -388,14 +424,27 @@ GEO_HD void group_steps_(float u, float b, float h, float hh, float hh2, float h
     for (int j = 0; j < G; ++j)
         rk4_step<KIND>(j ? ou[j - 1] : u, j ? ob[j - 1] : b, h, hh, hh2, hhh, h6, h2_6, &ou[j], &ob[j]);
 }
-// The stop flag of a group (its last state where the stop set is absorbing).
+// The lanes whose group stops (the last state's test where the stop set is
+// absorbing), as a wave mask.  hipcc takes the ballot of a single compare as
+// its mask but rebuilds any other condition through a VGPR (two VALU): with
+// the per-step interval test (one compare per state) the G ballots are ORed
+// in scalar ops; the compound test inside the horizon is ORed first and
+// balloted once.
 template <int G, int KIND, bool LAST_ONLY>
-GEO_HD bool group_stop_(const StopTest<KIND>& stop_at, const float (&ou)[G], const float (&ob)[G]) {
-    if constexpr (LAST_ONLY) return stop_at(ou[G - 1], ob[G - 1]);
-    bool s = false;
+GEO_HD uint64_t group_stop_(const StopTest<KIND>& stop_at, const float (&ou)[G], const float (&ob)[G]) {
+    if constexpr (LAST_ONLY) {
+        return ballot_(stop_at(ou[G - 1], ob[G - 1]));
+    } else if constexpr (KIND == kCurvedIn) {
+        bool s = false;
 #pragma unroll
-    for (int j = 0; j < G; ++j) s = s | stop_at(ou[j], ob[j]);
-    return s;
+        for (int j = 0; j < G; ++j) s = s | stop_at(ou[j], ob[j]);
+        return ballot_(s);
+    } else {
+        uint64_t m = 0;
+#pragma unroll
+        for (int j = 0; j < G; ++j) m |= ballot_(stop_at(ou[j], ob[j]));
+        return m;
+    }
 }
 
 template <int G, int KIND, bool LAST_ONLY>
@@ -429,9 +478,9 @@ GEO_HD uint32_t run_groups_pp(const StopTest<KIND>& stop_at, uint32_t ngroups, u
     // flag is garbage but harmless: `live` only ever loses bits.
     while (q < ngroups) {
         if (!done) group_steps_<G, KIND>(xu, xb, h, hh, hh2, hhh, h6, h2_6, au, ab);
-        bool hit = group_stop_<G, KIND, LAST_ONLY>(stop_at, au, ab);
-        live &= ~ballot_(hit);
-        if (hit && !done) {
+        uint64_t hit = group_stop_<G, KIND, LAST_ONLY>(stop_at, au, ab);
+        live &= ~hit;
+        if (in_ballot_(hit) && !done) {
             GEO_RARE();
             done = true;
             it = q * (uint32_t)G;
@@ -459,8 +508,8 @@ GEO_HD uint32_t run_groups_pp(const StopTest<KIND>& stop_at, uint32_t ngroups, u
         tu[G - 1] = xu;
         tb[G - 1] = xb;
         hit = group_stop_<G, KIND, LAST_ONLY>(stop_at, tu, tb);
-        live &= ~ballot_(hit);
-        if (hit && !done) {
+        live &= ~hit;
+        if (in_ballot_(hit) && !done) {
             GEO_RARE();
             done = true;
             it = q * (uint32_t)G;
@@ -542,7 +591,7 @@ template <int LOOP, int KIND>
 GEO_HD float geodesic_angle_v(const PixelConsts& k, float st, float ct, float rct, uint32_t* steps) {
     *steps = 0;
     float U, UB, early;
-    if (!geodesic_init(k, st, ct, rct, &early, &U, &UB)) return early;
+    if (!geodesic_init<KIND>(k, st, ct, rct, &early, &U, &UB)) return early;
     float h = k.step, hh = k.hh, hh2 = k.hh2, hhh = k.hhh, h6 = k.h6, h2_6 = k.h2_6;
     // Main loop (:134-191), restructured for the wave64 VALU: per step the
     // lane-exit flag is StopTest (crossing | escape | horizon); the budget
@@ -669,7 +718,7 @@ template <int KIND>
 GEO_HD float geodesic_angle_adaptive(const PixelConsts& k, float st, float ct, float rct, uint32_t* steps) {
     *steps = 0;
     float U, V, early;
-    if (!geodesic_init(k, st, ct, rct, &early, &U, &V)) return early;
+    if (!geodesic_init<KIND>(k, st, ct, rct, &early, &U, &V)) return early;
     const StopTest<KIND> stop_at(k);
     const uint32_t ms = k.max_steps;
     float h = k.step, ang = 0.0f;

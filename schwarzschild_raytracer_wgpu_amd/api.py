@@ -138,10 +138,13 @@ class Context:
         check("geo_set_fan", lib.geo_set_fan(self._h, a.ctypes.data, a.size))
 
     def solve_ray_fan(self, sphere_r: float, schwarz_r: float, max_iter: int, step: float, nr_nodes: int,
-                      r: float, stream=None) -> np.ndarray:
-        out = np.empty(nr_nodes, dtype=np.float32)
+                      r: float, stream=None, host: bool = True) -> np.ndarray | None:
+        """geo_solve_ray_fan: the context's fan, solved on the device.  host=True also
+        returns it (synchronises `stream`); host=False leaves it stream-ordered on the
+        device only, for the fan-mode draws that follow on `stream`."""
+        out = np.empty(nr_nodes, dtype=np.float32) if host else None
         check("geo_solve_ray_fan", lib.geo_solve_ray_fan(self._h, sphere_r, schwarz_r, max_iter, step, nr_nodes, r,
-                                                         out.ctypes.data, _stream_handle(stream)))
+                                                         out.ctypes.data if host else None, _stream_handle(stream)))
         return out
 
     def steps_flush(self, steps_total, stream=None) -> None:
@@ -251,6 +254,12 @@ class SphereRayTracer:
                                                          self.default_step, self.nr_nodes, r)
         return self.interpolation_grid
 
+    def update_device_fan(self, r: float, stream=None) -> None:
+        """The fan for observer radius r into the context only (stream-ordered, no
+        host copy): what a fan-mode draw reads.  interpolation_grid is not updated."""
+        self.ctx.solve_ray_fan(self.sphere_r, self.schwarz_r, self.max_iter, self.default_step, self.nr_nodes, r,
+                               stream=stream, host=False)
+
 
 @dataclass
 class RenderTarget:
@@ -289,12 +298,15 @@ class BasicSphereBuffer:
         self.ray_tracer = SphereRayTracer(sphere_radius, schwarz_radius, max_iter, step, self.NR_NODES_HALF, ctx)
         self.radial_position = None
 
-    def update_ray_fan(self, radial_position: float) -> None:
-        """basic_sphere_buffer.rs:85-88.  The fan is only consumed in fan mode;
-        direct mode integrates per pixel, so it just records r."""
+    def update_ray_fan(self, radial_position: float, stream=None) -> None:
+        """basic_sphere_buffer.rs:85-88.  The fan is only consumed in fan mode,
+        where it is solved into the sphere's context on `stream` (the reference
+        writes it into the sphere's fan texture; no host copy, so a frame loop
+        does not synchronise); direct mode integrates per pixel, so it just
+        records r."""
         self.radial_position = radial_position
         if self.mode == _lib.GEO_MODE_FAN:
-            self.ray_tracer.solve_ray_fan(radial_position)
+            self.ray_tracer.update_device_fan(radial_position, stream=stream)
 
     def scene(self) -> GeoScene:
         if self.radial_position is None:

@@ -301,10 +301,11 @@ __global__ __launch_bounds__(kStepSlots) void geo_steps_finalize(unsigned long l
 }
 
 // f64 restatement of SphereRayTracer::solve_geodesic (sphere_ray_tracer.rs:60-193),
-// operation for operation (no contraction).
-__device__ double solve_geodesic_f64(double sphere_r, double schwarz_r, uint32_t max_iter,
-                                     double default_step, double r, double energy,
-                                     double rotation, bool r_falling) {
+// operation for operation (no contraction).  The radial cases and
+// pre-filters (:60-119): false with the result in *early, else the initial
+// u' (:123).
+__device__ bool solve_geodesic_f64_init(double sphere_r, double schwarz_r, double r, double energy, double rotation,
+                                        bool r_falling, double* early, double* u_bar0) {
     const double NO_VALUE = GEO_NO_VALUE;
     const double PI = 3.14159265358979323846;
     const double b = rotation / energy;
@@ -313,14 +314,14 @@ __device__ double solve_geodesic_f64(double sphere_r, double schwarz_r, uint32_t
     const bool inside_sphere = r < sphere_r;
     if (rotation < 1e-10) {
         if (inside_sphere) {
-            if (outside) {
-                if (r_falling) return schwarz_r == 0. ? PI : NO_VALUE;
-                return 0.;
-            }
-            if (sphere_outside) return energy > 0. ? 0. : NO_VALUE;
-            return 0.;
+            if (outside)
+                *early = r_falling ? (schwarz_r == 0. ? PI : NO_VALUE) : 0.;
+            else
+                *early = sphere_outside ? (energy > 0. ? 0. : NO_VALUE) : 0.;
+        } else {
+            *early = (sphere_outside && r_falling) ? 0. : NO_VALUE;
         }
-        return (sphere_outside && r_falling) ? 0. : NO_VALUE;
+        return false;
     }
     const bool barrier_3r_2 = (schwarz_r > 0.) && 1. / (b * b) < 4. / (27. * schwarz_r * schwarz_r);
     const double r3_2 = 3. * schwarz_r / 2.;
@@ -328,10 +329,20 @@ __device__ double solve_geodesic_f64(double sphere_r, double schwarz_r, uint32_t
     if ((inside_sphere && !sphere_outside) || (!outside && sphere_outside && energy < 0.) ||
         (barrier_3r_2 && different_sides_3r_2) || (r < r3_2 && inside_sphere && r_falling) ||
         (r > r3_2 && !inside_sphere && !r_falling)) {
-        return NO_VALUE;
+        *early = NO_VALUE;
+        return false;
     }
+    *u_bar0 = (r_falling ? 1. : -1.) * sqrt(1. / (b * b) - (1. - schwarz_r / r) / (r * r));
+    return true;
+}
+
+// The literal main loop (:121-193) from the initial state (GEO_FAN_LITERAL 1).
+__device__ double solve_geodesic_f64_loop(double sphere_r, double schwarz_r, uint32_t max_iter,
+                                          double default_step, double r, double u_bar0) {
+    const double NO_VALUE = GEO_NO_VALUE;
+    const double r3_2 = 3. * schwarz_r / 2.;
     double u_k = 1. / r;
-    double u_bar_k = (r_falling ? 1. : -1.) * sqrt(1. / (b * b) - (1. - schwarz_r / r) / (r * r));
+    double u_bar_k = u_bar0;
     double angle = 0.;
     uint32_t iteration = 0;
     const double bound = 0.9 * fmin(u_k, 1. / fmax(sphere_r, r3_2));
@@ -388,6 +399,124 @@ __device__ double solve_geodesic_f64(double sphere_r, double schwarz_r, uint32_t
     return NO_VALUE;
 }
 
+// The same f64 solve, restructured for latency (GEO_FAN_LITERAL 0, the
+// default).  A fan is one lane per node, 400 lanes = 7 waves, so its time is
+// the longest node's dependent chain: the literal loop spends ~60 f64
+// instructions per step (two f64 divisions by 6 among them), this one the
+// scaled 14-op RK4 of the f32 kernel (geo_pixel.h rk4_step) in f64 --
+// U = c u, c = 3 rs/2 (1 for rs = 0), F(U) = U(U - 1) (-U in flat space),
+// the thresholds scaled alike, Newton's ratio scale-free.  It is the same
+// algorithm (stages, tests, Newton) with a different rounding of the f64
+// intermediates: the fan agrees with the literal f64 restatement to within
+// one f32 ulp (tests/test_gpu_parity.py, the fan tolerance).
+#ifndef GEO_FAN_LITERAL
+#define GEO_FAN_LITERAL 0
+#endif
+template <bool FLAT>
+__device__ __forceinline__ double fan_F(double U) {
+    return FLAT ? -U : __builtin_fma(U, U, -U);
+}
+template <bool FLAT>
+__device__ __forceinline__ void fan_rk4(double U, double V, double h, double hh, double hh2, double hhh, double h6,
+                                        double h2_6, double* NU, double* NV) {
+    const double fu = fan_F<FLAT>(U);
+    const double au = __builtin_fma(hh, V, U);
+    const double uh = __builtin_fma(h, V, U);
+    const double fa = fan_F<FLAT>(au);
+    const double bu = __builtin_fma(hh2, fu, au);
+    const double fb = fan_F<FLAT>(bu);
+    const double cu = __builtin_fma(hhh, fa, uh);
+    const double fc = fan_F<FLAT>(cu);
+    const double fab = fa + fb;
+    *NU = __builtin_fma(h2_6, fu + fab, uh);
+    *NV = __builtin_fma(h6, __builtin_fma(2.0, fab, fu) + fc, V);
+}
+// One step of the literal loop's tests (:134, :150, :184) from (U, V) to
+// (NU, NV): 0 continue, 1 crossing (Newton), 2 stop without a value.
+template <bool FLAT>
+__device__ __forceinline__ int fan_test(double U, double V, double NU, double SU, double BD, double HU) {
+    if (!FLAT && U > HU && V > 0.) return 2;  // the loop test on the pre-step state (:134)
+    if ((NU > SU) != (U > SU)) return 1;
+    if (NU < BD) return 2;
+    return 0;
+}
+// A lane's chain of RK4 steps is the fan's critical path, so the exit branch
+// (which waits for the newest state's compares) is taken once per kFanGroup
+// steps: the group's flags are formed without branches, and a group that
+// stops is replayed step by step from its start (the same arithmetic, so the
+// same result as testing every step).
+#ifndef GEO_FAN_GROUP
+#define GEO_FAN_GROUP 4
+#endif
+constexpr int kFanGroup = GEO_FAN_GROUP;
+template <bool FLAT>
+__device__ double fan_integrate(double sphere_r, double schwarz_r, uint32_t max_iter, double step, double r,
+                                double u_bar0) {
+    const double NO_VALUE = GEO_NO_VALUE;
+    const double r3_2 = 3. * schwarz_r / 2.;
+    const double c = FLAT ? 1. : r3_2;
+    const double u0 = 1. / r;
+    const double SU = c / sphere_r;                                      // sphere_u
+    const double BD = c * (0.9 * fmin(u0, 1. / fmax(sphere_r, r3_2)));  // bound
+    const double HU = FLAT ? __builtin_inf() : c / schwarz_r;           // schwarz_u
+    const double h = step, hh = step / 2., hh2 = step * step / 4., hhh = step * step / 2., h6 = step / 6.,
+                 h2_6 = step * step / 6.;
+    double U = c * u0, V = c * u_bar0;
+    if (!(U > 0.)) return NO_VALUE;
+    double angle = 0.;
+    uint32_t it = 0;
+    // whole groups while the budget allows; a stopping group falls through
+    // to the per-step loop below from its start state
+    while (it + kFanGroup <= max_iter) {
+        double su[kFanGroup + 1], sv[kFanGroup + 1];
+        su[0] = U;
+        sv[0] = V;
+        bool stop = false;
+#pragma unroll
+        for (int j = 0; j < kFanGroup; ++j) {
+            fan_rk4<FLAT>(su[j], sv[j], h, hh, hh2, hhh, h6, h2_6, &su[j + 1], &sv[j + 1]);
+            stop |= fan_test<FLAT>(su[j], sv[j], su[j + 1], SU, BD, HU) != 0;
+        }
+        if (stop) break;
+        U = su[kFanGroup];
+        V = sv[kFanGroup];
+#pragma unroll
+        for (int j = 0; j < kFanGroup; ++j) angle += step;  // the literal accumulation (:190)
+        it += kFanGroup;
+    }
+    for (; it < max_iter; ++it) {
+        double NU, NV;
+        fan_rk4<FLAT>(U, V, h, hh, hh2, hhh, h6, h2_6, &NU, &NV);
+        const int t = fan_test<FLAT>(U, V, NU, SU, BD, HU);
+        if (t == 2) return NO_VALUE;
+        if (t == 1) {
+            // Newton on the step length from the steeper end (:150-182)
+            double ns, wu, wv;
+            if (fabs(V) > fabs(NV)) {
+                ns = 0.;
+                wu = U;
+                wv = V;
+            } else {
+                ns = h;
+                wu = NU;
+                wv = NV;
+            }
+            for (int n = 0; n < 3; ++n) {
+                ns -= (wu - SU) / wv;
+                const double n2 = ns * ns;
+                fan_rk4<FLAT>(U, V, ns, ns / 2., n2 / 4., n2 / 2., ns / 6., n2 / 6., &wu, &wv);
+            }
+            return angle + ns;
+        }
+        U = NU;
+        V = NV;
+        angle += step;
+    }
+    // budget exhausted; the literal loop re-tests the final state only
+    // against :134 and `u > 0`, both of which end without a value too
+    return NO_VALUE;
+}
+
 __global__ void geo_fan_kernel(double sphere_r, double schwarz_r, uint32_t max_iter, double step,
                                uint32_t n, double r, float* fan) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -406,8 +535,16 @@ __global__ void geo_fan_kernel(double sphere_r, double schwarz_r, uint32_t max_i
         r_falling = theta > 0.;
         energy = sqrt(1. - schwarz_r / r);
     }
-    fan[i] = (float)(FRAC_PI_2 -
-                     solve_geodesic_f64(sphere_r, schwarz_r, max_iter, step, r, energy, rotation, r_falling));
+    double angle, u_bar0;
+    if (solve_geodesic_f64_init(sphere_r, schwarz_r, r, energy, rotation, r_falling, &angle, &u_bar0)) {
+#if GEO_FAN_LITERAL
+        angle = solve_geodesic_f64_loop(sphere_r, schwarz_r, max_iter, step, r, u_bar0);
+#else
+        angle = schwarz_r == 0. ? fan_integrate<true>(sphere_r, schwarz_r, max_iter, step, r, u_bar0)
+                                : fan_integrate<false>(sphere_r, schwarz_r, max_iter, step, r, u_bar0);
+#endif
+    }
+    fan[i] = (float)(FRAC_PI_2 - angle);
 }
 
 }  // namespace

@@ -198,8 +198,8 @@ def test_sphere_buffer_fan_mode_matches_oracle(geo, torch_mod):
     sky = make_sky("equirect", (512, 256))
     ctx = geo.Context(0)
     buf = geo.BasicSphereBuffer(ctx, 50.0, 1.0, sky, mode=geo.GEO_MODE_FAN)
-    buf.update_ray_fan(R_OBS)
-    fan = buf.ray_tracer.interpolation_grid.copy()
+    buf.update_ray_fan(R_OBS)  # stream-ordered, device only
+    fan = buf.ray_tracer.solve_ray_fan(R_OBS).copy()  # the same fan, copied to the host for the oracle
     frame = default_frame(w, h)
     dev = torch_mod.device("cuda:0")
     tgt = geo.RenderTarget(w, h, torch_mod.empty(w * h * 4, dtype=torch_mod.uint8, device=dev),

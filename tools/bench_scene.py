@@ -13,7 +13,12 @@ each part's GPU time from event pairs (parts back to back on one stream).
 latency-bound (10 000 lanes of sequential 48-node solves) and hides under the
 VALU-bound sky draw; the point draw waits for it (geo_points_draw).
 
-  python tools/bench_scene.py [--width 3840 --height 2160] [--frames 200] [--points 5000] [--spheres 1|3] [--overlap 1|0]
+--mode fan draws every sphere the way the reference displays it: each frame
+solves the sphere's 400-node f64 ray fan (geo_solve_ray_fan, SphereRayTracer::
+solve_ray_fan, lib.rs:292-295) and the sky lerps into it per pixel
+(shader.wgsl:77-84); --mode direct (default) integrates every pixel.
+
+  python tools/bench_scene.py [--width 3840 --height 2160] [--frames 200] [--points 5000] [--spheres 1|3] [--overlap 1|0] [--mode direct|fan]
 
 Textures are synthetic (the reference's are absent): the benchmark equirect
 sky, a 2048x1024 checkerboard planet and a seeded random-alpha cloud layer.
@@ -46,6 +51,8 @@ def main():
     p.add_argument("--overlap", type=int, default=1, choices=[0, 1],
                    help="1: the disk update on a side stream, overlapping the sphere draws (geo_points_draw "
                         "orders the point draw after it); 0: everything on one stream")
+    p.add_argument("--mode", default="direct", choices=["direct", "fan"],
+                   help="direct: per-pixel geodesics; fan: the reference's per-frame 400-node fan + per-pixel lerp")
     args = p.parse_args()
 
     import numpy as np
@@ -61,23 +68,38 @@ def main():
     sky = make_sky("equirect", (4096, 2048))
     planet = make_sky("equirect", (2048, 1024), seed=7)
     clouds = np.random.default_rng(11).integers(0, 256, size=(1024, 2048, 4), dtype=np.uint8)
-    spheres = [g.BasicSphereBuffer(0, 50.0, 1.0, sky, max_iter=args.max_steps),
-               g.BasicSphereBuffer(0, 1.1, 1.0, planet, max_iter=args.max_steps),
-               g.BasicSphereBuffer(0, 1.2, 1.0, clouds, max_iter=args.max_steps)][:args.spheres]
+    mode = g.GEO_MODE_FAN if args.mode == "fan" else g.GEO_MODE_DIRECT
+    spheres = [g.BasicSphereBuffer(0, 50.0, 1.0, sky, max_iter=args.max_steps, mode=mode),
+               g.BasicSphereBuffer(0, 1.1, 1.0, planet, max_iter=args.max_steps, mode=mode),
+               g.BasicSphereBuffer(0, 1.2, 1.0, clouds, max_iter=args.max_steps, mode=mode)][:args.spheres]
     disk = g.PointCloud.new_accretion_disk(spheres[0].ctx, 1.0, obs.get_position(), True, n=args.points)
     tgt = g.RenderTarget(w, h, torch.empty(w * h * 4, dtype=torch.uint8, device="cuda:0"))
 
     parts = ("disk update", "sky", "planet", "clouds")[:2 + len(spheres) - 1] + ("points",)
     side = torch.cuda.Stream() if args.overlap else None
 
+    # fan mode with --overlap 1: the spheres' fans (latency-bound, one lane per
+    # node) solved concurrently, one stream each, after the previous frame's
+    # draws that read them; the draws wait for all three
+    fan_streams = [torch.cuda.Stream() for _ in spheres] if (args.mode == "fan" and args.overlap) else None
+
     def frame(evs=None):
         obs.update_position((0.0, 0.0, 0.0), 1 / 60)
         r = obs.get_radial_position()
-        for s in spheres:
-            s.update_ray_fan(r)  # records r (direct mode integrates per pixel)
+        if fan_streams is not None and not evs:
+            main = torch.cuda.current_stream()
+            for s, fs in zip(spheres, fan_streams):
+                fs.wait_stream(main)
+                with torch.cuda.stream(fs):
+                    s.update_ray_fan(r)
+            for fs in fan_streams:
+                main.wait_stream(fs)
+        else:
+            for s in spheres:
+                s.update_ray_fan(r)  # fan mode: the fan on the device; direct: records r
         f = obs.calc_transformation_pipeline()
-        if evs:  # per-part timing: the parts back to back on one stream
-            evs[0].record()
+        if evs:  # per-part timing: the parts back to back on one stream (fan mode: the fans lie before
+            evs[0].record()  # evs[0], in no part's time)
             disk.update(obs.get_position(), 1 / 60)
             evs[1].record()
         else:
@@ -112,6 +134,7 @@ def main():
                  "(orbits, 2 x RayConnector, point draws)" if len(spheres) == 1 else
                  "the reference's frame with its commented-out planet and clouds: 3 composited per-pixel geodesic "
                  "spheres + accretion disk (orbits, 2 x RayConnector, point draws)"),
+        "mode": args.mode,
         "spheres": len(spheres),
         "overlap": bool(args.overlap),
         "width": w, "height": h, "frames": args.frames, "points": args.points, "max_steps": args.max_steps,

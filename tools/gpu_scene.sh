@@ -15,6 +15,13 @@ for S in 1 3; do for OV in 0 1; do for WH in "3840 2160" "1920 1080"; do
         > $OUT/scene_${TAG}_s${S}_o${OV}_$2.json 2> $OUT/scene_${TAG}_s${S}_o${OV}_$2.err
     rc=$?; echo "scene s=$S overlap=$OV ${1}x$2 rc=$rc"; cat $OUT/scene_${TAG}_s${S}_o${OV}_$2.json; [ $rc -eq 0 ] || exit $rc
 done; done; done
+# the reference's display path: per-frame f64 fans + fan-lerp draws
+for S in 1 3; do for WH in "3840 2160" "1920 1080"; do
+    set -- $WH
+    timeout -k 10 120 python tools/bench_scene.py --mode fan --width $1 --height $2 --spheres $S --overlap 1 \
+        > $OUT/scene_${TAG}_fan_s${S}_$2.json 2> $OUT/scene_${TAG}_fan_s${S}_$2.err
+    rc=$?; echo "scene fan s=$S ${1}x$2 rc=$rc"; cat $OUT/scene_${TAG}_fan_s${S}_$2.json; [ $rc -eq 0 ] || exit $rc
+done; done
 g++ -std=c++17 -O2 -D__HIP_PLATFORM_AMD__ -I include -I /opt/rocm/include examples/frame_loop.cpp \
     -L schwarzschild_raytracer_wgpu_amd -lgeo -L /opt/rocm/lib -lamdhip64 -Wl,-rpath,$(pwd)/schwarzschild_raytracer_wgpu_amd \
     -Wl,-rpath,/opt/rocm/lib -o $OUT/frame_loop || exit 1

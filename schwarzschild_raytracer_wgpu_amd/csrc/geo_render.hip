@@ -11,7 +11,8 @@
 // Work decomposition: one 256-thread workgroup per 8x32 pixel tile, each
 // wave64 an 8x8 square (compact 2-D footprint = coherent step counts);
 // the frame uniform rides in the kernarg segment (SGPRs, wave-uniform), the
-// ray fan is staged in LDS; per-lane ray state lives in VGPRs.  The hot loop
+// ray fan (fan mode) is read from its cache-resident device copy; per-lane
+// ray state lives in VGPRs.  The hot loop
 // is pure FP32 VALU — no MFMA, no LDS, no memory traffic.
 #include <hip/hip_runtime.h>
 
@@ -25,6 +26,14 @@
 #include "geo_ctx.h"
 #include "geo_pixel.h"
 
+// fan mode: 0 reads the two nodes of a pixel's lerp from the context's
+// device copy (1.6 KB for 400 nodes, cache-resident; as the reference's
+// shader reads its fan texture); 1 stages the fan in LDS per workgroup, a
+// global load and a barrier before any pixel work: 6 % slower at 4K
+// (0.0464 vs 0.0492 ms)
+#ifndef GEO_FAN_LDS
+#define GEO_FAN_LDS 0
+#endif
 #ifndef GEO_BH_SKIP_UV
 #define GEO_BH_SKIP_UV 1
 #endif
@@ -134,11 +143,13 @@ __device__ __forceinline__ void shade_pixel(const RenderArgs& a, float c2x, floa
 
 template <int MODE, int KIND>
 __global__ __launch_bounds__(kBlock) void geo_render_kernel(const RenderArgs a) {
+#if GEO_FAN_LDS
     __shared__ float s_fan[MODE == GEO_MODE_FAN ? kMaxFan : 1];
     if constexpr (MODE == GEO_MODE_FAN) {
         for (uint32_t i = threadIdx.x; i < a.n_fan; i += kBlock) s_fan[i] = a.fan[i];
         __syncthreads();
     }
+#endif
     const uint32_t px = blockIdx.x * kTileW + (threadIdx.x % kTileW);
     const uint32_t ly = blockIdx.y * kTileH + (threadIdx.x / kTileW);
     // local row -> frame row.  band_rows is a multiple of 8 (checked on the
@@ -158,7 +169,11 @@ __global__ __launch_bounds__(kBlock) void geo_render_kernel(const RenderArgs a) 
         const float rct = geo::rcpf_(ct);  // shared by the ray's 1/b^2 and its sky direction
         float lam;
         if constexpr (MODE == GEO_MODE_FAN) {
+#if GEO_FAN_LDS
             lam = geo::fan_lerp(s_fan, a.n_fan, st);
+#else
+            lam = geo::fan_lerp(a.fan, a.n_fan, st);
+#endif
         } else if constexpr (MODE == GEO_MODE_ADAPTIVE) {
             lam = geo::kPi2 - geo::geodesic_angle_adaptive<KIND>(a.k, st, ct, rct, &steps);
         } else {

@@ -7,13 +7,18 @@
 // Build:
 //   g++ -std=c++17 -O2 -D__HIP_PLATFORM_AMD__ -I include -I /opt/rocm/include examples/frame_loop.cpp
 //       -L schwarzschild_raytracer_wgpu_amd -lgeo -L /opt/rocm/lib -lamdhip64 -o frame_loop
-//   ./frame_loop [W H FRAMES out.ppm OVERLAP(1|0)]
+//   ./frame_loop [W H FRAMES out.ppm OVERLAP(1|0) MODE(direct|fan)]
+//
+// MODE fan draws the sky the way the reference displays it: each frame solves
+// the sphere's 400-node f64 ray fan on the GPU (stream-ordered, no host copy)
+// and the shader lerps into it; direct (default) integrates every pixel.
 //
 // Prints frames/s of the whole loop (host + GPU, K frames back to back) and
 // writes the last frame.  Scene: the reference's, scaled to rs = 1 (its
 // schwarz_r = 10 scene divided by 10): sky r = 50 with a synthetic equirect
 // texture, observer FrozenFall from (2.5, 0, 0.1), 5000-point disk.
 #include <chrono>
+#include <string>
 #include <cstdio>
 #include <cstdlib>
 
@@ -25,6 +30,8 @@ int main(int argc, char** argv) {
     const int frames = argc > 3 ? std::atoi(argv[3]) : 300;
     const char* out = argc > 4 ? argv[4] : "frame_loop.ppm";
     const bool overlap = argc > 5 ? std::atoi(argv[5]) != 0 : true;
+    // "fan": the reference's display path (a 400-node f64 fan per frame, lerped per pixel)
+    const bool fan = argc > 6 && std::string(argv[6]) == "fan";
     try {
         sr::Image sky;
         sky.width = 2048;
@@ -42,7 +49,7 @@ int main(int argc, char** argv) {
 
         sr::Renderer renderer(W, H, 1.0, sr::kPi / 2);
         renderer.observer().set_position({2.5, 0.0, 0.1});
-        sr::BasicSphereBuffer first_sphere(0, 50.0, 1.0, sky);
+        sr::BasicSphereBuffer first_sphere(0, 50.0, 1.0, sky, fan ? GEO_MODE_FAN : GEO_MODE_DIRECT);
         sr::PointCloud first_point_cloud =
             sr::PointCloud::new_accretion_disk(0, 1.0f, renderer.get_position(), true);
 
@@ -74,8 +81,9 @@ int main(int argc, char** argv) {
         std::fprintf(f, "P6\n%u %u\n255\n", W, H);
         for (size_t i = 0; i < (size_t)W * H; ++i) std::fwrite(&rgba[4 * i], 1, 3, f);
         std::fclose(f);
-        std::printf("%ux%u%s: %d frames in %.3f s = %.1f frames/s (%.4f ms/frame); observer r = %.4f\n", W, H,
-                    overlap ? " (disk update on a side stream)" : "", frames, s, frames / s, s / frames * 1e3,
+        std::printf("%ux%u%s%s: %d frames in %.3f s = %.1f frames/s (%.4f ms/frame); observer r = %.4f\n", W, H,
+                    fan ? " fan mode" : "", overlap ? " (disk update on a side stream)" : "", frames, s, frames / s,
+                    s / frames * 1e3,
                     renderer.get_radial_position());
         if (side) sr::hip_check(hipStreamDestroy(side), "hipStreamDestroy");
         return 0;

@@ -197,6 +197,14 @@ class SphereRayTracer {
               "geo_solve_ray_fan");
         return grid_;
     }
+    // The fan at radius r into the context only, asynchronous on `stream`
+    // (no host copy, so a frame loop does not synchronise); the host grid
+    // is not updated.
+    void update_device_fan(double r, void* stream = nullptr) {
+        check(geo_solve_ray_fan(ctx_->get(), sphere_r_, schwarz_r_, max_iter_, default_step_, (uint32_t)grid_.size(),
+                                r, nullptr, stream),
+              "geo_solve_ray_fan");
+    }
     const std::shared_ptr<Context>& context() const { return ctx_; }
 
    private:
@@ -295,10 +303,12 @@ class BasicSphereBuffer : public SchwarzschildSphereShaderDraw {
     }
 
     // update_ray_fan (:85-88); the direct mode integrates per pixel, so the
-    // radius is all it needs
-    void update_ray_fan(double radial_position) {
+    // radius is all it needs.  In fan mode the fan is solved into the
+    // sphere's context on `stream` (the stream its draws run on: the
+    // Renderer's), as the reference writes it into the sphere's fan texture.
+    void update_ray_fan(double radial_position, void* stream = nullptr) {
         radial_position_ = radial_position;
-        if (mode_ == GEO_MODE_FAN) ray_tracer_.solve_ray_fan(radial_position);
+        if (mode_ == GEO_MODE_FAN) ray_tracer_.update_device_fan(radial_position, stream);
     }
 
     // SchwarzschildSphereShaderDraw::draw (:92-100) + fs_main over the pass's target

@@ -189,6 +189,22 @@ def test_fan_kernel_matches_oracle(geo, torch_mod):
         assert np.mean(gpu == ref) > 0.99
 
 
+@pytest.mark.parametrize("max_iter", [0, 1, 2, 3, 5, 7, 37, 250, 1001, 1003])
+def test_fan_kernel_budget_edges(geo, torch_mod, max_iter):
+    """The fan kernel takes its steps in groups of 4 with a per-step tail for
+    the budget's remainder: budgets on and off the group size end each node
+    where the literal loop does (NO_VALUE on exhaustion, a crossing on the
+    last allowed step still counts)."""
+    ctx = geo.Context(0)
+    for sphere_r, rs, r in [(50.0, 1.0, R_OBS), (500.0, 10.0, 25.0), (50.0, 0.0, 3.0)]:
+        args = (sphere_r, rs, max_iter, math.pi / 100, 400, r)
+        gpu = ctx.solve_ray_fan(*args)
+        ref = O.solve_ray_fan(*args)
+        d = np.abs(gpu.astype(np.float64) - ref)
+        assert np.all(d <= np.spacing(np.abs(ref)).astype(np.float64)), (args, d.max())
+        assert np.mean(gpu == ref) > 0.99, args
+
+
 def test_sphere_buffer_fan_mode_matches_oracle(geo, torch_mod):
     """Reference-exact mode: BasicSphereBuffer.update_ray_fan + draw = fan lerp
     (shader.wgsl:77-84) with the GPU-solved fan."""

@@ -29,6 +29,10 @@ for OV in 1 0; do
     timeout -k 10 120 $OUT/frame_loop 3840 2160 1000 $OUT/fl4k_$OV.ppm $OV >> $OUT/frame_loop_$TAG.txt || exit $?
     timeout -k 10 120 $OUT/frame_loop 1920 1080 2000 $OUT/fl1080_$OV.ppm $OV >> $OUT/frame_loop_$TAG.txt || exit $?
 done
+for WH in "3840 2160" "1920 1080"; do
+    set -- $WH
+    timeout -k 10 120 $OUT/frame_loop $1 $2 2000 $OUT/flfan_$2.ppm 1 fan >> $OUT/frame_loop_$TAG.txt || exit $?
+done
 cat $OUT/frame_loop_$TAG.txt
 cmp $OUT/fl4k_0.ppm $OUT/fl4k_1.ppm && cmp $OUT/fl1080_0.ppm $OUT/fl1080_1.ppm && echo "frames equal"
 rm -f $OUT/fl*.ppm

@@ -56,14 +56,19 @@ int main(int argc, char** argv) {
         // The disk update is latency-bound (one lane per connector, sequential
         // 48-node solves): on a side stream it overlaps the VALU-bound sky
         // draw; PointCloud::draw waits for it (geo_points_draw).
-        hipStream_t side = nullptr;
+        hipStream_t side = nullptr, fan_stream = nullptr;
         if (overlap) sr::hip_check(hipStreamCreateWithFlags(&side, hipStreamNonBlocking), "hipStreamCreate");
+        // Fan mode: the frame's fan on its own stream.  The context double-buffers
+        // the fan and orders solves and draws with events, so this frame's fan
+        // overlaps the previous frame's draws and its own draw still waits for it.
+        if (overlap && fan)
+            sr::hip_check(hipStreamCreateWithFlags(&fan_stream, hipStreamNonBlocking), "hipStreamCreate");
         const double dt = 1.0 / 60.0;
         auto frame = [&]() {
             // State::update (lib.rs:287-300)
             renderer.update(dt);
             const double r = renderer.get_radial_position();
-            first_sphere.update_ray_fan(r);
+            first_sphere.update_ray_fan(r, fan_stream);
             first_point_cloud.update(renderer.get_position(), dt, side);
             // State::render (lib.rs:413-419): the first sphere and both point meshes
             renderer.render({&first_sphere}, {&first_point_cloud});
@@ -82,10 +87,11 @@ int main(int argc, char** argv) {
         for (size_t i = 0; i < (size_t)W * H; ++i) std::fwrite(&rgba[4 * i], 1, 3, f);
         std::fclose(f);
         std::printf("%ux%u%s%s: %d frames in %.3f s = %.1f frames/s (%.4f ms/frame); observer r = %.4f\n", W, H,
-                    fan ? " fan mode" : "", overlap ? " (disk update on a side stream)" : "", frames, s, frames / s,
+                    fan ? " fan mode" : "", overlap ? (fan ? " (disk update and fans on side streams)" : " (disk update on a side stream)") : "", frames, s, frames / s,
                     s / frames * 1e3,
                     renderer.get_radial_position());
         if (side) sr::hip_check(hipStreamDestroy(side), "hipStreamDestroy");
+        if (fan_stream) sr::hip_check(hipStreamDestroy(fan_stream), "hipStreamDestroy");
         return 0;
     } catch (const sr::Error& e) {
         std::fprintf(stderr, "sr::Error: %s\n", e.what());

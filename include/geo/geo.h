@@ -140,8 +140,14 @@ int geo_set_fan(geo_ctx* ctx, const float* fan, uint32_t n);
 
 /* Computes the ray fan on the GPU in f64 (SphereRayTracer::solve_ray_fan,
  * sphere_ray_tracer.rs:35-193) for nr_nodes nodes at observer radius r and
- * makes it the context's fan.  When fan_out (host) is non-NULL the call
- * synchronises `stream` and copies the nr_nodes f32 values there. */
+ * makes it the context's fan: fan-mode renders issued after this call read
+ * it.  Asynchronous on `stream`; the context keeps two fan buffers and
+ * orders them itself, so the stream need not be the renders' stream: the
+ * solve waits for the renders that read the buffer it overwrites (issued
+ * before the previous solve), and a render waits for the solve of the fan it
+ * reads.  A fan solved on a side stream thus overlaps the previous frame's
+ * draws.  When fan_out (host) is non-NULL the call synchronises `stream` and
+ * copies the nr_nodes f32 values there. */
 int geo_solve_ray_fan(geo_ctx* ctx, double sphere_r, double schwarz_r, uint32_t max_iter,
                       double step, uint32_t nr_nodes, double r, float* fan_out, void* stream);
 

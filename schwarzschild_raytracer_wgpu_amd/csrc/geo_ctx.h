@@ -12,8 +12,19 @@ struct geo_ctx {
     uint32_t* sky;
     uint32_t sky_w, sky_h;
     bool sky_opaque;
-    float* fan;
-    uint32_t fan_cap, n_fan;
+    // Ray fan, double-buffered so that a frame's fan can be solved on a side
+    // stream while the previous frame's fan-mode draws still read the other
+    // buffer.  fan[fan_cur] is the context's fan (fan_cur < 0: none).  Each
+    // buffer's last writer (geo_solve_ray_fan) and readers (fan-mode renders,
+    // a chained event: every render waits, after its launch, for the previous
+    // reader) are events, so a solve into a buffer waits for the draws that
+    // read it and a draw waits for the solve that wrote its buffer, whatever
+    // streams they run on.
+    float* fan[2];
+    uint32_t fan_cap, n_fan[2];
+    int fan_cur;
+    hipEvent_t fan_written[2], fan_read[2];
+    bool fan_written_rec[2], fan_read_rec[2];
     unsigned long long* step_slots;
 };
 

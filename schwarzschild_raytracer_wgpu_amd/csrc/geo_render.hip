@@ -597,12 +597,32 @@ int geo_ctx_create(int device, geo_ctx** out) {
         return GEO_EHIP;
     }
     c->num_cus = prop.multiProcessorCount;
+    c->fan_cur = -1;
+    for (int b = 0; b < 2; ++b) {
+        if (hipEventCreateWithFlags(&c->fan_written[b], hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&c->fan_read[b], hipEventDisableTiming) != hipSuccess) {
+            for (int j = 0; j <= b; ++j) {
+                if (c->fan_written[j]) (void)hipEventDestroy(c->fan_written[j]);
+                if (c->fan_read[j]) (void)hipEventDestroy(c->fan_read[j]);
+            }
+            delete c;
+            return GEO_EHIP;
+        }
+    }
     if (hipMalloc(&c->step_slots, sizeof(unsigned long long) * kStepSlots * kSlotStride) != hipSuccess) {
+        for (int b = 0; b < 2; ++b) {
+            (void)hipEventDestroy(c->fan_written[b]);
+            (void)hipEventDestroy(c->fan_read[b]);
+        }
         delete c;
         return GEO_ENOMEM;
     }
     if (hipMemset(c->step_slots, 0, sizeof(unsigned long long) * kStepSlots * kSlotStride) != hipSuccess) {
         (void)hipFree(c->step_slots);
+        for (int b = 0; b < 2; ++b) {
+            (void)hipEventDestroy(c->fan_written[b]);
+            (void)hipEventDestroy(c->fan_read[b]);
+        }
         delete c;
         return GEO_EHIP;
     }
@@ -613,8 +633,14 @@ int geo_ctx_create(int device, geo_ctx** out) {
 void geo_ctx_destroy(geo_ctx* c) {
     if (!c) return;
     DeviceGuard g(c->device);
+    // work in flight may still read the buffers or record the events
+    (void)hipDeviceSynchronize();
     if (c->sky) (void)hipFree(c->sky);
-    if (c->fan) (void)hipFree(c->fan);
+    for (int b = 0; b < 2; ++b) {
+        if (c->fan[b]) (void)hipFree(c->fan[b]);
+        (void)hipEventDestroy(c->fan_written[b]);
+        (void)hipEventDestroy(c->fan_read[b]);
+    }
     if (c->step_slots) (void)hipFree(c->step_slots);
     delete c;
 }
@@ -662,33 +688,49 @@ int geo_set_sky(geo_ctx* c, const uint8_t* rgba8, uint32_t w, uint32_t h) {
     return GEO_OK;
 }
 
+// Both fan buffers hold at least n nodes.  Growing them waits for the device
+// (renders in flight may read the old buffers); 400-node fans never regrow.
 static int ensure_fan(geo_ctx* c, uint32_t n) {
-    if (c->fan && c->fan_cap >= n) return GEO_OK;
-    if (c->fan) (void)hipFree(c->fan);
-    c->fan = nullptr;
+    if (c->fan[0] && c->fan_cap >= n) return GEO_OK;
+    if (hipDeviceSynchronize() != hipSuccess) return GEO_EHIP;
+    for (int b = 0; b < 2; ++b) {
+        if (c->fan[b]) (void)hipFree(c->fan[b]);
+        c->fan[b] = nullptr;
+        c->n_fan[b] = 0;
+    }
     c->fan_cap = 0;
-    if (hipMalloc(&c->fan, sizeof(float) * n) != hipSuccess) return GEO_ENOMEM;
+    c->fan_cur = -1;
+    if (hipMalloc(&c->fan[0], sizeof(float) * n) != hipSuccess) return GEO_ENOMEM;
+    if (hipMalloc(&c->fan[1], sizeof(float) * n) != hipSuccess) {
+        (void)hipFree(c->fan[0]);
+        c->fan[0] = nullptr;
+        return GEO_ENOMEM;
+    }
     c->fan_cap = n;
     return GEO_OK;
+}
+
+// The buffer a new fan goes to (the one the current fan is not in), ordered
+// on stream s after its previous writer and readers.
+static int fan_next(geo_ctx* c, hipStream_t s) {
+    const int b = c->fan_cur < 0 ? 0 : 1 - c->fan_cur;
+    if (c->fan_written_rec[b] && hipStreamWaitEvent(s, c->fan_written[b], 0) != hipSuccess) return -1;
+    if (c->fan_read_rec[b] && hipStreamWaitEvent(s, c->fan_read[b], 0) != hipSuccess) return -1;
+    return b;
 }
 
 int geo_set_fan(geo_ctx* c, const float* fan, uint32_t n) {
     if (!c || !fan || n < 2 || n > kMaxFan) return GEO_EINVAL;
     DeviceGuard g(c->device);
     if (!g.ok) return GEO_EHIP;
-    // as geo_set_sky: fan-mode renders in flight on any stream read the fan
-    // (geo_solve_ray_fan is the stream-ordered way to replace it per frame)
-    if (hipDeviceSynchronize() != hipSuccess) return GEO_EHIP;
     int st = ensure_fan(c, n);
-    if (st) {
-        c->n_fan = 0;
-        return st;
-    }
-    if (hipMemcpy(c->fan, fan, sizeof(float) * n, hipMemcpyHostToDevice) != hipSuccess) {
-        c->n_fan = 0;
-        return GEO_EHIP;
-    }
-    c->n_fan = n;
+    if (st) return st;
+    // a synchronous upload: into the free buffer once nothing reads it
+    const int b = c->fan_cur < 0 ? 0 : 1 - c->fan_cur;
+    if (hipDeviceSynchronize() != hipSuccess) return GEO_EHIP;
+    if (hipMemcpy(c->fan[b], fan, sizeof(float) * n, hipMemcpyHostToDevice) != hipSuccess) return GEO_EHIP;
+    c->n_fan[b] = n;
+    c->fan_cur = b;
     return GEO_OK;
 }
 
@@ -700,12 +742,17 @@ int geo_solve_ray_fan(geo_ctx* c, double sphere_r, double schwarz_r, uint32_t ma
     int st = ensure_fan(c, nr_nodes);
     if (st) return st;
     hipStream_t s = (hipStream_t)stream;
+    const int b = fan_next(c, s);
+    if (b < 0) return GEO_EHIP;
     hipLaunchKernelGGL(geo_fan_kernel, dim3((nr_nodes + 63) / 64), dim3(64), 0, s, sphere_r,
-                       schwarz_r, max_iter, step, nr_nodes, r, c->fan);
+                       schwarz_r, max_iter, step, nr_nodes, r, c->fan[b]);
     if (hipGetLastError() != hipSuccess) return GEO_EHIP;
-    c->n_fan = nr_nodes;
+    if (hipEventRecord(c->fan_written[b], s) != hipSuccess) return GEO_EHIP;
+    c->fan_written_rec[b] = true;
+    c->n_fan[b] = nr_nodes;
+    c->fan_cur = b;
     if (fan_out) {
-        if (hipMemcpyAsync(fan_out, c->fan, sizeof(float) * nr_nodes, hipMemcpyDeviceToHost, s) !=
+        if (hipMemcpyAsync(fan_out, c->fan[b], sizeof(float) * nr_nodes, hipMemcpyDeviceToHost, s) !=
             hipSuccess)
             return GEO_EHIP;
         if (hipStreamSynchronize(s) != hipSuccess) return GEO_EHIP;
@@ -735,7 +782,7 @@ static int render_impl(geo_ctx* c, const geo_frame* frame, const geo_scene* scen
     if (scene->max_steps > (1u << 24)) return GEO_EINVAL;  // a wave's step sum must fit u32
     if (defer && steps_total) return GEO_EINVAL;
     if (!c->sky) return GEO_ESTATE;
-    if (scene->mode == GEO_MODE_FAN && (!c->fan || c->n_fan < 2)) return GEO_ESTATE;
+    if (scene->mode == GEO_MODE_FAN && (c->fan_cur < 0 || c->n_fan[c->fan_cur] < 2)) return GEO_ESTATE;
     // bound > 0 (escape test folding, geo_pixel.h) needs r_obs > 0 and sphere_r > 0
     if (scene->mode != GEO_MODE_FAN &&
         (!(scene->step > 0.0f) || !(scene->r_obs > 0.0f) || !(scene->sphere_r > 0.0f) || !(scene->rs >= 0.0f)))
@@ -765,8 +812,9 @@ static int render_impl(geo_ctx* c, const geo_frame* frame, const geo_scene* scen
     a.sky_h256 = (float)c->sky_h * 256.0f;
     a.sky_pitch_b = (c->sky_w + 2u) * 4u;
     a.sky_bytes = a.sky_pitch_b * (c->sky_h + 2u);
-    a.fan = c->fan;
-    a.n_fan = c->n_fan;
+    const int fb = c->fan_cur;
+    a.fan = fb < 0 ? nullptr : c->fan[fb];
+    a.n_fan = fb < 0 ? 0u : c->n_fan[fb];
     a.out_rgba = reinterpret_cast<uint32_t*>(out_rgba8);
     a.out_mask = out_mask;
     a.out_uv = reinterpret_cast<float2*>(out_uv);
@@ -775,7 +823,15 @@ static int render_impl(geo_ctx* c, const geo_frame* frame, const geo_scene* scen
     hipStream_t s = (hipStream_t)stream;
     const dim3 grid(tiles_x, tiles_y);
     if (scene->mode == GEO_MODE_FAN) {
+        // after the solve that wrote the buffer; then this render joins the
+        // buffer's chain of readers (the wait is queued after the launch, so
+        // it holds back only later work on s, never this render)
+        if (c->fan_written_rec[fb] && hipStreamWaitEvent(s, c->fan_written[fb], 0) != hipSuccess) return GEO_EHIP;
         hipLaunchKernelGGL((geo_render_kernel<GEO_MODE_FAN, geo::kCurvedOut>), grid, dim3(kBlock), 0, s, a);
+        if (hipGetLastError() != hipSuccess) return GEO_EHIP;
+        if (c->fan_read_rec[fb] && hipStreamWaitEvent(s, c->fan_read[fb], 0) != hipSuccess) return GEO_EHIP;
+        if (hipEventRecord(c->fan_read[fb], s) != hipSuccess) return GEO_EHIP;
+        c->fan_read_rec[fb] = true;
     } else if (adaptive) {
         switch (geo::geodesic_kind(a.k)) {
             case geo::kCurvedOut:

@@ -205,6 +205,48 @@ def test_fan_kernel_budget_edges(geo, torch_mod, max_iter):
         assert np.mean(gpu == ref) > 0.99, args
 
 
+def test_fan_solved_on_side_stream_matches_one_stream(geo, torch_mod):
+    """The context double-buffers its fan and orders it with events: a loop
+    whose per-frame fans are solved on a side stream (with no waits of its
+    own; each solve overlaps the previous frame's draw) draws the same frames
+    as the loop on one stream, and a frame equals the oracle's render with
+    that frame's fan."""
+    from schwarzschild_raytracer_wgpu_amd.scenes import make_sky
+
+    w, h = 320, 180
+    dev = torch_mod.device("cuda:0")
+    sky = make_sky("equirect", (512, 256))
+
+    def loop(side):
+        obs = geo.Observer(1.0, math.pi / 2, w, h)
+        obs.set_position(2.5, 0.0, 0.1)
+        sphere = geo.BasicSphereBuffer(0, 50.0, 1.0, sky, mode=geo.GEO_MODE_FAN)
+        tgt = geo.RenderTarget(w, h, torch_mod.empty(w * h * 4, dtype=torch_mod.uint8, device=dev))
+        frames, radii = [], []
+        for i in range(12):
+            obs.set_position(2.5 + 0.25 * i, 0.0, 0.1)  # a new radius per frame: every fan differs
+            r = obs.get_radial_position()
+            sphere.update_ray_fan(r, stream=side)
+            sphere.draw(obs.calc_transformation_pipeline(), tgt)
+            frames.append(tgt.rgba.clone())
+            radii.append(r)
+        torch_mod.cuda.synchronize()
+        return [f.cpu().numpy() for f in frames], radii, obs
+
+    one, radii, _ = loop(None)
+    two, radii2, obs = loop(torch_mod.cuda.Stream(dev))
+    assert radii == radii2
+    for a, b in zip(one, two):
+        assert np.array_equal(a, b)
+    assert len({a.tobytes() for a in one}) == len(one)  # the frames differ: each one needs its own fan
+    # the last frame against the oracle with that frame's fan
+    fan = O.solve_ray_fan(50.0, 1.0, 1000, math.pi / 100, 400, radii[-1])
+    scene = geo.make_scene(1.0, 50.0, radii[-1], math.pi / 100, 1000, geo.GEO_MODE_FAN)
+    ref = O.render_f32(obs.calc_transformation_pipeline(), scene, sky, w, h, fan=fan, threads=8)
+    got = two[-1].reshape(h, w, 4)
+    assert np.mean(np.all(got == ref["rgba"], axis=-1)) > 0.999  # GPU fan within 1 f32 ulp of the oracle's
+
+
 def test_sphere_buffer_fan_mode_matches_oracle(geo, torch_mod):
     """Reference-exact mode: BasicSphereBuffer.update_ray_fan + draw = fan lerp
     (shader.wgsl:77-84) with the GPU-solved fan."""

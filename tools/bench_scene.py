@@ -16,7 +16,9 @@ VALU-bound sky draw; the point draw waits for it (geo_points_draw).
 --mode fan draws every sphere the way the reference displays it: each frame
 solves the sphere's 400-node f64 ray fan (geo_solve_ray_fan, SphereRayTracer::
 solve_ray_fan, lib.rs:292-295) and the sky lerps into it per pixel
-(shader.wgsl:77-84); --mode direct (default) integrates every pixel.
+(shader.wgsl:77-84); with --overlap 1 the fans go on side streams and
+overlap the previous frame's draws.  --mode direct (default) integrates every
+pixel.
 
   python tools/bench_scene.py [--width 3840 --height 2160] [--frames 200] [--points 5000] [--spheres 1|3] [--overlap 1|0] [--mode direct|fan]
 
@@ -79,24 +81,16 @@ def main():
     side = torch.cuda.Stream() if args.overlap else None
 
     # fan mode with --overlap 1: the spheres' fans (latency-bound, one lane per
-    # node) solved concurrently, one stream each, after the previous frame's
-    # draws that read them; the draws wait for all three
+    # node, 7 waves) solved on one side stream each; the context double-buffers
+    # its fan and orders solves and draws with events, so frame i's fans
+    # overlap frame i-1's draws and the draws still read their own frame's fan
     fan_streams = [torch.cuda.Stream() for _ in spheres] if (args.mode == "fan" and args.overlap) else None
 
     def frame(evs=None):
         obs.update_position((0.0, 0.0, 0.0), 1 / 60)
         r = obs.get_radial_position()
-        if fan_streams is not None and not evs:
-            main = torch.cuda.current_stream()
-            for s, fs in zip(spheres, fan_streams):
-                fs.wait_stream(main)
-                with torch.cuda.stream(fs):
-                    s.update_ray_fan(r)
-            for fs in fan_streams:
-                main.wait_stream(fs)
-        else:
-            for s in spheres:
-                s.update_ray_fan(r)  # fan mode: the fan on the device; direct: records r
+        for i, s in enumerate(spheres):  # fan mode: the fan on the device; direct: records r
+            s.update_ray_fan(r, stream=fan_streams[i] if (fan_streams and not evs) else None)
         f = obs.calc_transformation_pipeline()
         if evs:  # per-part timing: the parts back to back on one stream (fan mode: the fans lie before
             evs[0].record()  # evs[0], in no part's time)

@@ -31,7 +31,9 @@ for OV in 1 0; do
 done
 for WH in "3840 2160" "1920 1080"; do
     set -- $WH
-    timeout -k 10 120 $OUT/frame_loop $1 $2 2000 $OUT/flfan_$2.ppm 1 fan >> $OUT/frame_loop_$TAG.txt || exit $?
+    timeout -k 10 120 $OUT/frame_loop $1 $2 2000 $OUT/flfan1_$2.ppm 1 fan >> $OUT/frame_loop_$TAG.txt || exit $?
+    timeout -k 10 120 $OUT/frame_loop $1 $2 2000 $OUT/flfan0_$2.ppm 0 fan >> $OUT/frame_loop_$TAG.txt || exit $?
+    cmp $OUT/flfan1_$2.ppm $OUT/flfan0_$2.ppm || { echo "fan-mode frames differ"; exit 1; }
 done
 cat $OUT/frame_loop_$TAG.txt
 cmp $OUT/fl4k_0.ppm $OUT/fl4k_1.ppm && cmp $OUT/fl1080_0.ppm $OUT/fl1080_1.ppm && echo "frames equal"

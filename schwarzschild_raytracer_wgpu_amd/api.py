@@ -217,14 +217,30 @@ def _check_outputs(nrows: int, width: int, rgba, mask, uv, steps, steps_total) -
                                     ("out_uv", uv, 8 * n, (torch.float32,)),
                                     ("out_steps", steps, 4 * n, (torch.int32, torch.uint32)),
                                     ("steps_total", steps_total, 8, (torch.int64, torch.uint64))):
-        if t is None:
-            continue
-        if not t.is_cuda or not t.is_contiguous():
-            raise ValueError(f"{name} must be a contiguous device tensor")
-        if dtypes is not None and t.dtype not in dtypes:
-            raise ValueError(f"{name} must be one of {dtypes}, got {t.dtype}")
-        if t.numel() * t.element_size() < nbytes:
-            raise ValueError(f"{name} holds {t.numel() * t.element_size()} bytes, the rows need {nbytes}")
+        _check_buffer(name, t, nbytes, dtypes)
+
+
+def _check_buffer(name: str, t, nbytes: int, dtypes=None) -> None:
+    """t (optional) is a contiguous device tensor of >= nbytes bytes and, if
+    dtypes is given, one of those dtypes."""
+    if t is None:
+        return
+    if not t.is_cuda or not t.is_contiguous():
+        raise ValueError(f"{name} must be a contiguous device tensor")
+    if dtypes is not None and t.dtype not in dtypes:
+        raise ValueError(f"{name} must be one of {dtypes}, got {t.dtype}")
+    if t.numel() * t.element_size() < nbytes:
+        raise ValueError(f"{name} holds {t.numel() * t.element_size()} bytes, the rows need {nbytes}")
+
+
+def _check_point_outputs(target: "RenderTarget", row0: int, nrows: int, out_xy, n_xy: int) -> None:
+    """The point draws write RGBA8 pixels of rows [row0, row0 + nrows) of the
+    target (laid out from row0, as geo_render_rows' output) and 2 int32 per
+    vertex into out_xy."""
+    import torch
+
+    _check_buffer("target.rgba", target.rgba, 4 * nrows * target.width)
+    _check_buffer("out_xy", out_xy, 8 * n_xy, (torch.int32,))
 
 
 def make_scene(rs: float, sphere_r: float, r_obs: float, step: float = math.pi / 100.0, max_steps: int = 1000,
@@ -481,6 +497,7 @@ class PointCloud:
         that ran, and the next update() waits for it, so update() may run on
         a side stream, overlapping the sphere draws.  out_xy (device, int32):
         2 per connector, near side first."""
+        _check_point_outputs(target, 0, target.height, out_xy, self.n * (2 if self.has_farside else 1))
         check("geo_points_draw", lib.geo_points_draw(self._h, ctypes.byref(frame), target.width, target.height, 0,
                                                      target.height, _ptr(target.rgba), _ptr(out_xy),
                                                      _stream_handle(stream)))
@@ -491,6 +508,9 @@ def draw_points(ctx: Context, frame: GeoFrame, vertices, n: int, target: "Render
     """geo_draw_points: vs_main + PointList raster (shader.wgsl:36-74) of n
     vertices (device pointer or tensor, 4 floats each) over target rows."""
     nrows = target.height - row0 if nrows is None else nrows
+    _check_point_outputs(target, row0, nrows, out_xy, n)
+    if not isinstance(vertices, int):
+        _check_buffer("vertices", vertices, 16 * n)
     vp = vertices if isinstance(vertices, int) else _ptr(vertices)
     check("geo_draw_points", lib.geo_draw_points(ctx._h, ctypes.byref(frame), vp, n, target.width, target.height,
                                                  row0, nrows, _ptr(target.rgba), _ptr(out_xy),

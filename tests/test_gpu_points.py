@@ -172,3 +172,31 @@ def test_point_cloud_draw_equals_two_mesh_draws(geo, ctx, torch_mod):
     assert np.array_equal(host(a.rgba, torch_mod), host(b.rgba, torch_mod))
     assert np.array_equal(host(xy, torch_mod), np.concatenate([host(xn, torch_mod), host(xf, torch_mod)]))
     assert (host(xy, torch_mod)[:, 0] >= 0).sum() > 500
+
+
+def test_point_draws_reject_short_buffers(geo, ctx, torch_mod):
+    """The point draws write 4 B per target pixel and 2 int32 per vertex: a
+    target, out_xy or vertex buffer too small (or out_xy of another dtype) is
+    refused before any launch."""
+    w, h = 64, 32
+    frame = default_frame(w, h, pos=(25.0, 0.0, 1.0))
+    dev = torch_mod.device("cuda:0")
+    pc = geo.PointCloud(ctx, accretion_disk(100, seed=1), 1.0, (25.0, 0.0, 1.0), True, False)
+    ok = geo.RenderTarget(w, h, torch_mod.zeros(w * h * 4, dtype=torch_mod.uint8, device=dev))
+    short = geo.RenderTarget(w, h, torch_mod.zeros(w * h * 4 - 1, dtype=torch_mod.uint8, device=dev))
+    with pytest.raises(ValueError):
+        pc.draw(frame, short)
+    with pytest.raises(ValueError):  # near + far: 200 vertices
+        pc.draw(frame, ok, out_xy=torch_mod.empty((199, 2), dtype=torch_mod.int32, device=dev))
+    with pytest.raises(ValueError):
+        pc.draw(frame, ok, out_xy=torch_mod.empty((200, 2), dtype=torch_mod.float32, device=dev))
+    verts = torch_mod.zeros((99, 4), dtype=torch_mod.float32, device=dev)
+    with pytest.raises(ValueError):
+        geo.draw_points(ctx, frame, verts, 100, ok)
+    with pytest.raises(ValueError):  # rows [8, 32): 24 rows
+        geo.draw_points(ctx, frame, pc.vertices_ptr(False), 100, geo.RenderTarget(
+            w, h, torch_mod.zeros(23 * w * 4, dtype=torch_mod.uint8, device=dev)), row0=8)
+    pc.draw(frame, ok, out_xy=torch_mod.empty((200, 2), dtype=torch_mod.int32, device=dev))
+    geo.draw_points(ctx, frame, pc.vertices_ptr(False), 100, geo.RenderTarget(
+        w, h, torch_mod.zeros(24 * w * 4, dtype=torch_mod.uint8, device=dev)), row0=8)
+    torch_mod.cuda.synchronize()

@@ -159,7 +159,10 @@ int geo_solve_ray_fan(geo_ctx* ctx, double sphere_r, double schwarz_r, uint32_t 
  *   out_mask     nrows*width bytes, 1 = black hole / discard (optional)
  *   out_uv       nrows*width*2 floats, sky-sphere (U,V) (optional)
  *   out_steps    nrows*width u32, executed RK4 main-loop steps (optional)
- *   steps_total  one u64 that the executed steps of this call are ADDED to (optional)
+ *   steps_total  one u64 that the executed steps of this call are ADDED to (optional;
+ *                exactly this call's steps, also while other renders of the context
+ *                run on other streams: the call counts into a counter set of its own,
+ *                reused only after that set's previous fold)
  * Asynchronous on `stream`. */
 int geo_render_rows(geo_ctx* ctx, const geo_frame* frame, const geo_scene* scene,
                     uint32_t width, uint32_t height, uint32_t row0, uint32_t nrows,

@@ -25,7 +25,17 @@ struct geo_ctx {
     int fan_cur;
     hipEvent_t fan_written[2], fan_read[2];
     bool fan_written_rec[2], fan_read_rec[2];
+    // Sharded step counters: set 0 is the GEO_FLAG_DEFER_STEPS accumulator
+    // (geo_steps_flush folds it); a render with a steps_total of its own
+    // counts into one of kStepCallSets per-call sets, taken round-robin, and
+    // folds it into its total on its stream.  A set is taken again only after
+    // its previous fold (step_set_free), so renders on different streams never
+    // fold each other's counts.
     unsigned long long* step_slots;
+    static constexpr int kStepCallSets = 4;
+    hipEvent_t step_set_free[kStepCallSets];
+    bool step_set_rec[kStepCallSets];
+    int step_set_next;
 };
 
 // Makes `dev` current for the scope of a C-ABI call, restoring the caller's device.

@@ -52,6 +52,8 @@ constexpr int kWaveRows = 64 / kTileW;   // rows covered by one wave
 constexpr uint32_t kMaxFan = 4096;       // LDS fan capacity (16 KiB)
 constexpr int kStepSlots = 256;          // sharded step counters (one per 128-B line)
 constexpr int kSlotStride = 16;          // u64 per slot = 128 B (own cache line)
+constexpr size_t kSlotSetU64 = (size_t)kStepSlots * kSlotStride;  // one set of sharded counters
+constexpr int kSlotSets = 1 + geo_ctx::kStepCallSets;            // the DEFER accumulator + per-call sets
 
 struct RenderArgs {
     geo_frame frame;
@@ -598,33 +600,30 @@ int geo_ctx_create(int device, geo_ctx** out) {
     }
     c->num_cus = prop.multiProcessorCount;
     c->fan_cur = -1;
-    for (int b = 0; b < 2; ++b) {
-        if (hipEventCreateWithFlags(&c->fan_written[b], hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&c->fan_read[b], hipEventDisableTiming) != hipSuccess) {
-            for (int j = 0; j <= b; ++j) {
-                if (c->fan_written[j]) (void)hipEventDestroy(c->fan_written[j]);
-                if (c->fan_read[j]) (void)hipEventDestroy(c->fan_read[j]);
-            }
-            delete c;
-            return GEO_EHIP;
-        }
+    bool ok = true;
+    for (int b = 0; b < 2 && ok; ++b)
+        ok = hipEventCreateWithFlags(&c->fan_written[b], hipEventDisableTiming) == hipSuccess &&
+             hipEventCreateWithFlags(&c->fan_read[b], hipEventDisableTiming) == hipSuccess;
+    for (int i = 0; i < geo_ctx::kStepCallSets && ok; ++i)
+        ok = hipEventCreateWithFlags(&c->step_set_free[i], hipEventDisableTiming) == hipSuccess;
+    int st = ok ? GEO_OK : GEO_EHIP;
+    if (ok && hipMalloc(&c->step_slots, sizeof(unsigned long long) * kSlotSetU64 * kSlotSets) != hipSuccess) {
+        c->step_slots = nullptr;
+        st = GEO_ENOMEM;
     }
-    if (hipMalloc(&c->step_slots, sizeof(unsigned long long) * kStepSlots * kSlotStride) != hipSuccess) {
+    if (st == GEO_OK &&
+        hipMemset(c->step_slots, 0, sizeof(unsigned long long) * kSlotSetU64 * kSlotSets) != hipSuccess)
+        st = GEO_EHIP;
+    if (st != GEO_OK) {
+        if (c->step_slots) (void)hipFree(c->step_slots);
         for (int b = 0; b < 2; ++b) {
-            (void)hipEventDestroy(c->fan_written[b]);
-            (void)hipEventDestroy(c->fan_read[b]);
+            if (c->fan_written[b]) (void)hipEventDestroy(c->fan_written[b]);
+            if (c->fan_read[b]) (void)hipEventDestroy(c->fan_read[b]);
         }
+        for (int i = 0; i < geo_ctx::kStepCallSets; ++i)
+            if (c->step_set_free[i]) (void)hipEventDestroy(c->step_set_free[i]);
         delete c;
-        return GEO_ENOMEM;
-    }
-    if (hipMemset(c->step_slots, 0, sizeof(unsigned long long) * kStepSlots * kSlotStride) != hipSuccess) {
-        (void)hipFree(c->step_slots);
-        for (int b = 0; b < 2; ++b) {
-            (void)hipEventDestroy(c->fan_written[b]);
-            (void)hipEventDestroy(c->fan_read[b]);
-        }
-        delete c;
-        return GEO_EHIP;
+        return st;
     }
     *out = c;
     return GEO_OK;
@@ -641,6 +640,7 @@ void geo_ctx_destroy(geo_ctx* c) {
         (void)hipEventDestroy(c->fan_written[b]);
         (void)hipEventDestroy(c->fan_read[b]);
     }
+    for (int i = 0; i < geo_ctx::kStepCallSets; ++i) (void)hipEventDestroy(c->step_set_free[i]);
     if (c->step_slots) (void)hipFree(c->step_slots);
     delete c;
 }
@@ -819,8 +819,18 @@ static int render_impl(geo_ctx* c, const geo_frame* frame, const geo_scene* scen
     a.out_mask = out_mask;
     a.out_uv = reinterpret_cast<float2*>(out_uv);
     a.out_steps = out_steps;
-    a.step_slots = (steps_total || defer) ? c->step_slots : nullptr;
     hipStream_t s = (hipStream_t)stream;
+    // counters: the context's accumulator (DEFER), or a per-call set free of
+    // any earlier call's fold (steps_total; not in fan mode, which has none)
+    int call_set = -1;
+    a.step_slots = defer ? c->step_slots : nullptr;
+    if (steps_total && scene->mode != GEO_MODE_FAN) {
+        call_set = c->step_set_next;
+        c->step_set_next = (call_set + 1) % geo_ctx::kStepCallSets;
+        if (c->step_set_rec[call_set] && hipStreamWaitEvent(s, c->step_set_free[call_set], 0) != hipSuccess)
+            return GEO_EHIP;
+        a.step_slots = c->step_slots + (size_t)(1 + call_set) * kSlotSetU64;
+    }
     const dim3 grid(tiles_x, tiles_y);
     if (scene->mode == GEO_MODE_FAN) {
         // after the solve that wrote the buffer; then this render joins the
@@ -856,10 +866,11 @@ static int render_impl(geo_ctx* c, const geo_frame* frame, const geo_scene* scen
         }
     }
     if (hipGetLastError() != hipSuccess) return GEO_EHIP;
-    if (steps_total && scene->mode != GEO_MODE_FAN) {
-        hipLaunchKernelGGL(geo_steps_finalize, dim3(1), dim3(kStepSlots), 0, s, c->step_slots,
-                           steps_total);
+    if (call_set >= 0) {
+        hipLaunchKernelGGL(geo_steps_finalize, dim3(1), dim3(kStepSlots), 0, s, a.step_slots, steps_total);
         if (hipGetLastError() != hipSuccess) return GEO_EHIP;
+        if (hipEventRecord(c->step_set_free[call_set], s) != hipSuccess) return GEO_EHIP;
+        c->step_set_rec[call_set] = true;
     }
     return GEO_OK;
 }

@@ -173,6 +173,39 @@ def test_render_bands_interleaved(geo, torch_mod):
                                                                          device=dev))
 
 
+def test_step_totals_per_call_across_streams(geo, torch_mod):
+    """Each render's steps_total gets exactly its own rows' steps, also when
+    renders with their own totals overlap on different streams (more calls in
+    flight than the context has per-call counter sets), and a DEFER
+    accumulation on a third stream is not disturbed by them."""
+    from schwarzschild_raytracer_wgpu_amd import _lib
+    from schwarzschild_raytracer_wgpu_amd.scenes import make_sky
+
+    torch = torch_mod
+    w, h = 256, 192
+    frame, scene = default_frame(w, h), default_scene(2048)
+    ctx = make_ctx(geo, make_sky("equirect", (256, 128)))
+    full = render(geo, torch, ctx, frame, scene, w, h)
+    dev = torch.device("cuda:0")
+    want = [int(full["steps"][r0:r0 + 16].astype(np.int64).sum()) for r0 in range(0, h, 16)]
+    streams = [torch.cuda.Stream(dev) for _ in range(3)]
+    defer = geo.make_scene(scene.rs, scene.sphere_r, scene.r_obs, scene.step, scene.max_steps,
+                           flags=_lib.GEO_FLAG_DEFER_STEPS)
+    for _ in range(3):
+        totals = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in want]
+        outs = [torch.empty(16 * w * 4, dtype=torch.uint8, device=dev) for _ in want]
+        dout = torch.empty(h * w * 4, dtype=torch.uint8, device=dev)
+        acc = torch.zeros(1, dtype=torch.int64, device=dev)
+        torch.cuda.synchronize()  # the zero fills ran on the current stream
+        ctx.render_rows(frame, defer, w, h, 0, h, dout, stream=streams[2])
+        for i, r0 in enumerate(range(0, h, 16)):
+            ctx.render_rows(frame, scene, w, h, r0, 16, outs[i], steps_total=totals[i], stream=streams[i % 2])
+        ctx.steps_flush(acc, stream=streams[2])
+        torch.cuda.synchronize()
+        assert [int(t.item()) for t in totals] == want
+        assert int(acc.item()) == full["total"]
+
+
 def test_fan_kernel_matches_oracle(geo, torch_mod):
     ctx = geo.Context(0)
     for args in [(500.0, 10.0, 1000, math.pi / 100, 400, math.sqrt(626.0)),

@@ -249,14 +249,17 @@ int geo_rays_create(geo_ctx* ctx, float schwarz_r, uint32_t n_points, uint32_t s
 void geo_rays_destroy(geo_rays* rays);
 /* number of connectors */
 int geo_rays_count(const geo_rays* rays);
-/* RayConnector::set_position (:134-136) for every point (host, 3 floats per point). */
+/* RayConnector::set_position (:134-136) for every point (host, 3 floats per
+ * point).  Synchronous: waits for the batch's last update first. */
 int geo_rays_set_positions(geo_rays* rays, const float* pos_xyz);
 /* update_ray(other, iterations) (ray_connector.rs:48-132) for every connector,
  * or reset_ray(other) (:27-44) when reset != 0.  other_xyz (host): 3 floats
  * (one other end for all) or 3 per point when per_point != 0 (then the call
  * synchronises `stream` after uploading them).  out_vertices: device, 4 floats
  * per connector [x, y, z, incoming angle], or NULL for the batch's own buffer
- * (geo_rays_vertices).  Asynchronous on `stream`. */
+ * (geo_rays_vertices).  Asynchronous on `stream`; it waits for the batch's
+ * previous update, whichever stream that ran on.  Readers of the vertices
+ * (geo_draw_points) are the caller's to order: an update overwrites them. */
 int geo_rays_update(geo_rays* rays, const float* other_xyz, int per_point, uint32_t iterations, int reset,
                     float* out_vertices, void* stream);
 const float* geo_rays_vertices(const geo_rays* rays);

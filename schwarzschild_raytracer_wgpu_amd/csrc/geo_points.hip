@@ -355,6 +355,11 @@ struct geo_rays {
     uint64_t* rng = nullptr;
     uint8_t* respawn = nullptr;
     float* respawn_pos = nullptr;
+    // geo_rays handles: the last geo_rays_update (whatever its stream).  The
+    // next update waits for it (it reads and writes the same state), and
+    // geo_rays_set_positions waits for it before overwriting the positions.
+    hipEvent_t updated = nullptr;
+    bool updated_rec = false;
 };
 
 struct geo_points {
@@ -463,7 +468,11 @@ int geo_rays_create(geo_ctx* ctx, float schwarz_r, uint32_t n_points, uint32_t s
     if (!g.ok) return GEO_EHIP;
     geo_rays* r = new (std::nothrow) geo_rays();
     if (!r) return GEO_ENOMEM;
-    const int st = rays_init(r, ctx, schwarz_r, n_points, sides, pos_xyz);
+    int st = rays_init(r, ctx, schwarz_r, n_points, sides, pos_xyz);
+    if (!st && hipEventCreateWithFlags(&r->updated, hipEventDisableTiming) != hipSuccess) {
+        r->updated = nullptr;
+        st = GEO_EHIP;
+    }
     if (st) {
         rays_free(r);
         delete r;
@@ -476,6 +485,10 @@ int geo_rays_create(geo_ctx* ctx, float schwarz_r, uint32_t n_points, uint32_t s
 void geo_rays_destroy(geo_rays* r) {
     if (!r) return;
     DeviceGuard g(r->device);
+    if (r->updated) {
+        (void)hipEventSynchronize(r->updated);  // an update in flight still uses the buffers
+        (void)hipEventDestroy(r->updated);
+    }
     rays_free(r);
     delete r;
 }
@@ -486,6 +499,9 @@ int geo_rays_set_positions(geo_rays* r, const float* pos_xyz) {
     if (!r || !pos_xyz) return GEO_EINVAL;
     DeviceGuard g(r->device);
     if (!g.ok) return GEO_EHIP;
+    // the blocking copy below is not ordered against an update still running
+    // on a caller's non-blocking stream, which reads the positions
+    if (r->updated_rec && hipEventSynchronize(r->updated) != hipSuccess) return GEO_EHIP;
     std::vector<float> soa(3 * (size_t)r->n_points);
     for (uint32_t i = 0; i < r->n_points; ++i)
         for (int k = 0; k < 3; ++k) soa[(size_t)k * r->n_points + i] = pos_xyz[3 * (size_t)i + k];
@@ -499,15 +515,23 @@ int geo_rays_update(geo_rays* r, const float* other_xyz, int per_point, uint32_t
     DeviceGuard g(r->device);
     if (!g.ok) return GEO_EHIP;
     hipStream_t s = (hipStream_t)stream;
+    // after the previous update (its state, and the per-point staging buffer)
+    if (r->updated_rec && hipStreamWaitEvent(s, r->updated, 0) != hipSuccess) return GEO_EHIP;
+    int st;
     if (per_point) {
         if (hipMemcpyAsync(r->other, other_xyz, sizeof(float) * 3 * r->n_points, hipMemcpyHostToDevice, s) !=
                 hipSuccess ||
             hipStreamSynchronize(s) != hipSuccess)
             return GEO_EHIP;
-        return rays_launch(r, 0.f, 0.f, 0.f, r->other, iterations, reset, false, out_vertices, s);
+        st = rays_launch(r, 0.f, 0.f, 0.f, r->other, iterations, reset, false, out_vertices, s);
+    } else {
+        st = rays_launch(r, other_xyz[0], other_xyz[1], other_xyz[2], nullptr, iterations, reset, false,
+                         out_vertices, s);
     }
-    return rays_launch(r, other_xyz[0], other_xyz[1], other_xyz[2], nullptr, iterations, reset, false, out_vertices,
-                       s);
+    if (st) return st;
+    if (hipEventRecord(r->updated, s) != hipSuccess) return GEO_EHIP;
+    r->updated_rec = true;
+    return GEO_OK;
 }
 
 const float* geo_rays_vertices(const geo_rays* r) { return r ? reinterpret_cast<const float*>(r->verts) : nullptr; }

@@ -200,3 +200,26 @@ def test_point_draws_reject_short_buffers(geo, ctx, torch_mod):
     geo.draw_points(ctx, frame, pc.vertices_ptr(False), 100, geo.RenderTarget(
         w, h, torch_mod.zeros(24 * w * 4, dtype=torch_mod.uint8, device=dev)), row0=8)
     torch_mod.cuda.synchronize()
+
+
+def test_rays_updates_alternating_streams_bitexact(geo, ctx, torch_mod):
+    """RayConnectors updates issued on alternating non-blocking streams with no
+    host sync between them (each waits for the batch's previous update), with
+    a set_positions in the middle (it waits for the update in flight): the
+    same vertices as the oracle's sequential run."""
+    pos = accretion_disk(20000, seed=5)
+    pos2 = accretion_disk(20000, seed=6)
+    hip = geo.RayConnectors(ctx, 1.0, pos, sides=3)
+    ref = O.Rays(1.0, pos, sides=3, libm=False)
+    streams = [torch_mod.cuda.Stream() for _ in range(2)]
+    for f in range(8):
+        r = 25.0 * (2.0 / 25.0) ** (f / 7)
+        obs = np.array([r * math.cos(0.3 * f), r * math.sin(0.3 * f), 0.2], np.float32)
+        if f == 4:
+            hip.set_positions(pos2)
+            ref.pos = np.ascontiguousarray(pos2, dtype=np.float32).reshape(-1, 3)  # RayConnector::set_position
+        hip.update_ray(obs, 2, stream=streams[f % 2])
+        e = ref.update(obs, 2)
+    o = host(hip.vertices, torch_mod)
+    bad = np.argwhere(o.view(np.uint32) != e.view(np.uint32))
+    assert bad.size == 0, bad[:5]

@@ -153,6 +153,7 @@ def main():
     # metric; the fastest by max-over-ranks wall time is used for the timed
     # region.  Every rank holds the same all-reduced times, so all pick alike.
     lead_trials = None
+    link_probe = present_link_probe(sf, dist, args) if world > 1 else None
     if len(leads) > 1:
         spin_up(sf, args.spinup_frames * world)  # the trials compare layouts at the settled clock
         times = []
@@ -376,6 +377,7 @@ def main():
                                  "one stream after the timed region (%d render streams overlap consecutive frames "
                                  "inside it)" % sf.S)},
         "pipelined": pipelined,
+        "link_probe": link_probe,
         "compute_only": {"value": total_steps / compute_max, "ms_per_step": compute_max / args.steps * 1e3,
                          "what": "the same K frames rendered on the same streams without pack, gather or "
                                  "reassembly (max over ranks)"},
@@ -411,6 +413,34 @@ def spin_up(sf, n):
             sf.drain()
             torch.cuda.synchronize()
     sf.drain()
+
+
+def present_link_probe(sf, dist, args, reps=10):
+    """N > 1, before the lead trials: the present gather alone, timed.  Every
+    rank sends one batch contribution of the bench's size (K frames of the
+    largest peer share, RGB24 or RGBA8) to rank 0, `reps` times back to back.
+    It measures the per-peer link rate that DESIGN.md §6 models, on the node
+    the bench runs on.  Diagnostic only, outside the timed region."""
+    import torch
+
+    dev = sf.bufs[0].device
+    src = torch.zeros(sf.K * sf.tslice, dtype=torch.uint8, device=dev if args.dist_backend == "nccl" else "cpu")
+    gl = [torch.empty_like(src) for _ in range(sf.world)] if sf.rank == 0 else None
+    for _ in range(3):
+        dist.gather(src, gather_list=gl, dst=0)
+    torch.cuda.synchronize()
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        dist.gather(src, gather_list=gl, dst=0)
+    torch.cuda.synchronize()
+    dist.barrier()
+    dt = (time.perf_counter() - t0) / reps
+    nbytes = src.numel()
+    return {"what": "dist.gather of one batch contribution per rank to rank 0, %d back to back (%s)"
+                    % (reps, args.dist_backend),
+            "bytes_per_peer": nbytes, "ms_per_gather": dt * 1e3,
+            "per_peer_gb_s": nbytes / dt / 1e9, "into_rank0_gb_s": nbytes * (sf.world - 1) / dt / 1e9}
 
 
 def pmc_traffic(config, mode, world):

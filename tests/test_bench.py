@@ -24,7 +24,8 @@ def test_pmc_traffic_only_for_the_profiled_workload():
     assert bench.pmc_traffic("cfg3_4k", "fan", 1) is None
     assert bench.pmc_traffic("cfg3_4k", "direct", 2) is None  # full-frame bytes vs a rank's share
     assert bench.pmc_traffic("cfg5_8k_adaptive", "adaptive", 1) is not None
-    assert bench.pmc_traffic("cfg2_1080p", "direct", 1) is None  # never profiled
+    assert bench.pmc_traffic("cfg2_1080p", "direct", 1) is not None
+    assert bench.pmc_traffic("cfg1_256_cpu", "direct", 1) is None  # never profiled
 
 
 @pytest.mark.gpu

@@ -70,6 +70,10 @@ struct PixelConsts {
     // compare, `inv_b2 < barrier_lim` (-inf when pf_barrier is off), and the
     // squared outside-horizon energy
     float barrier_lim, e_out2;
+    // pf_always | pf_falling << 1 | pf_outgoing << 2 as one aligned word: the
+    // kernel reads it with one scalar load (the bool bytes above sit at
+    // unaligned kernarg offsets, which hipcc fetches with vector loads)
+    uint32_t pf_bits;
     // the integrator's scaled state U = scale*u (scale = 3 rs/2, or 1 for rs = 0)
     float scale, U0, SU, BD, HU;
     float SUp;  // next float above SU: (U > SU) == (U >= SUp) for every float U
@@ -78,6 +82,10 @@ struct PixelConsts {
     float tolG;  // tolU / 64: double the step after one whose estimate is below it
     float hmax;  // GEO_ADAPTIVE_MAX_GROWTH * step
 };
+
+#ifndef GEO_PF_BITS
+#define GEO_PF_BITS 1  // 0: read the pre-filter bools (A/B switch)
+#endif
 
 // Integration kinds (frame-uniform, chosen on the host):
 constexpr int kCurvedOut = 0;  // rs > 0, observer outside the horizon (r > rs)
@@ -177,6 +185,7 @@ GEO_HD PixelConsts make_consts(float rs, float sphere_r, float r, float step, ui
     k.pf_outgoing = r > k.r3_2 && !k.inside_sphere; // & !falling
     k.barrier_lim = k.pf_barrier ? k.barrier_thresh : -__builtin_inff();
     k.e_out2 = k.e_out * k.e_out;
+    k.pf_bits = (k.pf_always ? 1u : 0u) | (k.pf_falling ? 2u : 0u) | (k.pf_outgoing ? 4u : 0u);
     k.scale = k.rs_nonzero ? k.r3_2 : 1.0f;
     k.U0 = k.scale * k.u0;
     k.SU = k.scale * k.sphere_u;
@@ -306,7 +315,13 @@ GEO_HD bool geodesic_init(const PixelConsts& k, float st, float ct, float rct, f
     const float inv_b2 = e2 * ((rct * rct) * k.inv_r2);
     // pre-filters (:106-119), frame-uniform terms precomputed
     const bool eneg = KIND == kCurvedIn && k.pf_eneg && energy < 0.0f;
-    if (k.pf_always || eneg || inv_b2 < k.barrier_lim || lane_select_(falling_m, k.pf_falling, k.pf_outgoing)) {
+#if GEO_PF_BITS
+    const bool pf_always = (k.pf_bits & 1u) != 0, pf_falling = (k.pf_bits & 2u) != 0,
+               pf_outgoing = (k.pf_bits & 4u) != 0;
+#else
+    const bool pf_always = k.pf_always, pf_falling = k.pf_falling, pf_outgoing = k.pf_outgoing;
+#endif
+    if (pf_always || eneg || inv_b2 < k.barrier_lim || lane_select_(falling_m, pf_falling, pf_outgoing)) {
         *early = kNoValue;
         return false;
     }
@@ -534,6 +549,10 @@ GEO_HD uint32_t run_groups_pp(const StopTest<KIND>& stop_at, uint32_t ngroups, u
     return it;
 }
 
+#ifndef GEO_SCAN_BSEARCH
+#define GEO_SCAN_BSEARCH 1  // 0: the linear scan everywhere (A/B switch)
+#endif
+
 // After the group loop (run_groups): from the G + 1 states of the lane's
 // stopping group and `it` = the steps before it (or the whole-group budget),
 // the first stopping step, the budget tail of fewer than G steps, the
@@ -552,7 +571,24 @@ GEO_HD float geodesic_finish(const PixelConsts& k, const StopTest<KIND>& stop_at
     }
     GEO_OPAQUE(it);
     float ou = su_[0], oub = sb_[0], nu = su_[0], nub = sb_[0];
-    if (it + (uint32_t)G <= ms) {
+    if (G == 4 && GEO_SCAN_BSEARCH && stop_at.absorbing && GEO_ABSORBING_TEST && it + (uint32_t)G <= ms) {
+        // stopped inside the group, where the stop set is absorbing: the
+        // flags of states 1..4 are monotone (false.. then true.., state 4's
+        // true), so two tests find the first stopping state k -- state 2,
+        // then state 1 (k <= 2) or state 3 (k > 2) -- where the scan below
+        // makes four; the step is k, from state k - 1 to state k
+        const bool t2 = stop_at(su_[2], sb_[2]);
+        const bool tx = stop_at(t2 ? su_[1] : su_[3], t2 ? sb_[1] : sb_[3]);
+        const float lu = tx ? su_[0] : su_[1], lb = tx ? sb_[0] : sb_[1];  // k = 1 or 2
+        const float mu = tx ? su_[1] : su_[2], mb = tx ? sb_[1] : sb_[2];
+        const float hu = tx ? su_[2] : su_[3], hb = tx ? sb_[2] : sb_[3];  // k = 3 or 4
+        const float gu = tx ? su_[3] : su_[G], gb = tx ? sb_[3] : sb_[G];
+        ou = t2 ? lu : hu;
+        oub = t2 ? lb : hb;
+        nu = t2 ? mu : gu;
+        nub = t2 ? mb : gb;
+        it += (t2 ? 1u : 3u) + (tx ? 0u : 1u);
+    } else if (it + (uint32_t)G <= ms) {
         // stopped inside the group: the first step j whose flag holds
         bool found = false;
 #pragma unroll
@@ -947,8 +983,21 @@ GEO_HD void pad_sky(const uint8_t* rgba8, uint32_t tw, uint32_t th, uint32_t* ds
     }
 }
 
-// floor(x) as an int32 (one v_cvt_flr_i32_f32 on the device).
-GEO_HD int32_t floor_i32_(float x) { return (int32_t)__builtin_floorf(x); }
+// floor(x) as an int32 for |x| < 2^31 (the sampler's texel coordinates):
+// one v_cvt_flr_i32_f32 on the device, where hipcc emits v_floor_f32 +
+// v_cvt_i32_f32 (two half-rate opcodes) for the cast of floorf.
+#ifndef GEO_CVT_FLR
+#define GEO_CVT_FLR 1  // 0: the cast of floorf (A/B switch)
+#endif
+GEO_HD int32_t floor_i32_(float x) {
+#if defined(__HIP_DEVICE_COMPILE__) && GEO_CVT_FLR
+    int32_t r;
+    asm("v_cvt_flr_i32_f32 %0, %1" : "=v"(r) : "v"(x));
+    return r;
+#else
+    return (int32_t)__builtin_floorf(x);
+#endif
+}
 
 // The G|A channels of a texel into the two 16-bit halves (bytes 1 and 3 to
 // bytes 0 and 2): one v_perm_b32 on the device.

@@ -258,8 +258,7 @@ void geo_oracle_sincosf(float x, float* so, float* co) {
 }
 
 float geo_oracle_asinf(float x) {
-    x = clampf(x, -1.0f, 1.0f);
-    float a = fabsf(x);
+    float a = fminf(fabsf(x), 1.0f); /* NaN -> 1 (geo_math.h asinf_) */
     int big = a > 0.5f;
     float z, sq;
     if (big) {

@@ -124,8 +124,25 @@ GEO_HD float clampf_(float x, float lo, float hi) { return x < lo ? lo : (x > hi
 GEO_HD float fmaxf_(float a, float b) { return a > b ? a : b; }
 
 // sin and cos of x, |x| < ~1e4.
+// rint(t) and (int)rint(t) & 3 for |t| < 2^22 by the 1.5 * 2^23 shifter: t + M
+// rounds t to an integer (ties to even, as rintf) in the low mantissa bits, so
+// j = (t + M) - M exactly and the quadrant is the sum's low 2 bits (M = 0 mod
+// 4); full-rate adds where v_rndne_f32 and v_cvt_i32_f32 are half-rate.
+#ifndef GEO_SINCOS_SHIFTER
+#define GEO_SINCOS_SHIFTER 1  // 0: rintf and the int cast (A/B switch; same values)
+#endif
 GEO_HD void sincosf_(float x, float* s, float* c) {
+#if GEO_SINCOS_SHIFTER
+    constexpr float kShifter = 12582912.0f;  // 1.5 * 2^23
+    const float tj = x * kTwoOverPi + kShifter;
+    const float j = tj - kShifter;
+    uint32_t tb;
+    __builtin_memcpy(&tb, &tj, 4);
+    const int q = (int)(tb & 3u);
+#else
     const float j = __builtin_rintf(x * kTwoOverPi);
+    const int q = ((int)j) & 3;
+#endif
     float r = fmaf_(-j, 1.5703125f, x);
     r = fmaf_(-j, 4.837512969970703125e-4f, r);
     r = fmaf_(-j, 7.54978995489188216e-8f, r);
@@ -135,17 +152,18 @@ GEO_HD void sincosf_(float x, float* s, float* c) {
     const float pc = fmaf_(fmaf_(2.443315711809948e-5f, z, -1.388731625493765e-3f), z,
                            4.166664568298827e-2f);
     const float cs = fmaf_(pc * z, z, fmaf_(-0.5f, z, 1.0f));
-    const int q = ((int)j) & 3;
     const float sa = (q & 1) ? cs : sn;
     const float ca = (q & 1) ? sn : cs;
     *s = (q & 2) ? -sa : sa;
     *c = ((q + 1) & 2) ? -ca : ca;
 }
 
-// asin(x) for x in [-1, 1] (clamped).
+// asin(x) for x in [-1, 1]: |x| clamped to 1 by one v_min_f32 (a NaN x
+// becomes |x| = 1, i.e. +-pi/2 by its sign bit; a compare-and-select clamp
+// kept the NaN: 4 VALU for no case a frame produces), the sign restored by
+// the final copysign.
 GEO_HD float asinf_(float x) {
-    x = clampf_(x, -1.0f, 1.0f);
-    const float a = __builtin_fabsf(x);
+    const float a = __builtin_fminf(__builtin_fabsf(x), 1.0f);
     const bool big = a > 0.5f;
     const float z = big ? 0.5f * (1.0f - a) : a * a;
     // the square root only where it is used: a wave with no |x| > 1/2 lane

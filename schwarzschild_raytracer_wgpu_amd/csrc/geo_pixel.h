@@ -39,6 +39,11 @@ constexpr float kSixth = 1.0f / 6.0f;
 constexpr float kAdaptiveDefaultTol = 1e-6f;  // GEO_ADAPTIVE_DEFAULT_TOL
 constexpr uint32_t kAdaptiveMaxGrowth = 16u;   // GEO_ADAPTIVE_MAX_GROWTH
 
+// Integration kinds (frame-uniform, chosen on the host):
+constexpr int kCurvedOut = 0;  // rs > 0, observer outside the horizon (r > rs)
+constexpr int kCurvedIn = 1;   // rs > 0, observer on/inside the horizon
+constexpr int kFlat = 2;       // rs = 0: straight lines
+
 // Frame-constant scalars derived from the scene, evaluated identically on
 // every lane (and by the oracle).  Names follow sphere_ray_tracer.rs:60-132.
 struct PixelConsts {
@@ -74,6 +79,13 @@ struct PixelConsts {
     // kernel reads it with one scalar load (the bool bytes above sit at
     // unaligned kernarg offsets, which hipcc fetches with vector loads)
     uint32_t pf_bits;
+    // frame-uniform parts of the stop test and the initial loop test, folded
+    // on the host (gfx9 has no scalar float compares, so the kernel would
+    // evaluate them in VALU on every lane): StopTest's interval [stop_lo,
+    // stop_hi] and stop_bits = above0 (U0 > SU) | absorbing << 1 (for this
+    // frame's integration kind) | (max_steps != 0 && u0 > 0) << 2
+    float stop_lo, stop_hi;
+    uint32_t stop_bits;
     // the integrator's scaled state U = scale*u (scale = 3 rs/2, or 1 for rs = 0)
     float scale, U0, SU, BD, HU;
     float SUp;  // next float above SU: (U > SU) == (U >= SUp) for every float U
@@ -87,10 +99,6 @@ struct PixelConsts {
 #define GEO_PF_BITS 1  // 0: read the pre-filter bools (A/B switch)
 #endif
 
-// Integration kinds (frame-uniform, chosen on the host):
-constexpr int kCurvedOut = 0;  // rs > 0, observer outside the horizon (r > rs)
-constexpr int kCurvedIn = 1;   // rs > 0, observer on/inside the horizon
-constexpr int kFlat = 2;       // rs = 0: straight lines
 
 // Next float above a positive finite x.
 GEO_HD float next_up_(float x) {
@@ -192,6 +200,14 @@ GEO_HD PixelConsts make_consts(float rs, float sphere_r, float r, float step, ui
     k.BD = k.scale * k.bound;
     k.HU = k.scale * k.schwarz_u;
     k.SUp = next_up_(k.SU);
+    {
+        const bool above0 = k.U0 > k.SU;
+        const int kind = !k.rs_nonzero ? kFlat : (k.outside ? kCurvedOut : kCurvedIn);
+        const bool absorbing = kind != kCurvedIn && above0 && (kind == kFlat || k.SU < 1.0f);
+        k.stop_lo = above0 ? k.SUp : k.BD;
+        k.stop_hi = above0 ? k.HU : k.SU;
+        k.stop_bits = (above0 ? 1u : 0u) | (absorbing ? 2u : 0u) | ((max_steps != 0u && k.u0 > 0.0f) ? 4u : 0u);
+    }
     k.tolU = k.scale * (tol > 0.0f ? tol : kAdaptiveDefaultTol);
     k.tolG = k.tolU * (1.0f / 64.0f);
     k.hmax = step * (float)kAdaptiveMaxGrowth;
@@ -331,7 +347,7 @@ GEO_HD bool geodesic_init(const PixelConsts& k, float st, float ct, float rct, f
     if (!falling) ub = -ub;
     // loop test of :134-135 on the initial state (schwarz_u = +inf for rs = 0;
     // u0 > schwarz_u needs r < rs)
-    if ((KIND == kCurvedIn && k.u0 > k.schwarz_u && ub > 0.0f) || k.max_steps == 0u || !(k.u0 > 0.0f)) {
+    if ((KIND == kCurvedIn && k.u0 > k.schwarz_u && ub > 0.0f) || !(k.stop_bits & 4u)) {
         *early = kNoValue;
         return false;
     }
@@ -357,10 +373,9 @@ struct StopTest {
     bool above0;
     bool absorbing;  // the stop set is absorbing (run_groups): observer inside the sphere, sphere
                      // beyond the photon sphere (SU < 1: F < 0 below SU), outside the horizon
-    GEO_HDM explicit StopTest(const PixelConsts& k) : SU(k.SU), BD(k.BD), HU(k.HU), above0(k.U0 > k.SU) {
-        lo = above0 ? k.SUp : BD;
-        hi = above0 ? HU : SU;
-        absorbing = KIND != kCurvedIn && above0 && (KIND == kFlat || SU < 1.0f);
+    GEO_HDM explicit StopTest(const PixelConsts& k)
+        : SU(k.SU), BD(k.BD), HU(k.HU), lo(k.stop_lo), hi(k.stop_hi), above0((k.stop_bits & 1u) != 0) {
+        absorbing = KIND != kCurvedIn && (k.stop_bits & 2u) != 0;
     }
     GEO_HDM bool operator()(float NU, float NUB) const {
         if constexpr (KIND == kCurvedIn)

@@ -56,9 +56,12 @@ def parse():
                         "kernel time is measured on 20 back-to-back launches on one stream after the timed region. "
                         "N = 1 keeps one stream so that in-region launch times and rocprofv3's agree (--pipelined "
                         "reports the two-stream throughput beside it)")
-    p.add_argument("--frames-per-gather", type=int, default=8,
+    p.add_argument("--frames-per-gather", type=int, default=None,
                    help="N > 1: frames per RCCL gather to rank 0 (amortises the ~34 us host cost of a gather; "
-                        "rank 0 reassembles each batch with one geo_assemble_lead launch)")
+                        "rank 0 reassembles each batch with one geo_assemble_lead launch).  Default: --steps / 10, "
+                        "clamped to [1, 8]: the timed region ends with the last batch's gather and reassembly, "
+                        "and its first batch's renders run before any gather starts, so a short run wants "
+                        "shallow batches (20 steps: 2) and a long one amortises the host cost (200 steps: 8)")
     p.add_argument("--rank0-lead", default="auto", choices=["auto", "1", "2", "3", "4", "6"],
                    help="N > 1: rank 0's band height in 8-row bands per cycle (it renders rows that never cross "
                         "an xGMI link, so a link-bound present wants it larger); auto = the fastest of 1, 2, 3, 4, "
@@ -107,6 +110,8 @@ def main():
         else:
             dist.init_process_group("gloo")
 
+    if args.frames_per_gather is None:
+        args.frames_per_gather = max(1, min(8, args.steps // 10))
     cfg = CONFIGS[args.config]
     W, H = cfg.width, cfg.height
     obs = g.Observer(cfg.rs, cfg.fov, W, H)

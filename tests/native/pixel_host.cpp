@@ -94,3 +94,12 @@ extern "C" int host_sample_padded(const uint32_t* sky, uint32_t sw, uint32_t sh,
     delete[] pad;
     return 0;
 }
+
+// The header's transcendentals on n inputs (host build of geo_math.h), for
+// bit comparisons with the oracle's restatement.
+extern "C" void host_math(const float* x, uint32_t n, float* out_sin, float* out_cos, float* out_asin) {
+    for (uint32_t i = 0; i < n; ++i) {
+        geo::sincosf_(x[i], &out_sin[i], &out_cos[i]);
+        out_asin[i] = geo::asinf_(x[i]);
+    }
+}

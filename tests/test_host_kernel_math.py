@@ -208,3 +208,38 @@ def test_padded_sky_quad_equals_wrap_clamp(host, sw, sh):
     host.host_sample_padded(vp(sky.ctypes.data), ctypes.c_uint32(sw), ctypes.c_uint32(sh), vp(U.ctypes.data),
                             vp(V.ctypes.data), ctypes.c_uint32(U.size), vp(a.ctypes.data), vp(b.ctypes.data))
     assert np.array_equal(a, b)
+
+
+def test_host_transcendentals_equal_oracle(host):
+    """geo_math.h's sincosf_ (quadrant and rint by the 1.5 * 2^23 shifter) and
+    asinf_ (|x| clamped by fminf) host-compiled equal the oracle's
+    restatement (rintf, fminf) bit for bit: random and huge arguments,
+    x * 2/pi at and next to half-integers (the rounding ties), |x| > 1 and
+    NaN for asin (NaN -> +-pi/2 by its sign bit)."""
+    rng = np.random.default_rng(7)
+    two_over_pi = np.float32(0.636619772367581343076)
+    ties = []
+    for k in range(-600, 600):
+        t = np.float32(k + 0.5)
+        # arguments whose rounded product with 2/pi lands on, just below and just above k + 1/2
+        x0 = np.float32(t / two_over_pi)
+        for x in (x0, np.nextafter(x0, np.float32(np.inf)), np.nextafter(x0, np.float32(-np.inf))):
+            ties.append(x)
+    xs = np.concatenate([rng.uniform(-10, 10, 20000), rng.uniform(-1.2, 1.2, 20000), rng.uniform(-9000, 9000, 5000),
+                         np.array(ties, np.float64), [0.0, -0.0, 1.0, -1.0, 1.5, -1.5, np.nan, -np.nan]]
+                        ).astype(np.float32)
+    n = xs.size
+    s, c, a = (np.empty(n, np.float32) for _ in range(3))
+    host.host_math(xs.ctypes.data_as(ctypes.c_void_p), ctypes.c_uint32(n), s.ctypes.data_as(ctypes.c_void_p),
+                   c.ctypes.data_as(ctypes.c_void_p), a.ctypes.data_as(ctypes.c_void_p))
+    for i, x in enumerate(xs):
+        os_, oc = O.sincosf(float(x))
+        oa = O.asinf(float(x))
+        if math.isnan(x):
+            assert abs(a[i]) == np.float32(math.pi / 2)
+            continue
+        assert np.float32(os_).view(np.uint32) == s[i].view(np.uint32), (x, os_, s[i])
+        assert np.float32(oc).view(np.uint32) == c[i].view(np.uint32), (x, oc, c[i])
+        assert np.float32(oa).view(np.uint32) == a[i].view(np.uint32), (x, oa, a[i])
+    assert O.asinf(-1.5) == np.float32(-math.pi / 2)
+    assert abs(O.asinf(float("nan"))) == np.float32(math.pi / 2)

@@ -477,6 +477,9 @@ GEO_HD uint64_t group_stop_(const StopTest<KIND>& stop_at, const float (&ou)[G],
     }
 }
 
+#ifndef GEO_LIVE_EXEC
+#define GEO_LIVE_EXEC 1  // 0: a per-lane `done` flag masks the group steps (A/B switch)
+#endif
 template <int G, int KIND, bool LAST_ONLY>
 GEO_HD uint32_t run_groups_pp(const StopTest<KIND>& stop_at, uint32_t ngroups, uint32_t all, float h, float hh,
                               float hh2, float hhh, float h6, float h2_6, float (&su_)[G + 1], float (&sb_)[G + 1]) {
@@ -498,6 +501,57 @@ GEO_HD uint32_t run_groups_pp(const StopTest<KIND>& stop_at, uint32_t ngroups, u
     // set its states sit in is (it / G) & 1 after the loop: the loop carries
     // one lane flag (`done`), which keeps the lane-mask merges at its joins
     // to a minimum.
+#if GEO_LIVE_EXEC
+    // The lanes still integrating are the wave-uniform mask `live`, which is
+    // also the exec mask of the group steps: no per-lane flag, so the loop's
+    // scalar work is the masked regions, one AND per stop test and a branch
+    // (`hit`, uniform) past the rare block where lanes stop.
+    uint64_t live = ballot_(true);
+    uint32_t it = all;
+    uint32_t q = 0;
+    while (q < ngroups) {
+        if (in_ballot_(live)) group_steps_<G, KIND>(xu, xb, h, hh, hh2, hhh, h6, h2_6, au, ab);
+        uint64_t hit = group_stop_<G, KIND, LAST_ONLY>(stop_at, au, ab) & live;
+        if (hit != 0) {
+            if (in_ballot_(hit)) {
+                GEO_RARE();
+                it = q * (uint32_t)G;
+            }
+            live &= ~hit;
+        }
+        if (++q >= ngroups) break;
+        if (live == 0) break;
+        if (in_ballot_(live)) {
+            float ou[G], ob[G];
+            group_steps_<G, KIND>(au[G - 1], ab[G - 1], h, hh, hh2, hhh, h6, h2_6, ou, ob);
+#pragma unroll
+            for (int j = 0; j < G - 1; ++j) {
+                bu[j] = ou[j];
+                bb[j] = ob[j];
+            }
+            xu = ou[G - 1];
+            xb = ob[G - 1];
+        }
+        float tu[G], tb[G];
+#pragma unroll
+        for (int j = 0; j < G - 1; ++j) {
+            tu[j] = bu[j];
+            tb[j] = bb[j];
+        }
+        tu[G - 1] = xu;
+        tb[G - 1] = xb;
+        hit = group_stop_<G, KIND, LAST_ONLY>(stop_at, tu, tb) & live;
+        if (hit != 0) {
+            if (in_ballot_(hit)) {
+                GEO_RARE();
+                it = q * (uint32_t)G;
+            }
+            live &= ~hit;
+        }
+        ++q;
+        if (live == 0) break;
+    }
+#else
     bool done = false;
     uint64_t live = ballot_(true);  // wave-uniform: the lanes still integrating
     uint32_t it = all;
@@ -547,6 +601,7 @@ GEO_HD uint32_t run_groups_pp(const StopTest<KIND>& stop_at, uint32_t ngroups, u
         ++q;
         if (live == 0) break;
     }
+#endif
     // the set holding the stopping group (B: start a_G, then b_1..b_{G-1}, X);
     // a lane on the budget continues from the last group's end state, which
     // sits where a B group's start state (a_G, after an A group) or an A

@@ -477,6 +477,9 @@ GEO_HD uint64_t group_stop_(const StopTest<KIND>& stop_at, const float (&ou)[G],
     }
 }
 
+#ifndef GEO_PAIR_LOOP
+#define GEO_PAIR_LOOP 1  // 0: exit tests after each group (A/B switch)
+#endif
 #ifndef GEO_LIVE_EXEC
 #define GEO_LIVE_EXEC 1  // 0: a per-lane `done` flag masks the group steps (A/B switch)
 #endif
@@ -509,6 +512,68 @@ GEO_HD uint32_t run_groups_pp(const StopTest<KIND>& stop_at, uint32_t ngroups, u
     uint64_t live = ballot_(true);
     uint32_t it = all;
     uint32_t q = 0;
+#if GEO_PAIR_LOOP
+    // One exit test per A+B pair of groups: a group whose lanes are all done
+    // runs with an empty exec mask, which the masked region's execz branch
+    // skips, so the pair needs no test between its groups; an odd budget's
+    // last group is an A group after the loop.
+    // one exit edge (hipcc's structurizer turns a second one into lane-mask
+    // flags at the latch): an empty `live` zeroes the pair counter instead
+    uint32_t rem = ngroups >> 1;
+    while (rem != 0) {
+        if (in_ballot_(live)) group_steps_<G, KIND>(xu, xb, h, hh, hh2, hhh, h6, h2_6, au, ab);
+        uint64_t hit = group_stop_<G, KIND, LAST_ONLY>(stop_at, au, ab) & live;
+        --rem;
+        if (hit != 0) {
+            if (in_ballot_(hit)) {
+                GEO_RARE();
+                it = q * (uint32_t)G;
+            }
+            live &= ~hit;
+            rem = live == 0 ? 0u : rem;  // (the B group below then runs on an empty exec mask: skipped)
+        }
+        if (in_ballot_(live)) {
+            float ou[G], ob[G];
+            group_steps_<G, KIND>(au[G - 1], ab[G - 1], h, hh, hh2, hhh, h6, h2_6, ou, ob);
+#pragma unroll
+            for (int j = 0; j < G - 1; ++j) {
+                bu[j] = ou[j];
+                bb[j] = ob[j];
+            }
+            xu = ou[G - 1];
+            xb = ob[G - 1];
+        }
+        float tu[G], tb[G];
+#pragma unroll
+        for (int j = 0; j < G - 1; ++j) {
+            tu[j] = bu[j];
+            tb[j] = bb[j];
+        }
+        tu[G - 1] = xu;
+        tb[G - 1] = xb;
+        hit = group_stop_<G, KIND, LAST_ONLY>(stop_at, tu, tb) & live;
+        q += 2u;
+        // `live` empties only where lanes stop, so its test sits in that
+        // branch: a pair without stops ends in the counter's compare alone
+        if (hit != 0) {
+            if (in_ballot_(hit)) {
+                GEO_RARE();
+                it = (q - 1u) * (uint32_t)G;
+            }
+            live &= ~hit;
+            rem = live == 0 ? 0u : rem;
+        }
+    }
+    if ((ngroups & 1u) != 0 && live != 0) {
+        if (in_ballot_(live)) group_steps_<G, KIND>(xu, xb, h, hh, hh2, hhh, h6, h2_6, au, ab);
+        const uint64_t hit = group_stop_<G, KIND, LAST_ONLY>(stop_at, au, ab) & live;
+        if (in_ballot_(hit)) {
+            GEO_RARE();
+            it = q * (uint32_t)G;
+        }
+        ++q;
+    }
+#else
     while (q < ngroups) {
         if (in_ballot_(live)) group_steps_<G, KIND>(xu, xb, h, hh, hh2, hhh, h6, h2_6, au, ab);
         uint64_t hit = group_stop_<G, KIND, LAST_ONLY>(stop_at, au, ab) & live;
@@ -551,6 +616,7 @@ GEO_HD uint32_t run_groups_pp(const StopTest<KIND>& stop_at, uint32_t ngroups, u
         ++q;
         if (live == 0) break;
     }
+#endif
 #else
     bool done = false;
     uint64_t live = ballot_(true);  // wave-uniform: the lanes still integrating

@@ -70,8 +70,31 @@ GEO_HD float fmaf_(float a, float b, float c) { return __builtin_fmaf(a, b, c); 
 #ifndef GEO_FAST_SQRT
 #define GEO_FAST_SQRT 1  // 0: the builtin everywhere (A/B switch, tools/gpu_ab.sh)
 #endif
+// GEO_UNIFORM_FIXUP (sqrtf_, rcpf_): the fast sequence runs on every lane
+// with no exec-mask change, and the out-of-range lanes are redone in a
+// wave-uniform branch that a typical wave never takes (a divergent if/else
+// costs ~6 scalar instructions of exec juggling per call, ~10 calls a pixel).
+#ifndef GEO_UNIFORM_FIXUP
+#define GEO_UNIFORM_FIXUP 1
+#endif
 GEO_HD float sqrtf_(float x) {
 #if defined(__HIP_DEVICE_COMPILE__) && GEO_FAST_SQRT
+#if GEO_UNIFORM_FIXUP
+    const bool ok = x >= 0x1p-96f;
+    const float s = __builtin_amdgcn_sqrtf(x);
+    const uint32_t si = __builtin_bit_cast(uint32_t, s);
+    const float sm = __builtin_bit_cast(float, si - 1u);
+    const float sp = __builtin_bit_cast(float, si + 1u);
+    const float rm = __builtin_fmaf(-sm, s, x);
+    const float rp = __builtin_fmaf(-sp, s, x);
+    const float t = (0.0f >= rm) ? sm : s;
+    float r = (0.0f < rp) ? sp : t;
+    if (__builtin_amdgcn_ballot_w64(!ok) != 0) {
+        GEO_COLD_ARM();
+        r = ok ? r : __builtin_sqrtf(x);
+    }
+    return r;
+#else
     if (x >= 0x1p-96f) {
         const float s = __builtin_amdgcn_sqrtf(x);
         const uint32_t si = __builtin_bit_cast(uint32_t, s);
@@ -82,6 +105,7 @@ GEO_HD float sqrtf_(float x) {
         const float t = (0.0f >= rm) ? sm : s;
         return (0.0f < rp) ? sp : t;
     }
+#endif
 #endif
     return __builtin_sqrtf(x);
 }
@@ -98,10 +122,21 @@ GEO_HD float sqrtf_(float x) {
 GEO_HD float rcpf_(float x) {
 #if defined(__HIP_DEVICE_COMPILE__) && GEO_FAST_RCP
     const float ax = __builtin_fabsf(x);
+#if GEO_UNIFORM_FIXUP
+    const bool ok = __builtin_amdgcn_fmed3f(ax, 0x1p-126f, 0x1.fffffep125f) == ax;
+    const float r0 = __builtin_amdgcn_rcpf(x);
+    float r = __builtin_fmaf(__builtin_fmaf(-x, r0, 1.0f), r0, r0);
+    if (__builtin_amdgcn_ballot_w64(!ok) != 0) {
+        GEO_COLD_ARM();
+        r = ok ? r : 1.0f / x;
+    }
+    return r;
+#else
     if (__builtin_amdgcn_fmed3f(ax, 0x1p-126f, 0x1.fffffep125f) == ax) {
         const float r = __builtin_amdgcn_rcpf(x);
         return __builtin_fmaf(__builtin_fmaf(-x, r, 1.0f), r, r);
     }
+#endif
 #endif
     return 1.0f / x;
 }

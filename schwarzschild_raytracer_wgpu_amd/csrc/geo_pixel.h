@@ -1008,14 +1008,50 @@ GEO_HD void pixel_central_dir(const CameraConsts& cc, const float* m1, float psi
     }
 }
 
+// floor(x) as an int32 for |x| < 2^31 (the sampler's texel coordinates):
+// one v_cvt_flr_i32_f32 on the device, where hipcc emits v_floor_f32 +
+// v_cvt_i32_f32 (two half-rate opcodes) for the cast of floorf.
+#ifndef GEO_CVT_FLR
+#define GEO_CVT_FLR 1  // 0: the cast of floorf (A/B switch)
+#endif
+GEO_HD int32_t floor_i32_(float x) {
+#if defined(__HIP_DEVICE_COMPILE__) && GEO_CVT_FLR
+    int32_t r;
+    asm("v_cvt_flr_i32_f32 %0, %1" : "=v"(r) : "v"(x));
+    return r;
+#else
+    return (int32_t)__builtin_floorf(x);
+#endif
+}
+
 // Fan lookup (shader.wgsl:77-84); i+1 clamped to n-1 (weight 0 there).
+// On the device, with the same bits: the quotient by pi as a * RN(1/pi) plus
+// one fma correction (exhaustively equal to a / pi over fan_lerp's domain,
+// tests/native/divpi_exhaustive.hip), the index by v_cvt_flr_i32_f32 and the
+// weight by v_fract_f32 (t - floor(t), exact for t >= 0).
+#ifndef GEO_FAN_FAST
+#define GEO_FAN_FAST 1  // 0: the division and floorf (A/B switch; same values)
+#endif
 GEO_HD float fan_lerp(const float* fan, uint32_t n, float st) {
     const float theta = asinf_(st);
-    float t = clampf_((kPi2 - theta) / kPi, 0.0f, 1.0f);
+    const float a = kPi2 - theta;
+#if defined(__HIP_DEVICE_COMPILE__) && GEO_FAN_FAST
+    constexpr float kRcpPi = 1.0f / kPi;
+    const float q0 = a * kRcpPi;
+    const float quot = fmaf_(fmaf_(-q0, kPi, a), kRcpPi, q0);
+#else
+    const float quot = a / kPi;
+#endif
+    float t = clampf_(quot, 0.0f, 1.0f);
     t = t * (float)(n - 1u);
+#if defined(__HIP_DEVICE_COMPILE__) && GEO_FAN_FAST
+    const uint32_t i = (uint32_t)floor_i32_(t);
+    const float w = __builtin_amdgcn_fractf(t);
+#else
     const float fl = __builtin_floorf(t);
     const uint32_t i = (uint32_t)fl;
     const float w = t - fl;
+#endif
     const uint32_t i1 = (i + 1u < n) ? i + 1u : n - 1u;
     return fan[i] * (1.0f - w) + fan[i1] * w;
 }
@@ -1119,21 +1155,6 @@ GEO_HD void pad_sky(const uint8_t* rgba8, uint32_t tw, uint32_t th, uint32_t* ds
     }
 }
 
-// floor(x) as an int32 for |x| < 2^31 (the sampler's texel coordinates):
-// one v_cvt_flr_i32_f32 on the device, where hipcc emits v_floor_f32 +
-// v_cvt_i32_f32 (two half-rate opcodes) for the cast of floorf.
-#ifndef GEO_CVT_FLR
-#define GEO_CVT_FLR 1  // 0: the cast of floorf (A/B switch)
-#endif
-GEO_HD int32_t floor_i32_(float x) {
-#if defined(__HIP_DEVICE_COMPILE__) && GEO_CVT_FLR
-    int32_t r;
-    asm("v_cvt_flr_i32_f32 %0, %1" : "=v"(r) : "v"(x));
-    return r;
-#else
-    return (int32_t)__builtin_floorf(x);
-#endif
-}
 
 // The G|A channels of a texel into the two 16-bit halves (bytes 1 and 3 to
 // bytes 0 and 2): one v_perm_b32 on the device.

@@ -77,3 +77,21 @@ def test_cvt_flr_and_sincos_shifter_exhaustive(tmp_path):
                     os.path.join(HERE, "native", "flr_exhaustive.hip"), "-o", exe], check=True)
     r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and "mismatches 0" in r.stdout, r.stdout + r.stderr
+
+
+def test_fan_quotient_by_pi_exhaustive(tmp_path):
+    """geo::fan_lerp's device quotient by pi (RN(1/pi) product plus one fma
+    correction) equals the correctly rounded a / pi over its whole domain
+    (tests/native/divpi_exhaustive.hip)."""
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    if not (os.path.exists(HIPCC) or shutil.which("hipcc")):
+        pytest.skip("no hipcc")
+    exe = str(tmp_path / "divpi_exhaustive")
+    subprocess.run([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off",
+                    "-fhip-fp32-correctly-rounded-divide-sqrt", "-fno-gpu-flush-denormals-to-zero",
+                    os.path.join(HERE, "native", "divpi_exhaustive.hip"), "-o", exe], check=True)
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "mismatches 0" in r.stdout, r.stdout + r.stderr

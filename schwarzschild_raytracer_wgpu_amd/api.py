@@ -393,7 +393,8 @@ class RayConnectors:
 
     def set_positions(self, positions) -> None:
         pos = np.ascontiguousarray(positions, dtype=np.float32).reshape(-1, 3)
-        assert pos.shape[0] == self.n_points
+        if pos.shape[0] != self.n_points:
+            raise ValueError(f"positions: {self.n_points} points expected, got {pos.shape[0]}")
         check("geo_rays_set_positions", lib.geo_rays_set_positions(self._h, pos.ctypes.data))
 
     def _call(self, other, iterations: int, reset: bool, stream):

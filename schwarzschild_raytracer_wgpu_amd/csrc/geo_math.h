@@ -64,9 +64,12 @@ GEO_HD float fmaf_(float a, float b, float c) { return __builtin_fmaf(a, b, c); 
 // v_sqrt_f32 in a 2^32 pre-scale for x < 2^-96 and a class fix-up for
 // ±0/+inf (≈ 17 VALU).  For x >= 2^-96 (finite or +inf) the scale is not
 // applied and the fix-up returns the corrected value, so the correction alone
-// gives the same bits (9 VALU).  Smaller, zero and NaN inputs take the builtin
-// (a branch that no lane of a typical wave takes).  Exhaustively checked
-// against __builtin_sqrtf over all 2^32 inputs (tests/test_gpu_math.py).
+// gives the same bits (9 VALU).  Cheaper still (GEO_SQRT_RSQ, the default):
+// s = x rsq(x) corrected once by its residual, s + (x - s^2) rsq(x)/2, which
+// is correctly rounded for every finite x >= 2^-96 (5 VALU).  Smaller, zero,
+// NaN and infinite inputs take the builtin (a branch that no lane of a
+// typical wave takes).  Exhaustively checked against __builtin_sqrtf over all
+// 2^32 inputs (tests/test_gpu_math.py).
 #ifndef GEO_FAST_SQRT
 #define GEO_FAST_SQRT 1  // 0: the builtin everywhere (A/B switch, tools/gpu_ab.sh)
 #endif
@@ -77,9 +80,26 @@ GEO_HD float fmaf_(float a, float b, float c) { return __builtin_fmaf(a, b, c); 
 #ifndef GEO_UNIFORM_FIXUP
 #define GEO_UNIFORM_FIXUP 1
 #endif
+#ifndef GEO_SQRT_RSQ
+#define GEO_SQRT_RSQ 1  // 0: v_sqrt_f32 with the +-1-ulp correction (A/B switch; same values)
+#endif
 GEO_HD float sqrtf_(float x) {
 #if defined(__HIP_DEVICE_COMPILE__) && GEO_FAST_SQRT
-#if GEO_UNIFORM_FIXUP
+#if GEO_UNIFORM_FIXUP && GEO_SQRT_RSQ
+    // s = x rsq(x), corrected once by the residual: s + (x - s^2) rsq(x)/2.
+    // Correctly rounded for every finite x >= 2^-96 (the exhaustive test over
+    // all 2^32 inputs below covers it): 5 VALU + the range test, against 9.
+    const bool ok = __builtin_amdgcn_fmed3f(x, 0x1p-96f, 0x1.fffffep127f) == x;  // NaN, +inf fail
+    const float y = __builtin_amdgcn_rsqf(x);
+    const float s0 = x * y;
+    const float hy = 0.5f * y;
+    float r = __builtin_fmaf(__builtin_fmaf(-s0, s0, x), hy, s0);
+    if (__builtin_amdgcn_ballot_w64(!ok) != 0) {
+        GEO_COLD_ARM();
+        r = ok ? r : __builtin_sqrtf(x);
+    }
+    return r;
+#elif GEO_UNIFORM_FIXUP
     const bool ok = x >= 0x1p-96f;
     const float s = __builtin_amdgcn_sqrtf(x);
     const uint32_t si = __builtin_bit_cast(uint32_t, s);

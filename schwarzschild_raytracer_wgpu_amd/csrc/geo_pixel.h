@@ -878,6 +878,9 @@ GEO_HD void dp5_step(float U, float V, float h, float hh, float* NU, float* NV, 
     *SE = fmaf_(e6, g6, fmaf_(e5, g5, fmaf_(e4, g4, fmaf_(e3, g3, e1 * g1))));
 }
 
+#ifndef GEO_ADAPTIVE_HFACTOR
+#define GEO_ADAPTIVE_HFACTOR 1  // 0: the step update as h + h / h / h * 0.5 selects (A/B switch; same bits)
+#endif
 // Traveled angle with error-controlled steps, or kNoValue; *steps = step
 // attempts (accepted + rejected).  Same ray set-up, stop order and Newton
 // sphere crossing as the fixed-step path (sphere_ray_tracer.rs:60-193), with
@@ -913,11 +916,21 @@ GEO_HD float geodesic_angle_adaptive(const PixelConsts& k, float st, float ct, f
         }
         // min(2h, hmax) as a growth test: h is step/2^j or step*2^j <= hmax with
         // hmax = 16 step, so h < hmax implies 2h <= hmax (same bits, 2 fewer VALU)
+#if GEO_ADAPTIVE_HFACTOR
+        // the new step as h times 2, 1 or 1/2 (exact: the same bits as h + h,
+        // h and h * 0.5), one multiply after two selects of the factor
+        const float grow = (err < k.tolG && h < k.hmax) ? 2.0f : 1.0f;
+        U = acc ? NU : U;
+        V = acc ? NV : V;
+        ang = acc ? ang + h : ang;
+        h = h * (acc ? grow : 0.5f);
+#else
         const float hg = (err < k.tolG && h < k.hmax) ? h + h : h;
         U = acc ? NU : U;
         V = acc ? NV : V;
         ang = acc ? ang + h : ang;
         h = acc ? hg : h * 0.5f;
+#endif
     }
     *steps = it;
     if (!stopped || (NU > k.SU) == (U > k.SU)) return kNoValue;

@@ -1196,13 +1196,14 @@ GEO_HD uint32_t sample_sky_quad_f(const Quad& quad, float tw256, float th256, fl
     quad(nx >> 8, ny >> 8, t);
     const uint32_t t00 = t[0], t10 = t[1], t01 = t[2], t11 = t[3];
     const uint32_t iwx = 256u - wx, iwy = 256u - wy;
-    // horizontal (fields <= 255*256), truncated to 8 bits, then vertical, rounded
-    const uint32_t trb = (lerp2_(rb_(t00), rb_(t10), iwx, wx) >> 8) & 0x00FF00FFu;
-    const uint32_t brb = (lerp2_(rb_(t01), rb_(t11), iwx, wx) >> 8) & 0x00FF00FFu;
-    const uint32_t tga = (lerp2_(ga_perm_(t00), ga_perm_(t10), iwx, wx) >> 8) & 0x00FF00FFu;
-    const uint32_t bga = (lerp2_(ga_perm_(t01), ga_perm_(t11), iwx, wx) >> 8) & 0x00FF00FFu;
-    const uint32_t crb = ((lerp2_(trb, brb, iwy, wy) + 0x00800080u) >> 8) & 0x00FF00FFu;
-    const uint32_t cga = ((lerp2_(tga, bga, iwy, wy) + 0x00800080u) >> 8) & 0x00FF00FFu;
+    // horizontal (fields <= 255*256), truncated to 8 bits, then vertical, rounded;
+    // (x >> 8) & 0x00FF00FF is ga_perm_'s byte move (one v_perm_b32)
+    const uint32_t trb = ga_perm_(lerp2_(rb_(t00), rb_(t10), iwx, wx));
+    const uint32_t brb = ga_perm_(lerp2_(rb_(t01), rb_(t11), iwx, wx));
+    const uint32_t tga = ga_perm_(lerp2_(ga_perm_(t00), ga_perm_(t10), iwx, wx));
+    const uint32_t bga = ga_perm_(lerp2_(ga_perm_(t01), ga_perm_(t11), iwx, wx));
+    const uint32_t crb = ga_perm_(lerp2_(trb, brb, iwy, wy) + 0x00800080u);
+    const uint32_t cga = ga_perm_(lerp2_(tga, bga, iwy, wy) + 0x00800080u);
     return crb | (cga << 8);
 }
 template <typename Quad>

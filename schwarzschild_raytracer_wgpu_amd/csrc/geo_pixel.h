@@ -86,6 +86,10 @@ struct PixelConsts {
     // frame's integration kind) | (max_steps != 0 && u0 > 0) << 2
     float stop_lo, stop_hi;
     uint32_t stop_bits;
+    // |U'| above which a ray may overshoot the absorbing stop set (see
+    // absorbing_safe_): kRiskK / h^3 less the ray-independent part of the
+    // scaled 1/b bound, scale sqrt(max(0, h_over_r2))
+    float risk_ub;
     // the integrator's scaled state U = scale*u (scale = 3 rs/2, or 1 for rs = 0)
     float scale, U0, SU, BD, HU;
     float SUp;  // next float above SU: (U > SU) == (U >= SUp) for every float U
@@ -136,6 +140,14 @@ typedef bool LaneMask;
 GEO_HD LaneMask lane_mask_(bool c) { return c; }
 GEO_HD bool lane_select_(LaneMask m, bool a, bool b) { return m ? a : b; }
 #endif
+
+// Overshoot bound of the absorbing-set test (absorbing_safe_): a ray's |U'|
+// stays below scale/b along its path, and a step h can carry U from above the
+// sphere to below 0 and back within a group of 4 only if h^3 scale/b is of
+// order 1/3 (F(U) = U^2 - U is positive again below 0, so a deep overshoot is
+// pushed back up).  Rays with h^3 scale/b above kRiskK = 1e-3 (a margin of
+// ~300) take the per-step test.
+constexpr float kRiskK = 1e-3f;
 
 // tol: GEO_MODE_ADAPTIVE local error tolerance in u (<= 0: the default 1e-6).
 GEO_HD PixelConsts make_consts(float rs, float sphere_r, float r, float step, uint32_t max_steps,
@@ -207,6 +219,7 @@ GEO_HD PixelConsts make_consts(float rs, float sphere_r, float r, float step, ui
         k.stop_lo = above0 ? k.SUp : k.BD;
         k.stop_hi = above0 ? k.HU : k.SU;
         k.stop_bits = (above0 ? 1u : 0u) | (absorbing ? 2u : 0u) | ((max_steps != 0u && k.u0 > 0.0f) ? 4u : 0u);
+        k.risk_ub = kRiskK / (step * step * step) - k.scale * __builtin_sqrtf(k.h_over_r2 > 0.0f ? k.h_over_r2 : 0.0f);
     }
     k.tolU = k.scale * (tol > 0.0f ? tol : kAdaptiveDefaultTol);
     k.tolG = k.tolU * (1.0f / 64.0f);
@@ -685,6 +698,9 @@ GEO_HD uint32_t run_groups_pp(const StopTest<KIND>& stop_at, uint32_t ngroups, u
     return it;
 }
 
+#ifndef GEO_RISK_TEST
+#define GEO_RISK_TEST 1  // 0: the frame-uniform absorbing choice alone (A/B and fuzz switch)
+#endif
 #ifndef GEO_SCAN_BSEARCH
 #define GEO_SCAN_BSEARCH 1  // 0: the linear scan everywhere (A/B switch)
 #endif
@@ -695,8 +711,8 @@ GEO_HD uint32_t run_groups_pp(const StopTest<KIND>& stop_at, uint32_t ngroups, u
 // crossing test and Newton (sphere_ray_tracer.rs:150-191).  *steps =
 // executed main-loop RK4 steps.
 template <int G, int KIND>
-GEO_HD float geodesic_finish(const PixelConsts& k, const StopTest<KIND>& stop_at, uint32_t it, float (&su_)[G + 1],
-                             float (&sb_)[G + 1], uint32_t* steps) {
+GEO_HD float geodesic_finish(const PixelConsts& k, const StopTest<KIND>& stop_at, bool absorbing, uint32_t it,
+                             float (&su_)[G + 1], float (&sb_)[G + 1], uint32_t* steps) {
     const uint32_t ms = k.max_steps;
     // Opaque copies: the per-step flags are recomputed from the state rather
     // than carried out of the loop as lane masks.
@@ -707,7 +723,7 @@ GEO_HD float geodesic_finish(const PixelConsts& k, const StopTest<KIND>& stop_at
     }
     GEO_OPAQUE(it);
     float ou = su_[0], oub = sb_[0], nu = su_[0], nub = sb_[0];
-    if (G == 4 && GEO_SCAN_BSEARCH && stop_at.absorbing && GEO_ABSORBING_TEST && it + (uint32_t)G <= ms) {
+    if (G == 4 && GEO_SCAN_BSEARCH && absorbing && GEO_ABSORBING_TEST && it + (uint32_t)G <= ms) {
         // stopped inside the group, where the stop set is absorbing: the
         // flags of states 1..4 are monotone (false.. then true.., state 4's
         // true), so two tests find the first stopping state k -- state 2,
@@ -797,24 +813,35 @@ GEO_HD float geodesic_angle_v(const PixelConsts& k, float st, float ct, float rc
         su_[j] = U;
         sb_[j] = UB;
     }
+    // The once-per-group test needs the stop set to be absorbing for the
+    // discrete RK4 map too: a wave with an outgoing ray fast enough to
+    // overshoot U = 0 and be pushed back (U' < -risk_ub: near-radial rays
+    // away from the black hole; none in the default scenes' views) takes the
+    // per-step test, which is exact for any ray.  Falling rays cannot leave
+    // the horizon side (F > 0 there, U keeps rising).
+#if GEO_RISK_TEST
+    const bool absorbing = stop_at.absorbing && ballot_(UB < -k.risk_ub) == 0;
+#else
+    const bool absorbing = stop_at.absorbing;
+#endif
     // per lane: steps before its stopping group (budget: all)
     uint32_t it;
 #if GEO_PINGPONG
-    if (stop_at.absorbing)  // frame-uniform
+    if (absorbing)  // wave-uniform
         it = run_groups_pp<G, KIND, GEO_ABSORBING_TEST != 0>(stop_at, ngroups, ngroups * (uint32_t)G, h, hh, hh2,
                                                              hhh, h6, h2_6, su_, sb_);
     else
         it = run_groups_pp<G, KIND, false>(stop_at, ngroups, ngroups * (uint32_t)G, h, hh, hh2, hhh, h6, h2_6,
                                            su_, sb_);
 #else
-    if (stop_at.absorbing)  // frame-uniform
+    if (absorbing)  // wave-uniform
         it = run_groups<G, KIND, GEO_ABSORBING_TEST != 0>(stop_at, ngroups, ngroups * (uint32_t)G, h, hh, hh2, hhh,
                                                           h6, h2_6, su_, sb_);
     else
         it = run_groups<G, KIND, false>(stop_at, ngroups, ngroups * (uint32_t)G, h, hh, hh2, hhh, h6, h2_6, su_,
                                         sb_);
 #endif
-    return geodesic_finish<G, KIND>(k, stop_at, it, su_, sb_, steps);
+    return geodesic_finish<G, KIND>(k, stop_at, absorbing, it, su_, sb_, steps);
 }
 
 #ifndef GEO_LOOP_VARIANT

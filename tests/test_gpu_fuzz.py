@@ -1,11 +1,13 @@
 """Fuzz parity on the GPU: the HIP kernels (through the C-ABI) equal the
 oracle's f32 restatement bit for bit (mask, UV bits, steps, RGBA) on seeded
 random scenes (tests/fuzz_scenes.py), direct and adaptive, 64x36 each."""
+import os
+
 import numpy as np
 import pytest
 
 import oracle as O
-from fuzz_scenes import random_scene
+from fuzz_scenes import REGRESSION_SEEDS, random_scene
 from test_gpu_parity import geo, make_ctx, render, torch_mod  # noqa: F401  (fixtures)
 
 pytestmark = pytest.mark.gpu
@@ -20,13 +22,16 @@ def test_gpu_fuzz_bitexact(geo, torch_mod, adaptive):  # noqa: F811
     sky = make_sky("equirect", (256, 128))
     ctx = make_ctx(geo, sky)
     bad = []
-    n = 600 if not adaptive else 300
-    for seed in range(n):
-        frame, scene, desc = random_scene(10_000 + seed, W, H, adaptive=adaptive)
+    # GEO_FUZZ_N / GEO_FUZZ_BASE: a longer sweep on other seeds (default: the committed 600 + 300)
+    n = int(os.environ.get("GEO_FUZZ_N", 600 if not adaptive else 300))
+    base = int(os.environ.get("GEO_FUZZ_BASE", 10_000))
+    seeds = [base + i for i in range(n)] + ([] if adaptive else list(REGRESSION_SEEDS))
+    for seed in seeds:
+        frame, scene, desc = random_scene(seed, W, H, adaptive=adaptive)
         hip = render(geo, torch_mod, ctx, frame, scene, W, H)
         ref = O.render_f32(frame, scene, sky, W, H, threads=4)
         same = all(np.array_equal(hip[f], ref[f]) for f in ("mask", "steps", "rgba")) and np.array_equal(
             hip["uv"].view(np.uint32), ref["uv"].view(np.uint32)) and hip["total"] == ref["steps_total"]
         if not same:
             bad.append(desc)
-    assert not bad, f"{len(bad)} of {n} scenes differ: {bad[:5]}"
+    assert not bad, f"{len(bad)} of {len(seeds)} scenes differ: {bad[:5]}"

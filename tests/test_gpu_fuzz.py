@@ -12,7 +12,7 @@ from test_gpu_parity import geo, make_ctx, render, torch_mod  # noqa: F401  (fix
 
 pytestmark = pytest.mark.gpu
 
-W, H = 64, 36
+W, H = int(os.environ.get("GEO_FUZZ_W", 64)), int(os.environ.get("GEO_FUZZ_H", 36))
 
 
 @pytest.mark.parametrize("adaptive", [False, True], ids=["direct", "adaptive"])

@@ -35,3 +35,35 @@ def test_gpu_fuzz_bitexact(geo, torch_mod, adaptive):  # noqa: F811
         if not same:
             bad.append(desc)
     assert not bad, f"{len(bad)} of {len(seeds)} scenes differ: {bad[:5]}"
+
+
+def test_gpu_fuzz_fan_mode_bitexact(geo, torch_mod):  # noqa: F811
+    """Fan mode (the reference's display path) on the fuzz scenes: each
+    scene's 400-node fan solved on the GPU, drawn with the fan lerp, and the
+    oracle's f32 lerp over the same fan: mask, UV bits and RGBA equal."""
+    from schwarzschild_raytracer_wgpu_amd import _lib
+    from schwarzschild_raytracer_wgpu_amd.scenes import make_sky
+
+    torch = torch_mod
+    sky = make_sky("equirect", (256, 128))
+    ctx = make_ctx(geo, sky)
+    dev = torch.device("cuda:0")
+    n = int(os.environ.get("GEO_FUZZ_N", 300))
+    base = int(os.environ.get("GEO_FUZZ_BASE", 10_000))
+    bad = []
+    for seed in range(base, base + n):
+        frame, scene, desc = random_scene(seed, W, H)
+        scene.mode = _lib.GEO_MODE_FAN
+        fan = ctx.solve_ray_fan(scene.sphere_r, scene.rs, 1000, scene.step, 400, scene.r_obs)
+        rgba = torch.empty(W * H * 4, dtype=torch.uint8, device=dev)
+        mask = torch.empty(W * H, dtype=torch.uint8, device=dev)
+        uv = torch.empty(W * H * 2, dtype=torch.float32, device=dev)
+        ctx.render_rows(frame, scene, W, H, 0, H, rgba, mask, uv)
+        torch.cuda.synchronize()
+        ref = O.render_f32(frame, scene, sky, W, H, fan=fan, threads=4)
+        same = (np.array_equal(mask.cpu().numpy().reshape(H, W), ref["mask"])
+                and np.array_equal(rgba.cpu().numpy().reshape(H, W, 4), ref["rgba"])
+                and np.array_equal(uv.cpu().numpy().reshape(H, W, 2).view(np.uint32), ref["uv"].view(np.uint32)))
+        if not same:
+            bad.append(desc)
+    assert not bad, f"{len(bad)} of {n} scenes differ: {bad[:5]}"

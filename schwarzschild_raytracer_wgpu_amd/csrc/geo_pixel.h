@@ -514,9 +514,7 @@ GEO_HD uint32_t run_groups_pp(const StopTest<KIND>& stop_at, uint32_t ngroups, u
     }
     // Groups q = 0, 2, 4, ... are A groups, 1, 3, ... B groups.  A lane that
     // stops in group q records it = q G (a multiple of G below `all`), so the
-    // set its states sit in is (it / G) & 1 after the loop: the loop carries
-    // one lane flag (`done`), which keeps the lane-mask merges at its joins
-    // to a minimum.
+    // set its states sit in is (it / G) & 1 after the loop.
 #if GEO_LIVE_EXEC
     // The lanes still integrating are the wave-uniform mask `live`, which is
     // also the exec mask of the group steps: no per-lane flag, so the loop's
@@ -529,9 +527,9 @@ GEO_HD uint32_t run_groups_pp(const StopTest<KIND>& stop_at, uint32_t ngroups, u
     // One exit test per A+B pair of groups: a group whose lanes are all done
     // runs with an empty exec mask, which the masked region's execz branch
     // skips, so the pair needs no test between its groups; an odd budget's
-    // last group is an A group after the loop.
-    // one exit edge (hipcc's structurizer turns a second one into lane-mask
-    // flags at the latch): an empty `live` zeroes the pair counter instead
+    // last group is an A group after the loop.  The loop has one exit edge
+    // (hipcc's structurizer turns a second one into lane-mask flags at the
+    // latch): an empty `live` zeroes the pair counter instead of breaking.
     uint32_t rem = ngroups >> 1;
     while (rem != 0) {
         if (in_ballot_(live)) group_steps_<G, KIND>(xu, xb, h, hh, hh2, hhh, h6, h2_6, au, ab);
@@ -631,6 +629,8 @@ GEO_HD uint32_t run_groups_pp(const StopTest<KIND>& stop_at, uint32_t ngroups, u
     }
 #endif
 #else
+    // the loop carries one lane flag (`done`), which keeps the lane-mask
+    // merges at its joins to a minimum
     bool done = false;
     uint64_t live = ballot_(true);  // wave-uniform: the lanes still integrating
     uint32_t it = all;

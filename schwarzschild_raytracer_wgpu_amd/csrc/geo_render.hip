@@ -37,18 +37,32 @@
 #ifndef GEO_BH_SKIP_UV
 #define GEO_BH_SKIP_UV 1
 #endif
-// rows of a workgroup's 8-wide tile (a multiple of 8): 8, 16 and 32 time the
-// same, 64 and 128 are 1.3 % and 4.5 % slower
+// A workgroup's tile: GEO_TILE_WAVES_X 8x8 waves side by side, GEO_TILE_H
+// rows (a multiple of 8).  32 x 8 (4 waves abreast): a tile row spans 32 sky
+// texels = one 128-B line, so neighbouring waves share their sky lines in one
+// CU instead of fetching them on up to 4 XCDs' L2s (102.8 -> 59.5 MB of L2
+// fabric reads per 4K frame, config 3 -2 to -5 %, config 5 -2 %, config 2
+// -1.5 % against 8 x 32; 16 x 16, 64 x 8 and 32 x 16 in between)
 #ifndef GEO_TILE_H
-#define GEO_TILE_H 32
+#define GEO_TILE_H 8
+#endif
+#ifndef GEO_TILE_WAVES_X
+#define GEO_TILE_WAVES_X 4
+#endif
+// consecutive tiles per XCD run (xcd_tile; 0 or 1: the hardware's round-robin)
+#ifndef GEO_XCD_CHUNK
+#define GEO_XCD_CHUNK 1
 #endif
 
 namespace {
 
-constexpr int kTileW = 8;   // a wave64 covers an 8x8 pixel square (fewest divergent
-constexpr int kTileH = GEO_TILE_H;  // steps per wave; tools/ubench/loop_ab.hip), a block 8 x kTileH
-constexpr int kBlock = kTileW * kTileH;  // 256 threads = 4 waves
-constexpr int kWaveRows = 64 / kTileW;   // rows covered by one wave
+constexpr int kWaveRows = 8;  // a wave64 covers an 8x8 pixel square (fewest divergent
+                              // steps per wave; tools/ubench/loop_ab.hip)
+constexpr int kWavesX = GEO_TILE_WAVES_X;  // waves side by side in a tile
+constexpr int kTileW = 8 * kWavesX;
+constexpr int kTileH = GEO_TILE_H;  // a block kTileW x kTileH
+constexpr int kBlock = kTileW * kTileH;  // 256 threads = 4 waves (32 x 8)
+static_assert(kTileH % kWaveRows == 0 && kBlock % 64 == 0, "tile of whole 8x8 waves");
 constexpr uint32_t kMaxFan = 4096;       // LDS fan capacity (16 KiB)
 constexpr int kStepSlots = 256;          // sharded step counters (one per 128-B line)
 constexpr int kSlotStride = 16;          // u64 per slot = 128 B (own cache line)
@@ -143,6 +157,30 @@ __device__ __forceinline__ void shade_pixel(const RenderArgs& a, float c2x, floa
     if (a.out_steps) a.out_steps[o] = steps;
 }
 
+// Workgroups are dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md,
+// "blocks b and b + 8 share one"), each with its own L2.  The remap hands
+// each XCD runs of GEO_XCD_CHUNK consecutive tiles (chunk c to the XCD of
+// c % 8), so neighbouring tiles share an L2's sky lines; every XCD still gets
+// every 8th chunk of the frame.  Off by default: with 8 x 32 tiles, chunks of
+// 4-16 cut the fabric reads as the 32 x 8 tile does but timed -1 % on config
+// 3 and +2-4 % on config 2; on 32 x 8 tiles chunks of 4 are slower on every
+// config.  Bijective: the first n - n % (8 * chunk)
+// workgroups are permuted among themselves, the rest keep their own tile.
+// Placement only changes speed.
+template <uint32_t kC>
+__device__ __forceinline__ uint2 xcd_tile() {
+    if constexpr (kC <= 1) return make_uint2(blockIdx.x, blockIdx.y);
+    constexpr uint32_t kSpan = 8u * kC;
+    const uint32_t gx = gridDim.x, n = gx * gridDim.y;
+    const uint32_t l = blockIdx.y * gx + blockIdx.x;
+    uint32_t t = l;
+    if (l < n - n % kSpan) {
+        const uint32_t q = l / 8u;
+        t = ((q / kC) * 8u + l % 8u) * kC + q % kC;
+    }
+    return make_uint2(t % gx, t / gx);
+}
+
 template <int MODE, int KIND>
 __global__ __launch_bounds__(kBlock) void geo_render_kernel(const RenderArgs a) {
 #if GEO_FAN_LDS
@@ -152,13 +190,15 @@ __global__ __launch_bounds__(kBlock) void geo_render_kernel(const RenderArgs a) 
         __syncthreads();
     }
 #endif
-    const uint32_t px = blockIdx.x * kTileW + (threadIdx.x % kTileW);
-    const uint32_t ly = blockIdx.y * kTileH + (threadIdx.x / kTileW);
+    const uint2 tile = xcd_tile<GEO_XCD_CHUNK>();
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x) >> 6;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t px = tile.x * kTileW + (wave % kWavesX) * 8u + lane % 8u;
     // local row -> frame row.  band_rows is a multiple of 8 (checked on the
     // host): each 8-row wave lies in one band and the mapping is wave-uniform
     // (scalar ops; the band index by a multiply-high, band_rows_magic).
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x) >> 6;
-    const uint32_t wl0 = blockIdx.y * kTileH + wave * kWaveRows;
+    const uint32_t wl0 = tile.y * kTileH + (wave / kWavesX) * kWaveRows;
+    const uint32_t ly = wl0 + lane / 8u;
     const uint32_t band = __umulhi(wl0, a.band_magic);
     const uint32_t py = a.row0 + band * a.band_stride + (wl0 - band * a.band_rows) + (ly - wl0);
     uint32_t steps = 0;
@@ -190,7 +230,7 @@ __global__ __launch_bounds__(kBlock) void geo_render_kernel(const RenderArgs a) 
             // slots.  No block barrier, so a wave that finishes early frees
             // its slot at once.
             const uint32_t total = wave_sum_u32(steps);
-            const uint32_t slot = (blockIdx.x * (kBlock / 64) + wave) % kStepSlots;
+            const uint32_t slot = (tile.x * (kBlock / 64) + wave) % kStepSlots;
             if ((threadIdx.x & 63) == 0 && total)
                 atomicAdd(&a.step_slots[slot * kSlotStride], (unsigned long long)total);
         }

@@ -10,7 +10,7 @@ ROOT=$(pwd); TAG=${1:-r02}
 mkdir -p gpurun_out
 SETS=("GRBM_GUI_ACTIVE SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_VALU"
       "SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_FMA_F32 SQ_THREAD_CYCLES_VALU SQ_INSTS_VALU_FLOPS_FP32"
-      "FETCH_SIZE" "WRITE_SIZE")
+      "FETCH_SIZE" "WRITE_SIZE" "TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum")
 CONFIG=cfg3_4k bash tools/gpu_pmc.sh pmc3_$TAG "${SETS[@]}" || exit $?
 CONFIG=cfg5_8k_adaptive bash tools/gpu_pmc.sh pmc5_$TAG "${SETS[@]}" || exit $?
 python tools/pmc_to_profile.py pmc3_$TAG gpurun_out/${TAG}_cfg3_4k_pmc.json "cfg3_4k (3840x2160, 2048 steps, direct)" || exit 1

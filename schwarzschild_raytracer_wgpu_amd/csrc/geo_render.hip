@@ -8,8 +8,9 @@
 //                            (sphere_ray_tracer.rs:35-193)
 //   geo_steps_finalize       folds the sharded step counters into the caller's u64
 //
-// Work decomposition: one 256-thread workgroup per 8x32 pixel tile, each
-// wave64 an 8x8 square (compact 2-D footprint = coherent step counts);
+// Work decomposition: one 256-thread workgroup per 32x8 pixel tile, each
+// wave64 an 8x8 square (compact 2-D footprint = coherent step counts), the
+// four side by side (a tile row spans one 128-B sky line);
 // the frame uniform rides in the kernarg segment (SGPRs, wave-uniform), the
 // ray fan (fan mode) is read from its cache-resident device copy; per-lane
 // ray state lives in VGPRs.  The hot loop

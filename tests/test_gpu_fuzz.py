@@ -34,6 +34,7 @@ def test_gpu_fuzz_bitexact(geo, torch_mod, adaptive):  # noqa: F811
             hip["uv"].view(np.uint32), ref["uv"].view(np.uint32)) and hip["total"] == ref["steps_total"]
         if not same:
             bad.append(desc)
+    print(f"fuzz {'adaptive' if adaptive else 'direct'}: {len(seeds)} scenes at {W}x{H}, {len(bad)} differ")
     assert not bad, f"{len(bad)} of {len(seeds)} scenes differ: {bad[:5]}"
 
 
@@ -66,4 +67,5 @@ def test_gpu_fuzz_fan_mode_bitexact(geo, torch_mod):  # noqa: F811
                 and np.array_equal(uv.cpu().numpy().reshape(H, W, 2).view(np.uint32), ref["uv"].view(np.uint32)))
         if not same:
             bad.append(desc)
+    print(f"fuzz fan: {n} scenes at {W}x{H}, {len(bad)} differ")
     assert not bad, f"{len(bad)} of {n} scenes differ: {bad[:5]}"

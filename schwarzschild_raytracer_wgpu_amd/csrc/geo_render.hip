@@ -9,8 +9,8 @@
 //   geo_steps_finalize       folds the sharded step counters into the caller's u64
 //
 // Work decomposition: one 256-thread workgroup per 32x8 pixel tile, each
-// wave64 an 8x8 square (compact 2-D footprint = coherent step counts), the
-// four side by side (a tile row spans one 128-B sky line);
+// wave64 a 16x4 block (compact 2-D footprint = coherent step counts), 2 x 2
+// of them (a tile row spans one 128-B sky line);
 // the frame uniform rides in the kernarg segment (SGPRs, wave-uniform), the
 // ray fan (fan mode) is read from its cache-resident device copy; per-lane
 // ray state lives in VGPRs.  The hot loop
@@ -38,8 +38,8 @@
 #ifndef GEO_BH_SKIP_UV
 #define GEO_BH_SKIP_UV 1
 #endif
-// A workgroup's tile: GEO_TILE_WAVES_X 8x8 waves side by side, GEO_TILE_H
-// rows (a multiple of 8).  32 x 8 (4 waves abreast): a tile row spans 32 sky
+// A workgroup's tile: GEO_TILE_WAVES_X waves side by side, GEO_TILE_H rows
+// (a multiple of a wave's rows).  32 x 8: a tile row spans 32 sky
 // texels = one 128-B line, so neighbouring waves share their sky lines in one
 // CU instead of fetching them on up to 4 XCDs' L2s (102.8 -> 59.5 MB of L2
 // fabric reads per 4K frame, config 3 -2 to -5 %, config 5 -2 %, config 2
@@ -48,7 +48,13 @@
 #define GEO_TILE_H 8
 #endif
 #ifndef GEO_TILE_WAVES_X
-#define GEO_TILE_WAVES_X 4
+#define GEO_TILE_WAVES_X 2
+#endif
+// pixels across one wave, 64 / GEO_WAVE_W rows: 16 x 4 in the 32 x 8 tile
+// (-0.5 % on config 3 against four 8 x 8 squares, configs 5 and 2 the same;
+// 32 x 2 is +2.5 %)
+#ifndef GEO_WAVE_W
+#define GEO_WAVE_W 16
 #endif
 // consecutive tiles per XCD run (xcd_tile; 0 or 1: the hardware's round-robin)
 #ifndef GEO_XCD_CHUNK
@@ -57,13 +63,17 @@
 
 namespace {
 
-constexpr int kWaveRows = 8;  // a wave64 covers an 8x8 pixel square (fewest divergent
-                              // steps per wave; tools/ubench/loop_ab.hip)
+constexpr int kWaveW = GEO_WAVE_W;      // a wave64 covers a compact 16x4 block (few divergent
+constexpr int kWaveRows = 64 / kWaveW;  // steps per wave; tools/ubench/loop_ab.hip)
 constexpr int kWavesX = GEO_TILE_WAVES_X;  // waves side by side in a tile
-constexpr int kTileW = 8 * kWavesX;
+constexpr int kTileW = kWaveW * kWavesX;
 constexpr int kTileH = GEO_TILE_H;  // a block kTileW x kTileH
-constexpr int kBlock = kTileW * kTileH;  // 256 threads = 4 waves (32 x 8)
-static_assert(kTileH % kWaveRows == 0 && kBlock % 64 == 0, "tile of whole 8x8 waves");
+constexpr int kBlock = kTileW * kTileH;  // 256 threads = 4 waves (32 x 8, 2 x 2 waves of 16 x 4)
+static_assert(kTileH % kWaveRows == 0 && kBlock % 64 == 0, "tile of whole waves");
+// band heights are multiples of 8 (the C-ABI's contract, geo.h), so a wave's
+// rows never straddle a band for any wave shape up to 8 rows
+constexpr uint32_t kBandRowAlign = 8;
+static_assert(kBandRowAlign % kWaveRows == 0, "a wave's rows lie in one band");
 constexpr uint32_t kMaxFan = 4096;       // LDS fan capacity (16 KiB)
 constexpr int kStepSlots = 256;          // sharded step counters (one per 128-B line)
 constexpr int kSlotStride = 16;          // u64 per slot = 128 B (own cache line)
@@ -194,12 +204,12 @@ __global__ __launch_bounds__(kBlock) void geo_render_kernel(const RenderArgs a) 
     const uint2 tile = xcd_tile<GEO_XCD_CHUNK>();
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x) >> 6;
     const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t px = tile.x * kTileW + (wave % kWavesX) * 8u + lane % 8u;
+    const uint32_t px = tile.x * kTileW + (wave % kWavesX) * kWaveW + lane % kWaveW;
     // local row -> frame row.  band_rows is a multiple of 8 (checked on the
     // host): each 8-row wave lies in one band and the mapping is wave-uniform
     // (scalar ops; the band index by a multiply-high, band_rows_magic).
     const uint32_t wl0 = tile.y * kTileH + (wave / kWavesX) * kWaveRows;
-    const uint32_t ly = wl0 + lane / 8u;
+    const uint32_t ly = wl0 + lane / kWaveW;
     const uint32_t band = __umulhi(wl0, a.band_magic);
     const uint32_t py = a.row0 + band * a.band_stride + (wl0 - band * a.band_rows) + (ly - wl0);
     uint32_t steps = 0;
@@ -1032,7 +1042,7 @@ int geo_render_bands(geo_ctx* c, const geo_frame* frame, const geo_scene* scene,
                      uint32_t nbands, uint8_t* out_rgba8, uint8_t* out_mask, float* out_uv,
                      uint32_t* out_steps, unsigned long long* steps_total, void* stream) {
     if (!c || !frame || !scene || !out_rgba8 || width == 0 || height == 0 || band_rows == 0 ||
-        nbands == 0 || band_step == 0 || band_rows < (uint32_t)kWaveRows || (band_rows & (band_rows - 1)) != 0)
+        nbands == 0 || band_step == 0 || band_rows < kBandRowAlign || (band_rows & (band_rows - 1)) != 0)
         return GEO_EINVAL;
     if (width > (1u << 20) || height > (1u << 20)) return GEO_EINVAL;
     const uint64_t first = (uint64_t)band0 * band_rows;
@@ -1050,7 +1060,7 @@ int geo_render_band_set(geo_ctx* c, const geo_frame* frame, const geo_scene* sce
                         unsigned long long* steps_total, void* stream) {
     // band_rows: a multiple of 8, at most 4096 unless a power of two (band_rows_magic)
     if (!c || !frame || !scene || !out_rgba8 || width == 0 || height == 0 || band_rows == 0 || nbands == 0 ||
-        row_stride < band_rows || band_rows % (uint32_t)kWaveRows != 0 ||
+        row_stride < band_rows || band_rows % kBandRowAlign != 0 ||
         ((band_rows & (band_rows - 1)) != 0 && band_rows > 4096u))
         return GEO_EINVAL;
     if (width > (1u << 20) || height > (1u << 20)) return GEO_EINVAL;

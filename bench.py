@@ -76,11 +76,13 @@ def parse():
     p.add_argument("--cpu-threads", type=int, default=16)
     p.add_argument("--cpu-row-step", type=int, default=None,
                    help="CPU baseline sample: every k-th row (default 1 up to 4K, 4 above)")
-    p.add_argument("--cpu-seconds", type=float, default=1.0)
     p.add_argument("--mode", default=None, choices=["direct", "fan", "adaptive"],
                    help="default: the config's mode (cfg1-4 direct, cfg5_8k_adaptive adaptive)")
-    p.add_argument("--check-frame", action="store_true",
-                   help="rank 0 checks the assembled frame against a single-launch full frame")
+    p.add_argument("--no-frame-check", action="store_true",
+                   help="skip rank 0's check, after the timed region, that every frame of the timed run's last "
+                        "batch (the frames as assembled for present) equals a single-launch render of the frame; "
+                        "by default it runs and a mismatch exits non-zero")
+    p.add_argument("--check-frame", action="store_true", help=argparse.SUPPRESS)  # the default since round 3
     p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                    help="nccl (= RCCL over xGMI); gloo stages the gather through host memory (tests only)")
     return p.parse_args()
@@ -318,17 +320,34 @@ def main():
     elapsed_max, kernel_ms_max, compute_max = float(stats[0]), float(stats[1]), float(stats[2])
     total_steps, total_pixels, evals_all = (int(x) for x in tot.tolist())
 
-    if args.check_frame and rank == 0:
+    # rank 0, outside the timed region: the frames of the timed run's last
+    # batch, as assembled for present from every rank's bands (RCCL gather +
+    # geo_assemble_lead at N > 1), against a single-launch render of the frame
+    frame_check = None
+    if not args.no_frame_check and rank == 0:
         ref = torch.empty(H * W * 4, dtype=torch.uint8, device=dev)
         ctx.render_rows(frame, scene, W, H, 0, H, ref)
         torch.cuda.synchronize()
-        if not torch.equal(sf.frame_rgba(), ref):
-            raise SystemExit("assembled frame differs from the single-launch frame")
-        print(f"check-frame: assembled {W}x{H} frame from {world} rank(s) equals the single-launch frame",
-              file=sys.stderr)
+        nbatch = sf.last[2] + 1
+        same = [bool(torch.equal(sf.frame_rgba(k), ref)) for k in range(nbatch)] if world > 1 else [
+            bool(torch.equal(sf.frame_rgba(), ref))]
+        frame_check = {"ok": all(same), "frames": len(same), "ranks": world,
+                       "what": "rank 0's assembled frames of the timed run's last batch == a single-launch "
+                               "geo_render_rows of the whole frame (byte-exact RGBA)"}
+        print(f"frame-check: {sum(same)} of {len(same)} assembled {W}x{H} frame(s) from {world} rank(s) equal "
+              f"the single-launch frame", file=sys.stderr)
 
+    if world > 1:
+        # every rank exits with rank 0's verdict (a peer left running would hang the launcher)
+        ok = torch.tensor([0 if frame_check is not None and not frame_check["ok"] else 1], device=rdev)
+        dist.broadcast(ok, src=0)
+        frame_ok = bool(ok.item())
+    else:
+        frame_ok = frame_check is None or frame_check["ok"]
     if rank != 0:
         dist.destroy_process_group()
+        if not frame_ok:
+            raise SystemExit(1)
         return
 
     value = total_steps / elapsed_max
@@ -402,9 +421,12 @@ def main():
     if world == 1 and not args.no_cpu_baseline and mode != g.GEO_MODE_FAN:
         out["cpu_baseline"] = cpu_baseline(frame, scene, sky, W, H, args)
         out["reference_equivalent"] = reference_fan_cost(ctx, cfg, obs.get_radial_position())
+    out["frame_check"] = frame_check
     print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    if not frame_ok:
+        raise SystemExit("frame check failed: an assembled frame differs from the single-launch frame")
 
 
 def spin_up(sf, n):
@@ -526,35 +548,67 @@ def reference_fan_cost(ctx, cfg, r):
                     "device_fans: the three fans into their contexts on three streams, one sync per frame"}
 
 
-def cpu_baseline(frame, scene, sky, W, H, args):
-    """The oracle's scalar f32 restatement of the same per-pixel integrator
-    (oracle/geo_oracle.c: pthreads over rows, one pixel per thread-iteration),
-    on whole frames of the same workload until >= --cpu-seconds of wall time."""
-    import oracle as O
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
 
+    return platform.processor() or "unknown"
+
+
+def cpu_baseline(frame, scene, sky, W, H, args):
+    """The same per-pixel integrator on the host cores: geo_render_cpu
+    (libgeo_cpu.so, include/geo/geo_cpu.h), the product's geo_pixel.h built
+    for the host (g++ -O2 -ffp-contract=off), scalar, std::thread row blocks
+    (BASELINE.md §3).  One warm-up, then the median of 3 runs of the frame
+    (every 4th row above 4K)."""
+    import ctypes
+    import statistics
+
+    import numpy as np
+
+    lib = ctypes.CDLL(os.path.join(ROOT, "schwarzschild_raytracer_wgpu_amd", "libgeo_cpu.so"))
+    vp, u32 = ctypes.c_void_p, ctypes.c_uint32
+    lib.geo_render_cpu.restype = ctypes.c_int
+    lib.geo_render_cpu.argtypes = [vp, vp, vp, u32, u32, vp, u32, u32, u32, u32, u32, u32, ctypes.c_int, vp, vp, vp,
+                                   vp, vp]
     threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
     k = args.cpu_row_step or (1 if W * H <= 3840 * 2160 else 4)
     nrows = (H + k - 1) // k
-    steps = 0
-    frames = 0
-    t0 = time.perf_counter()
-    while True:
-        r = O.render_f32(frame, scene, sky, W, H, row0=0, nrows=nrows, row_step=k, threads=threads,
-                         want_uv=False, want_steps=False)
-        steps += r["steps_total"]
-        frames += 1
+    sky = np.ascontiguousarray(sky, dtype=np.uint8)
+    rgba = np.empty((nrows, W, 4), np.uint8)
+    total = ctypes.c_ulonglong()
+    times, steps = [], None
+    for rep in range(4):
+        t0 = time.perf_counter()
+        rc = lib.geo_render_cpu(ctypes.addressof(frame), ctypes.addressof(scene), sky.ctypes.data, sky.shape[1],
+                                sky.shape[0], None, 0, W, H, 0, nrows, k, threads, rgba.ctypes.data, None, None,
+                                None, ctypes.addressof(total))
         dt = time.perf_counter() - t0
-        if dt >= args.cpu_seconds:
-            break
+        if rc != 0:
+            raise SystemExit(f"geo_render_cpu: {rc}")
+        if rep > 0:  # rep 0 warms up
+            times.append(dt)
+        steps = total.value
+    med = statistics.median(times)
     what = "full" if k == 1 else f"every {k}th row of the"
     return {
-        "value": steps / dt,
+        "value": steps / med,
         "unit": "geodesic-step-attempts·pixels/s" if scene.mode == 2 else "geodesic-steps·pixels/s",
         "cores": threads,
         "kind": "port",
-        "sample": f"{frames} x {what} {W}x{H} frame ({nrows * W} pixels, {steps // frames} steps each) "
-                  f"in {dt:.2f} s wall on {threads} threads",
-        "seconds": dt,
+        "cpu_model": cpu_model(),
+        "sample": f"{what} {W}x{H} frame ({nrows * W} pixels, {steps} steps): median of 3 runs after one warm-up, "
+                  f"{threads} threads",
+        "seconds_per_run": times,
+        "implementation": "geo_render_cpu (libgeo_cpu.so): geo_pixel.h compiled for the host, g++ -O2 "
+                          "-ffp-contract=off -mfma -msse4.1, scalar, std::thread row blocks; output bit-identical "
+                          "to the kernel's (tests/test_cpu_baseline.py)",
     }
 
 

@@ -69,7 +69,7 @@ def _load() -> ctypes.CDLL:
         "geo_oracle_solve_ray_fan_f64": (None, [f64, f64, u32, f64, u32, f64, vp]),
         "geo_oracle_geodesic_at_theta_f64": (f64, [f64, f64, u32, f64, f64, f64, vp]),
         "geo_oracle_pixel_f64": (None, [vp, vp, vp, u32, u32, u32, u32, u32, vp]),
-        "geo_oracle_render_f64": (i, [vp, vp, vp, u32, u32, u32, u32, u32, i, vp, vp, vp, vp]),
+        "geo_oracle_render_f64": (i, [vp, vp, vp, u32, u32, u32, u32, u32, u32, i, vp, vp, vp, vp, vp]),
         "geo_oracle_render_f32": (i, [vp, vp, vp, u32, vp, u32, u32, u32, u32, u32, u32, u32, i, vp, vp, vp,
                                       vp, vp]),
         "geo_oracle_observer_frame": (None, [f64, f64, f64, f64, vp, f64, f64, i, f64, vp]),
@@ -159,19 +159,24 @@ def pixel_f64(frame, scene, width, height, px, py, fan=None) -> OraclePx:
     return out
 
 
-def render_f64(frame, scene, width, height, row0=0, nrows=None, fan=None, threads=8):
-    nrows = height - row0 if nrows is None else nrows
+def render_f64(frame, scene, width, height, row0=0, nrows=None, fan=None, threads=8, row_step=1):
+    """The f64 literal restatement on rows row0, row0 + row_step, ... (nrows of
+    them): mask, uv, steps, lam (traveled-angle result lambda') and theta
+    (the pixel's angle to the black hole) per pixel."""
+    nrows = (height - row0 + row_step - 1) // row_step if nrows is None else nrows
     fr, sc = as_frame(frame), as_scene(scene)
     fan_a = None if fan is None else np.ascontiguousarray(fan, dtype=np.float32)
     mask = np.empty((nrows, width), np.uint8)
     uv = np.empty((nrows, width, 2), np.float32)
     steps = np.empty((nrows, width), np.uint32)
     lam = np.empty((nrows, width), np.float64)
+    theta = np.empty((nrows, width), np.float64)
     rc = lib.geo_oracle_render_f64(_addr(fr), _addr(sc), _np(fan_a), 0 if fan_a is None else fan_a.size, width,
-                                   height, row0, nrows, threads, _np(mask), _np(uv), _np(steps), _np(lam))
+                                   height, row0, nrows, row_step, threads, _np(mask), _np(uv), _np(steps), _np(lam),
+                                   _np(theta))
     if rc != 0:
         raise ValueError(f"geo_oracle_render_f64: {rc}")
-    return dict(mask=mask, uv=uv, steps=steps, lam=lam)
+    return dict(mask=mask, uv=uv, steps=steps, lam=lam, theta=theta)
 
 
 def render_f32(frame, scene, sky, width, height, row0=0, nrows=None, row_step=1, fan=None, threads=8,

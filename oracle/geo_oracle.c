@@ -300,6 +300,7 @@ typedef struct {
     float hh, h6, hh2, hhh, h2_6, r3_2, sphere_u, schwarz_u, u0, h_over_r2, inv_r2, bound, e_out, e_in, barrier;
     int r_inside_h, outside, sphere_outside, inside_sphere, diff_sides, rs_nonzero;
     float scale, U0, SU, BD, HU; /* scaled state U = scale*u */
+    float ubk;                   /* scale * (E/r) outside the horizon: UB0 = ubk |st|/ct */
     float tolU, tolG, hmax;      /* GEO_MODE_ADAPTIVE step control */
 } fconsts;
 
@@ -326,7 +327,7 @@ static fconsts make_fconsts(const geo_scene* s) {
     k.bound = 0.9f * (k.u0 < um ? k.u0 : um);
     k.e_out = sqrtf(1.0f - k.rs / k.r);
     k.e_in = sqrtf(-1.0f + k.rs / k.r);
-    k.barrier = 4.0f / (27.0f * k.rs * k.rs);
+        k.barrier = 4.0f / (27.0f * k.rs * k.rs);
     k.r_inside_h = k.r < k.rs;
     k.outside = k.r > k.rs;
     k.sphere_outside = k.sphere_r > k.rs;
@@ -338,6 +339,7 @@ static fconsts make_fconsts(const geo_scene* s) {
     k.SU = k.scale * k.sphere_u;
     k.BD = k.scale * k.bound;
     k.HU = k.scale * k.schwarz_u;
+    k.ubk = k.scale * (k.e_out * k.u0);
     k.tolU = k.scale * (s->tol > 0.0f ? s->tol : GEO_ADAPTIVE_DEFAULT_TOL);
     k.tolG = k.tolU * (1.0f / 64.0f);
     k.hmax = k.step * (float)GEO_ADAPTIVE_MAX_GROWTH;
@@ -489,12 +491,25 @@ static float geodesic_f32(const fconsts* k, float st, float ct, float rct, int a
         (barrier && k->diff_sides) || (k->r < k->r3_2 && k->inside_sphere && falling) ||
         (k->r > k->r3_2 && !k->inside_sphere && !falling))
         return 15.0f;
-    float ub = sqrtf(maxz(0.0f, inv_b2 - k->h_over_r2));
-    if (!falling) ub = -ub;
-    /* loop test (:134-135) for the initial state, in the reference's variables */
-    if ((k->rs_nonzero && k->u0 > k->schwarz_u && ub > 0.0f) || k->max_steps == 0u || !(k->u0 > 0.0f)) return 15.0f;
+    /* u'0 = sqrt(1/b^2 - (1 - rs/r)/r^2) (:123), scaled: UB = c u'0.  Outside
+     * the horizon E^2 = 1 - rs/r, so the radicand is (E/r)^2 (1/ct^2 - 1) =
+     * (E/r)^2 tan^2 theta and UB = (c E/r) |st|/ct: well conditioned where the
+     * literal difference cancels (|theta| << 1, a tangential ray: up to 4e-4
+     * rad of traveled angle in f32).  Inside the horizon both terms of the
+     * radicand are positive and the literal form is kept. */
+    float UB;
+    if (k->r_inside_h) {
+        float ub = sqrtf(maxz(0.0f, inv_b2 - k->h_over_r2));
+        if (!falling) ub = -ub;
+        UB = k->scale * ub;
+    } else {
+        UB = (k->ubk * fabsf(st)) * rct;
+        if (!falling) UB = -UB;
+    }
+    /* loop test (:134-135) for the initial state (u' > 0 <=> UB > 0) */
+    if ((k->rs_nonzero && k->u0 > k->schwarz_u && UB > 0.0f) || k->max_steps == 0u || !(k->u0 > 0.0f)) return 15.0f;
     int flat = !k->rs_nonzero;
-    float U = k->U0, UB = k->scale * ub;
+    float U = k->U0;
     if (adaptive) return adaptive_f32(k, U, UB, flat, steps);
     uint32_t it = 0;
     for (;;) { /* :134-191, one step per iteration */
@@ -695,6 +710,7 @@ typedef struct {
     float* uv;
     uint32_t* steps;
     double* lam;
+    double* theta;
     uint64_t total;
 } job_t;
 
@@ -728,7 +744,7 @@ static void* job_f32(void* arg) {
 static void* job_f64(void* arg) {
     job_t* j = (job_t*)arg;
     for (uint32_t r = (uint32_t)j->tid; r < j->nrows; r += (uint32_t)j->threads) {
-        uint32_t py = j->row0 + r;
+        uint32_t py = j->row0 + r * j->row_step;
         for (uint32_t px = 0; px < j->width; ++px) {
             size_t o = (size_t)r * j->width + px;
             geo_oracle_px p;
@@ -740,6 +756,7 @@ static void* job_f64(void* arg) {
             }
             if (j->steps) j->steps[o] = p.steps;
             if (j->lam) j->lam[o] = p.lam;
+            if (j->theta) j->theta[o] = p.theta;
         }
     }
     return NULL;
@@ -818,9 +835,10 @@ int geo_oracle_render_f32(const geo_frame* f, const geo_scene* s, const float* f
 }
 
 int geo_oracle_render_f64(const geo_frame* f, const geo_scene* s, const float* fan, uint32_t n_fan,
-                          uint32_t width, uint32_t height, uint32_t row0, uint32_t nrows,
-                          int threads, uint8_t* mask, float* uv, uint32_t* steps, double* lam) {
-    if (!f || !s || width == 0 || height == 0 || (uint64_t)row0 + nrows > height) return -1;
+                          uint32_t width, uint32_t height, uint32_t row0, uint32_t nrows, uint32_t row_step,
+                          int threads, uint8_t* mask, float* uv, uint32_t* steps, double* lam, double* theta) {
+    if (!f || !s || width == 0 || height == 0 || row_step == 0) return -1;
+    if ((uint64_t)row0 + (uint64_t)(nrows ? nrows - 1 : 0) * row_step >= height) return -1;
     if (s->mode == GEO_MODE_FAN && (!fan || n_fan < 2)) return -1;
     job_t j;
     memset(&j, 0, sizeof(j));
@@ -832,10 +850,12 @@ int geo_oracle_render_f64(const geo_frame* f, const geo_scene* s, const float* f
     j.height = height;
     j.row0 = row0;
     j.nrows = nrows;
+    j.row_step = row_step;
     j.mask = mask;
     j.uv = uv;
     j.steps = steps;
     j.lam = lam;
+    j.theta = theta;
     return run_jobs(&j, threads, job_f64, NULL);
 }
 

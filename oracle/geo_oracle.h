@@ -61,9 +61,12 @@ double geo_oracle_geodesic_at_theta_f64(double sphere_r, double schwarz_r, uint3
 void geo_oracle_pixel_f64(const geo_frame* f, const geo_scene* s, const float* fan, uint32_t n_fan,
                           uint32_t width, uint32_t height, uint32_t px, uint32_t py,
                           geo_oracle_px* out);
+/* rows row0, row0 + row_step, ... (nrows of them); any output may be NULL.
+ * theta: the pixel's angle to the black hole (the solve_ray_fan node angle
+ * it stands for). */
 int geo_oracle_render_f64(const geo_frame* f, const geo_scene* s, const float* fan, uint32_t n_fan,
-                          uint32_t width, uint32_t height, uint32_t row0, uint32_t nrows,
-                          int threads, uint8_t* mask, float* uv, uint32_t* steps, double* lam);
+                          uint32_t width, uint32_t height, uint32_t row0, uint32_t nrows, uint32_t row_step,
+                          int threads, uint8_t* mask, float* uv, uint32_t* steps, double* lam, double* theta);
 
 /* f32 kernel mirror.  rgba/mask/uv/steps may be NULL (except rgba). */
 int geo_oracle_render_f32(const geo_frame* f, const geo_scene* s, const float* fan, uint32_t n_fan,

@@ -60,35 +60,19 @@ GEO_HD float fmaf_(float a, float b, float c) { return __builtin_fmaf(a, b, c); 
 #endif
 
 // Correctly rounded sqrt, equal to __builtin_sqrtf for every input.  On the
-// device, hipcc's correctly rounded sequence wraps the ±1-ulp correction of
+// device, hipcc's correctly rounded sequence wraps the +-1-ulp correction of
 // v_sqrt_f32 in a 2^32 pre-scale for x < 2^-96 and a class fix-up for
-// ±0/+inf (≈ 17 VALU).  For x >= 2^-96 (finite or +inf) the scale is not
-// applied and the fix-up returns the corrected value, so the correction alone
-// gives the same bits (9 VALU).  Cheaper still (GEO_SQRT_RSQ, the default):
-// s = x rsq(x) corrected once by its residual, s + (x - s^2) rsq(x)/2, which
-// is correctly rounded for every finite x >= 2^-96 (5 VALU).  Smaller, zero,
-// NaN and infinite inputs take the builtin (a branch that no lane of a
-// typical wave takes).  Exhaustively checked against __builtin_sqrtf over all
-// 2^32 inputs (tests/test_gpu_math.py).
-#ifndef GEO_FAST_SQRT
-#define GEO_FAST_SQRT 1  // 0: the builtin everywhere (A/B switch, tools/gpu_ab.sh)
-#endif
-// GEO_UNIFORM_FIXUP (sqrtf_, rcpf_): the fast sequence runs on every lane
-// with no exec-mask change, and the out-of-range lanes are redone in a
-// wave-uniform branch that a typical wave never takes (a divergent if/else
-// costs ~6 scalar instructions of exec juggling per call, ~10 calls a pixel).
-#ifndef GEO_UNIFORM_FIXUP
-#define GEO_UNIFORM_FIXUP 1
-#endif
-#ifndef GEO_SQRT_RSQ
-#define GEO_SQRT_RSQ 1  // 0: v_sqrt_f32 with the +-1-ulp correction (A/B switch; same values)
-#endif
+// +-0/+inf (~17 VALU).  Here: s = x rsq(x) corrected once by its residual,
+// s + (x - s^2) rsq(x)/2, which is correctly rounded for every finite
+// x >= 2^-96 (5 VALU + the range test; exhaustively checked against
+// __builtin_sqrtf over all 2^32 inputs, tests/test_gpu_math.py).  Smaller,
+// zero, NaN and infinite inputs take the builtin.  The fast sequence runs on
+// every lane with no exec-mask change, and the out-of-range lanes are redone
+// in a wave-uniform branch that a typical wave never takes (a divergent
+// if/else costs ~6 scalar instructions of exec juggling per call, ~10 calls
+// a pixel).
 GEO_HD float sqrtf_(float x) {
-#if defined(__HIP_DEVICE_COMPILE__) && GEO_FAST_SQRT
-#if GEO_UNIFORM_FIXUP && GEO_SQRT_RSQ
-    // s = x rsq(x), corrected once by the residual: s + (x - s^2) rsq(x)/2.
-    // Correctly rounded for every finite x >= 2^-96 (the exhaustive test over
-    // all 2^32 inputs below covers it): 5 VALU + the range test, against 9.
+#if defined(__HIP_DEVICE_COMPILE__)
     const bool ok = __builtin_amdgcn_fmed3f(x, 0x1p-96f, 0x1.fffffep127f) == x;  // NaN, +inf fail
     const float y = __builtin_amdgcn_rsqf(x);
     const float s0 = x * y;
@@ -99,50 +83,21 @@ GEO_HD float sqrtf_(float x) {
         r = ok ? r : __builtin_sqrtf(x);
     }
     return r;
-#elif GEO_UNIFORM_FIXUP
-    const bool ok = x >= 0x1p-96f;
-    const float s = __builtin_amdgcn_sqrtf(x);
-    const uint32_t si = __builtin_bit_cast(uint32_t, s);
-    const float sm = __builtin_bit_cast(float, si - 1u);
-    const float sp = __builtin_bit_cast(float, si + 1u);
-    const float rm = __builtin_fmaf(-sm, s, x);
-    const float rp = __builtin_fmaf(-sp, s, x);
-    const float t = (0.0f >= rm) ? sm : s;
-    float r = (0.0f < rp) ? sp : t;
-    if (__builtin_amdgcn_ballot_w64(!ok) != 0) {
-        GEO_COLD_ARM();
-        r = ok ? r : __builtin_sqrtf(x);
-    }
-    return r;
 #else
-    if (x >= 0x1p-96f) {
-        const float s = __builtin_amdgcn_sqrtf(x);
-        const uint32_t si = __builtin_bit_cast(uint32_t, s);
-        const float sm = __builtin_bit_cast(float, si - 1u);
-        const float sp = __builtin_bit_cast(float, si + 1u);
-        const float rm = __builtin_fmaf(-sm, s, x);
-        const float rp = __builtin_fmaf(-sp, s, x);
-        const float t = (0.0f >= rm) ? sm : s;
-        return (0.0f < rp) ? sp : t;
-    }
-#endif
-#endif
     return __builtin_sqrtf(x);
+#endif
 }
 // Correctly rounded reciprocal, equal to 1.0f / x (hipcc's correctly rounded
-// division, ≈ 11 VALU) for every input.  For normal |x| < 2^126 the
-// Markstein step r + r(1 - x r) on the 1-ulp v_rcp_f32 seed is correctly
-// rounded (3 VALU; checked against the builtin for all 2^32 inputs on the GPU,
+// division, ~11 VALU) for every input.  For normal |x| < 2^126 the Markstein
+// step r + r(1 - x r) on the 1-ulp v_rcp_f32 seed is correctly rounded (3
+// VALU; checked against the builtin for all 2^32 inputs on the GPU,
 // tests/test_gpu_math.py; outside that range the seed's result is denormal,
 // zero or infinite and the step is not exact).  The range test is one
-// v_med3_f32 + compare (NaN fails it); other inputs take the builtin.
-#ifndef GEO_FAST_RCP
-#define GEO_FAST_RCP 1  // 0: the builtin everywhere (A/B switch, tools/gpu_ab.sh)
-#endif
+// v_med3_f32 + compare (NaN fails it); other lanes take the builtin in a
+// wave-uniform branch, as in sqrtf_.
 GEO_HD float rcpf_(float x) {
-#if defined(__HIP_DEVICE_COMPILE__) && GEO_FAST_RCP
+#if defined(__HIP_DEVICE_COMPILE__)
     const float ax = __builtin_fabsf(x);
-#if GEO_UNIFORM_FIXUP
     const bool ok = __builtin_amdgcn_fmed3f(ax, 0x1p-126f, 0x1.fffffep125f) == ax;
     const float r0 = __builtin_amdgcn_rcpf(x);
     float r = __builtin_fmaf(__builtin_fmaf(-x, r0, 1.0f), r0, r0);
@@ -152,28 +107,14 @@ GEO_HD float rcpf_(float x) {
     }
     return r;
 #else
-    if (__builtin_amdgcn_fmed3f(ax, 0x1p-126f, 0x1.fffffep125f) == ax) {
-        const float r = __builtin_amdgcn_rcpf(x);
-        return __builtin_fmaf(__builtin_fmaf(-x, r, 1.0f), r, r);
-    }
-#endif
-#endif
     return 1.0f / x;
+#endif
 }
 // The quotient of the specification: a times the correctly rounded
 // reciprocal of b (two IEEE roundings, within 1 ulp of a / b).  On gfx950
-// that is rcpf_'s 5 VALU plus one multiply instead of the ≈ 11 of a
+// that is rcpf_'s 5 VALU plus one multiply instead of the ~11 of a
 // correctly rounded division; the oracle mirrors it as a * (1.0f / b).
-#ifndef GEO_DIVF
-#define GEO_DIVF 1  // 0: a / b (timing A/B only: not the specification the oracle mirrors)
-#endif
-GEO_HD float divf_(float a, float b) {
-#if GEO_DIVF
-    return a * rcpf_(b);
-#else
-    return a / b;
-#endif
-}
+GEO_HD float divf_(float a, float b) { return a * rcpf_(b); }
 GEO_HD float clampf_(float x, float lo, float hi) { return x < lo ? lo : (x > hi ? hi : x); }
 // max(a, b) with a NaN `a` mapped to b (used to clamp radicands at 0).
 GEO_HD float fmaxf_(float a, float b) { return a > b ? a : b; }
@@ -183,21 +124,13 @@ GEO_HD float fmaxf_(float a, float b) { return a > b ? a : b; }
 // rounds t to an integer (ties to even, as rintf) in the low mantissa bits, so
 // j = (t + M) - M exactly and the quadrant is the sum's low 2 bits (M = 0 mod
 // 4); full-rate adds where v_rndne_f32 and v_cvt_i32_f32 are half-rate.
-#ifndef GEO_SINCOS_SHIFTER
-#define GEO_SINCOS_SHIFTER 1  // 0: rintf and the int cast (A/B switch; same values)
-#endif
 GEO_HD void sincosf_(float x, float* s, float* c) {
-#if GEO_SINCOS_SHIFTER
     constexpr float kShifter = 12582912.0f;  // 1.5 * 2^23
     const float tj = x * kTwoOverPi + kShifter;
     const float j = tj - kShifter;
     uint32_t tb;
     __builtin_memcpy(&tb, &tj, 4);
     const int q = (int)(tb & 3u);
-#else
-    const float j = __builtin_rintf(x * kTwoOverPi);
-    const int q = ((int)j) & 3;
-#endif
     float r = fmaf_(-j, 1.5703125f, x);
     r = fmaf_(-j, 4.837512969970703125e-4f, r);
     r = fmaf_(-j, 7.54978995489188216e-8f, r);

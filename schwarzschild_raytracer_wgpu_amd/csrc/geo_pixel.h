@@ -18,18 +18,6 @@
 
 #include "geo_math.h"
 
-// 1: one exit test per group where the stop set is absorbing (run_groups);
-// 0: a test per step everywhere (A/B switch, tools/gpu_ab.sh).
-#ifndef GEO_ABSORBING_TEST
-#define GEO_ABSORBING_TEST 1
-#endif
-
-// 1: the RK4 loop's frame constants held in VGPRs (geodesic_angle_v);
-// 0: left to the compiler, which keeps them in SGPRs (A/B switch)
-#ifndef GEO_VGPR_CONSTS
-#define GEO_VGPR_CONSTS 1
-#endif
-
 namespace geo {
 
 constexpr float kNoValue = 15.0f;          // SphereRayTracer::NO_VALUE, sphere_ray_tracer.rs:22
@@ -40,8 +28,8 @@ constexpr float kAdaptiveDefaultTol = 1e-6f;  // GEO_ADAPTIVE_DEFAULT_TOL
 constexpr uint32_t kAdaptiveMaxGrowth = 16u;   // GEO_ADAPTIVE_MAX_GROWTH
 
 // Integration kinds (frame-uniform, chosen on the host):
-constexpr int kCurvedOut = 0;  // rs > 0, observer outside the horizon (r > rs)
-constexpr int kCurvedIn = 1;   // rs > 0, observer on/inside the horizon
+constexpr int kCurvedOut = 0;  // rs > 0, observer outside the horizon (r > rs), step in [2^-10, 1/2]
+constexpr int kCurvedIn = 1;   // rs > 0, any other observer or step: the reference's tests as written
 constexpr int kFlat = 2;       // rs = 0: straight lines
 
 // Frame-constant scalars derived from the scene, evaluated identically on
@@ -82,16 +70,13 @@ struct PixelConsts {
     // frame-uniform parts of the stop test and the initial loop test, folded
     // on the host (gfx9 has no scalar float compares, so the kernel would
     // evaluate them in VALU on every lane): StopTest's interval [stop_lo,
-    // stop_hi] and stop_bits = above0 (U0 > SU) | absorbing << 1 (for this
-    // frame's integration kind) | (max_steps != 0 && u0 > 0) << 2
+    // stop_hi] and stop_bits = above0 (U0 > SU) | (max_steps != 0 && u0 > 0) << 2
     float stop_lo, stop_hi;
     uint32_t stop_bits;
-    // |U'| above which a ray may overshoot the absorbing stop set (see
-    // absorbing_safe_): kRiskK / h^3 less the ray-independent part of the
-    // scaled 1/b bound, scale sqrt(max(0, h_over_r2))
-    float risk_ub;
+    int kind;  // the frame's integration kind (geodesic_kind)
     // the integrator's scaled state U = scale*u (scale = 3 rs/2, or 1 for rs = 0)
     float scale, U0, SU, BD, HU;
+    float ub_k;  // scale * (e_out * u0): outside the horizon UB0 = ub_k |sin theta| / cos theta
     float SUp;  // next float above SU: (U > SU) == (U >= SUp) for every float U
     // GEO_MODE_ADAPTIVE step control (geodesic_angle_adaptive), scaled like U
     float tolU;  // scale * tol: reject a step whose error estimate exceeds it
@@ -99,9 +84,6 @@ struct PixelConsts {
     float hmax;  // GEO_ADAPTIVE_MAX_GROWTH * step
 };
 
-#ifndef GEO_PF_BITS
-#define GEO_PF_BITS 1  // 0: read the pre-filter bools (A/B switch)
-#endif
 
 
 // Next float above a positive finite x.
@@ -141,13 +123,14 @@ GEO_HD LaneMask lane_mask_(bool c) { return c; }
 GEO_HD bool lane_select_(LaneMask m, bool a, bool b) { return m ? a : b; }
 #endif
 
-// Overshoot bound of the absorbing-set test (absorbing_safe_): a ray's |U'|
-// stays below scale/b along its path, and a step h can carry U from above the
-// sphere to below 0 and back within a group of 4 only if h^3 scale/b is of
-// order 1/3 (F(U) = U^2 - U is positive again below 0, so a deep overshoot is
-// pushed back up).  Rays with h^3 scale/b above kRiskK = 1e-3 (a margin of
-// ~300) take the per-step test.
-constexpr float kRiskK = 1e-3f;
+// Step sizes for which the interval stop test of kCurvedOut is exact
+// ("Exact group test"): a state entering U > HU from the
+// interval always has U' > 0 there (the reference's horizon test `u > 1/rs &&
+// u' > 0`, :134, then holds at once) and every later state stays above HU.
+// Proved for one f32 RK4 step with h in [2^-10, 1/2]; other steps take the
+// general kCurvedIn test.
+constexpr float kHorizonStepMin = 0x1p-10f;
+constexpr float kHorizonStepMax = 0.5f;
 
 // tol: GEO_MODE_ADAPTIVE local error tolerance in u (<= 0: the default 1e-6).
 GEO_HD PixelConsts make_consts(float rs, float sphere_r, float r, float step, uint32_t max_steps,
@@ -211,15 +194,16 @@ GEO_HD PixelConsts make_consts(float rs, float sphere_r, float r, float step, ui
     k.SU = k.scale * k.sphere_u;
     k.BD = k.scale * k.bound;
     k.HU = k.scale * k.schwarz_u;
+    k.ub_k = k.scale * (k.e_out * k.u0);
     k.SUp = next_up_(k.SU);
     {
         const bool above0 = k.U0 > k.SU;
-        const int kind = !k.rs_nonzero ? kFlat : (k.outside ? kCurvedOut : kCurvedIn);
-        const bool absorbing = kind != kCurvedIn && above0 && (kind == kFlat || k.SU < 1.0f);
+        k.kind = !k.rs_nonzero ? kFlat
+                 : (k.outside && step >= kHorizonStepMin && step <= kHorizonStepMax) ? kCurvedOut
+                                                                                       : kCurvedIn;
         k.stop_lo = above0 ? k.SUp : k.BD;
         k.stop_hi = above0 ? k.HU : k.SU;
-        k.stop_bits = (above0 ? 1u : 0u) | (absorbing ? 2u : 0u) | ((max_steps != 0u && k.u0 > 0.0f) ? 4u : 0u);
-        k.risk_ub = kRiskK / (step * step * step) - k.scale * __builtin_sqrtf(k.h_over_r2 > 0.0f ? k.h_over_r2 : 0.0f);
+        k.stop_bits = (above0 ? 1u : 0u) | ((max_steps != 0u && k.u0 > 0.0f) ? 4u : 0u);
     }
     k.tolU = k.scale * (tol > 0.0f ? tol : kAdaptiveDefaultTol);
     k.tolG = k.tolU * (1.0f / 64.0f);
@@ -227,9 +211,10 @@ GEO_HD PixelConsts make_consts(float rs, float sphere_r, float r, float step, ui
     return k;
 }
 
-GEO_HD int geodesic_kind(const PixelConsts& k) {
-    return !k.rs_nonzero ? kFlat : (k.outside ? kCurvedOut : kCurvedIn);
-}
+// kFlat for rs = 0; kCurvedOut outside the horizon for the steps its stop
+// test is exact for (kHorizonStepMin..Max); kCurvedIn (the reference's full
+// per-step tests) otherwise, which is exact for any frame.
+GEO_HD int geodesic_kind(const PixelConsts& k) { return k.kind; }
 
 // The integrator works on the scaled state U = c u (c = 3 rs/2): RK4 commutes
 // with a linear rescaling of the state, and c f(u) = c(-u + c u^2) becomes
@@ -344,28 +329,37 @@ GEO_HD bool geodesic_init(const PixelConsts& k, float st, float ct, float rct, f
     const float inv_b2 = e2 * ((rct * rct) * k.inv_r2);
     // pre-filters (:106-119), frame-uniform terms precomputed
     const bool eneg = KIND == kCurvedIn && k.pf_eneg && energy < 0.0f;
-#if GEO_PF_BITS
     const bool pf_always = (k.pf_bits & 1u) != 0, pf_falling = (k.pf_bits & 2u) != 0,
                pf_outgoing = (k.pf_bits & 4u) != 0;
-#else
-    const bool pf_always = k.pf_always, pf_falling = k.pf_falling, pf_outgoing = k.pf_outgoing;
-#endif
     if (pf_always || eneg || inv_b2 < k.barrier_lim || lane_select_(falling_m, pf_falling, pf_outgoing)) {
         *early = kNoValue;
         return false;
     }
-    // RK4 init (:122-132); the radicand is clamped at 0 (the reference yields
-    // NaN there only for |theta| < ~1e-8, never at a fan node).
-    float ub = sqrtf_(fmaxf_(0.0f, inv_b2 - k.h_over_r2));
-    if (!falling) ub = -ub;
-    // loop test of :134-135 on the initial state (schwarz_u = +inf for rs = 0;
-    // u0 > schwarz_u needs r < rs)
-    if ((KIND == kCurvedIn && k.u0 > k.schwarz_u && ub > 0.0f) || !(k.stop_bits & 4u)) {
+    // RK4 init (:122-132), scaled: UB = c u'0, u'0 = sqrt(1/b^2 - (1 - rs/r)/r^2).
+    // Outside the horizon E^2 = 1 - rs/r, so the radicand is (E/r)^2 tan^2
+    // theta and UB = (c E/r) |st|/ct (ub_k = c E/r): no cancellation where
+    // the literal difference loses every digit (|theta| << 1, a tangential
+    // ray: up to 4e-4 rad of traveled angle in f32 against the f64 literal
+    // form), and no square root.  Inside the horizon both radicand terms are
+    // positive and the literal form stays (clamped at 0: the reference
+    // yields NaN there only for |theta| < ~1e-8, never at a fan node).
+    float UB;
+    if (KIND == kCurvedIn && k.r_inside_h) {
+        float ub = sqrtf_(fmaxf_(0.0f, inv_b2 - k.h_over_r2));
+        if (!falling) ub = -ub;
+        UB = k.scale * ub;
+    } else {
+        UB = (k.ub_k * __builtin_fabsf(st)) * rct;
+        if (!falling) UB = -UB;
+    }
+    // loop test of :134-135 on the initial state (u' > 0 <=> UB > 0;
+    // schwarz_u = +inf for rs = 0; u0 > schwarz_u needs r < rs)
+    if ((KIND == kCurvedIn && k.u0 > k.schwarz_u && UB > 0.0f) || !(k.stop_bits & 4u)) {
         *early = kNoValue;
         return false;
     }
     *U0 = k.U0;
-    *UB0 = k.scale * ub;
+    *UB0 = UB;
     return true;
 }
 
@@ -379,73 +373,39 @@ GEO_HD bool geodesic_init(const PixelConsts& k, float st, float ct, float rct, f
 //   outside (U0 <= SU):          stop <=> NU not in [BD, SU]
 //       (crossing inward | escape; the horizon HU > SU is a crossing too)
 // `!(NU >= BD)` is (NU < BD) or NaN and, with BD > 0, also covers the `u > 0`
-// test.  NaN always stops.  Inside the horizon the general test is kept.
+// test.  NaN always stops.  The horizon half of the reference's loop test,
+// `u > 1/rs && u' > 0`, is `NU > HU` alone for kCurvedOut: a state that
+// enters U > HU from the interval has U' > 0 for the RK4 map at the steps
+// kCurvedOut admits ("Exact group test").  kCurvedIn keeps
+// the reference's tests as written.
 template <int KIND>
 struct StopTest {
     float SU, BD, HU, lo, hi;
+    float vmin;  // above0 ? 0 : -inf (exact())
     bool above0;
-    bool absorbing;  // the stop set is absorbing (run_groups): observer inside the sphere, sphere
-                     // beyond the photon sphere (SU < 1: F < 0 below SU), outside the horizon
     GEO_HDM explicit StopTest(const PixelConsts& k)
-        : SU(k.SU), BD(k.BD), HU(k.HU), lo(k.stop_lo), hi(k.stop_hi), above0((k.stop_bits & 1u) != 0) {
-        absorbing = KIND != kCurvedIn && (k.stop_bits & 2u) != 0;
-    }
+        : SU(k.SU), BD(k.BD), HU(k.HU), lo(k.stop_lo), hi(k.stop_hi),
+          vmin((k.stop_bits & 1u) != 0 ? 0.0f : -__builtin_inff()), above0((k.stop_bits & 1u) != 0) {}
     GEO_HDM bool operator()(float NU, float NUB) const {
         if constexpr (KIND == kCurvedIn)
             return ((NU > SU) != above0) | !(NU >= BD) | ((NU > HU) & (NUB > 0.0f));
         else
             return med3_(NU, lo, hi) != NU;
     }
+    // The same flag with the horizon's `u' > 0` evaluated, for a stepper the
+    // kCurvedOut argument does not cover (the adaptive RK5(4) map, whose step
+    // grows to 16 h): NU < lo | NaN | (NU > hi & NUB > vmin), where vmin = 0
+    // inside the sphere (the horizon test) and -inf outside it (NU > hi = SU
+    // is a crossing; a NaN NUB comes with a NaN NU).  Three compares, each
+    // balloted on its own.
+    GEO_HDM bool exact(float NU, float NUB) const {
+        if constexpr (KIND == kCurvedOut)
+            return !(NU >= lo) | ((NU > hi) & (NUB > vmin));
+        else
+            return (*this)(NU, NUB);
+    }
 };
 
-// The group loop: G RK4 steps per exit test; returns the steps before the
-// stopping group (or `all` when the budget of whole groups runs out), with the
-// group's G + 1 states in su_/sb_.
-//
-// LAST_ONLY tests only the group's last state.  That is exact when the stop
-// set is ABSORBING: once a step's state is in it, every later state is too.
-// It holds for an observer inside the sphere outside the horizon (kCurvedOut,
-// kFlat with U0 > SU) when the sphere lies beyond the photon sphere (SU < 1),
-// whose stop set is then {U <= SU} + {U > HU} + NaN:
-//  * U <= SU < 1 (r > 1.5 rs): F(U) < 0, so U' falls by ~h|F| per step.  The
-//    step that first lands at U <= SU came from above, and U' is already
-//    negative after it.  u has no minimum beyond the photon sphere (u'' < 0
-//    there), so U keeps falling until it escapes (U < BD < SU) or goes NaN.
-//  * U > HU = 1.5 (inside the horizon): F(U) > 0, so U' grows by ~h F and U
-//    keeps rising.
-// The margins (h|F| ~ 1e-3 per step) dwarf f32 rounding.  The GPU parity tests
-// and the host-compiled header tests check it bit for bit against the
-// oracle's literal per-step test.  An observer outside the sphere can graze
-// it, entering and leaving within a group, and inside the photon sphere u has
-// minima, so those keep the per-step test.
-template <int G, int KIND, bool LAST_ONLY>
-GEO_HD uint32_t run_groups(const StopTest<KIND>& stop_at, uint32_t ngroups, uint32_t all, float h, float hh,
-                           float hh2, float hhh, float h6, float h2_6, float (&su_)[G + 1], float (&sb_)[G + 1]) {
-    for (uint32_t q = 0; q < ngroups; ++q) {
-        bool stop = false;
-#pragma unroll
-        for (int j = 0; j < G; ++j) {
-            rk4_step<KIND>(su_[j], sb_[j], h, hh, hh2, hhh, h6, h2_6, &su_[j + 1], &sb_[j + 1]);
-            if constexpr (!LAST_ONLY) stop = stop | stop_at(su_[j + 1], sb_[j + 1]);
-        }
-        if constexpr (LAST_ONLY) stop = stop_at(su_[G], sb_[G]);
-        if (stop) return q * (uint32_t)G;
-        su_[0] = su_[G];
-        sb_[0] = sb_[G];
-    }
-    return all;
-}
-
-// run_groups without copies (GEO_PINGPONG): the loop alternates two register
-// sets, group A stepping from X into a_1..a_G and group B from a_G into
-// b_1..b_{G-1}, X, so neither ends with the start-state move of run_groups.
-// Its exit is wave-uniform (every lane done, or the budget): a lane that stops
-// is masked off (`done`) and keeps its stopping group's states in whichever
-// set that group wrote; after the loop one select per state puts them in
-// su_/sb_.  Results equal run_groups' bit for bit.
-#ifndef GEO_PINGPONG
-#define GEO_PINGPONG 1
-#endif
 // The lanes of the wave for which p holds (a uniform SGPR mask), and the
 // rarely taken arm of a branch that must stay a branch: a volatile asm cannot
 // be speculated, so the compiler cannot turn the arm into a select that every
@@ -467,36 +427,69 @@ GEO_HD void group_steps_(float u, float b, float h, float hh, float hh2, float h
     for (int j = 0; j < G; ++j)
         rk4_step<KIND>(j ? ou[j - 1] : u, j ? ob[j - 1] : b, h, hh, hh2, hhh, h6, h2_6, &ou[j], &ob[j]);
 }
-// The lanes whose group stops (the last state's test where the stop set is
-// absorbing), as a wave mask.  hipcc takes the ballot of a single compare as
-// its mask but rebuilds any other condition through a VGPR (two VALU): with
-// the per-step interval test (one compare per state) the G ballots are ORed
-// in scalar ops; the compound test inside the horizon is ORed first and
-// balloted once.
-template <int G, int KIND, bool LAST_ONLY>
+
+// The exit test of a group of G RK4 steps, exact: it holds iff the per-step
+// StopTest holds for one of the group's G states (the group's start state is
+// inside the interval, or the previous group would have stopped).  Three
+// forms, chosen per frame:
+//   kTestLow  (kCurvedOut/kFlat, observer inside the sphere): the minimum of
+//             states 1..G-1 below lo, or state G outside [lo, hi] (or NaN).
+//             A state above hi = HU needs no test of its own: it has U' > 0,
+//             and U > HU with U' >= 0 maps to U' >= U, U'' >= U' under the
+//             f32 RK4 map (all stage values exceed 1, so every F >= 0), so
+//             state G is above HU too.  NaN propagates to state G.
+//   kTestBoth (kCurvedOut/kFlat, observer outside the sphere): the minimum
+//             below lo or the maximum above hi (the ray can graze the sphere,
+//             entering and leaving within a group), or state G outside.
+//   kTestEach (kCurvedIn): the reference's compound test on every state.
+// (round 2 tested the last state alone, exact only while no state left the
+// interval and came back within a group, which a near-radial outgoing ray at
+// a large step breaks; the minimum costs 2 VALU per group more)
+// hipcc takes the ballot of a single compare as its mask but rebuilds any
+// other condition through a VGPR (two VALU), so the compares are balloted one
+// by one and ORed in scalar ops; the compound test is ORed first and balloted
+// once.
+constexpr int kTestLow = 0;
+constexpr int kTestBoth = 1;
+constexpr int kTestEach = 2;
+
+template <int G, int KIND, int TEST>
 GEO_HD uint64_t group_stop_(const StopTest<KIND>& stop_at, const float (&ou)[G], const float (&ob)[G]) {
-    if constexpr (LAST_ONLY) {
-        return ballot_(stop_at(ou[G - 1], ob[G - 1]));
-    } else if constexpr (KIND == kCurvedIn) {
+    if constexpr (TEST == kTestEach || G == 1) {
         bool s = false;
 #pragma unroll
         for (int j = 0; j < G; ++j) s = s | stop_at(ou[j], ob[j]);
         return ballot_(s);
     } else {
-        uint64_t m = 0;
+        // the minimum of all G states (v_min3_f32: one op for G = 3, two for
+        // 4), NaN-free; a NaN state makes state G NaN, which `!(<= hi)` sees
+        float mn = ou[0];
 #pragma unroll
-        for (int j = 0; j < G; ++j) m |= ballot_(stop_at(ou[j], ob[j]));
+        for (int j = 1; j < G; ++j) mn = __builtin_fminf(mn, ou[j]);
+        uint64_t m = ballot_(!(mn >= stop_at.lo)) | ballot_(!(ou[G - 1] <= stop_at.hi));
+        if constexpr (TEST == kTestBoth) {
+            float mx = ou[0];
+#pragma unroll
+            for (int j = 1; j < G - 1; ++j) mx = __builtin_fmaxf(mx, ou[j]);  // v_max3_f32
+            m |= ballot_(mx > stop_at.hi);
+        }
         return m;
     }
 }
 
-#ifndef GEO_PAIR_LOOP
-#define GEO_PAIR_LOOP 1  // 0: exit tests after each group (A/B switch)
-#endif
-#ifndef GEO_LIVE_EXEC
-#define GEO_LIVE_EXEC 1  // 0: a per-lane `done` flag masks the group steps (A/B switch)
-#endif
-template <int G, int KIND, bool LAST_ONLY>
+// The group loop: G RK4 steps per exit test; returns the steps before the
+// stopping group (or `all` when the budget of whole groups runs out), with the
+// group's G + 1 states in su_/sb_.  A lane that stops inside a group discards
+// the rest of it (the oracle keeps the literal per-step loop; tests require
+// bit equality).
+//
+// The loop alternates two register sets, group A stepping from X into
+// a_1..a_G and group B from a_G into b_1..b_{G-1}, X, so neither ends with a
+// start-state move.  Its exit is wave-uniform (every lane done, or the
+// budget): a lane that stops is masked off and keeps its stopping group's
+// states in whichever set that group wrote; after the loop one select per
+// state puts them in su_/sb_.
+template <int G, int KIND, int TEST>
 GEO_HD uint32_t run_groups_pp(const StopTest<KIND>& stop_at, uint32_t ngroups, uint32_t all, float h, float hh,
                               float hh2, float hhh, float h6, float h2_6, float (&su_)[G + 1], float (&sb_)[G + 1]) {
     float xu = su_[0], xb = sb_[0];  // X: group A's start, group B's end
@@ -515,7 +508,7 @@ GEO_HD uint32_t run_groups_pp(const StopTest<KIND>& stop_at, uint32_t ngroups, u
     // Groups q = 0, 2, 4, ... are A groups, 1, 3, ... B groups.  A lane that
     // stops in group q records it = q G (a multiple of G below `all`), so the
     // set its states sit in is (it / G) & 1 after the loop.
-#if GEO_LIVE_EXEC
+    //
     // The lanes still integrating are the wave-uniform mask `live`, which is
     // also the exec mask of the group steps: no per-lane flag, so the loop's
     // scalar work is the masked regions, one AND per stop test and a branch
@@ -523,7 +516,6 @@ GEO_HD uint32_t run_groups_pp(const StopTest<KIND>& stop_at, uint32_t ngroups, u
     uint64_t live = ballot_(true);
     uint32_t it = all;
     uint32_t q = 0;
-#if GEO_PAIR_LOOP
     // One exit test per A+B pair of groups: a group whose lanes are all done
     // runs with an empty exec mask, which the masked region's execz branch
     // skips, so the pair needs no test between its groups; an odd budget's
@@ -533,7 +525,7 @@ GEO_HD uint32_t run_groups_pp(const StopTest<KIND>& stop_at, uint32_t ngroups, u
     uint32_t rem = ngroups >> 1;
     while (rem != 0) {
         if (in_ballot_(live)) group_steps_<G, KIND>(xu, xb, h, hh, hh2, hhh, h6, h2_6, au, ab);
-        uint64_t hit = group_stop_<G, KIND, LAST_ONLY>(stop_at, au, ab) & live;
+        uint64_t hit = group_stop_<G, KIND, TEST>(stop_at, au, ab) & live;
         --rem;
         if (hit != 0) {
             if (in_ballot_(hit)) {
@@ -562,7 +554,7 @@ GEO_HD uint32_t run_groups_pp(const StopTest<KIND>& stop_at, uint32_t ngroups, u
         }
         tu[G - 1] = xu;
         tb[G - 1] = xb;
-        hit = group_stop_<G, KIND, LAST_ONLY>(stop_at, tu, tb) & live;
+        hit = group_stop_<G, KIND, TEST>(stop_at, tu, tb) & live;
         q += 2u;
         // `live` empties only where lanes stop, so its test sits in that
         // branch: a pair without stops ends in the counter's compare alone
@@ -577,110 +569,13 @@ GEO_HD uint32_t run_groups_pp(const StopTest<KIND>& stop_at, uint32_t ngroups, u
     }
     if ((ngroups & 1u) != 0 && live != 0) {
         if (in_ballot_(live)) group_steps_<G, KIND>(xu, xb, h, hh, hh2, hhh, h6, h2_6, au, ab);
-        const uint64_t hit = group_stop_<G, KIND, LAST_ONLY>(stop_at, au, ab) & live;
+        const uint64_t hit = group_stop_<G, KIND, TEST>(stop_at, au, ab) & live;
         if (in_ballot_(hit)) {
             GEO_RARE();
             it = q * (uint32_t)G;
         }
         ++q;
     }
-#else
-    while (q < ngroups) {
-        if (in_ballot_(live)) group_steps_<G, KIND>(xu, xb, h, hh, hh2, hhh, h6, h2_6, au, ab);
-        uint64_t hit = group_stop_<G, KIND, LAST_ONLY>(stop_at, au, ab) & live;
-        if (hit != 0) {
-            if (in_ballot_(hit)) {
-                GEO_RARE();
-                it = q * (uint32_t)G;
-            }
-            live &= ~hit;
-        }
-        if (++q >= ngroups) break;
-        if (live == 0) break;
-        if (in_ballot_(live)) {
-            float ou[G], ob[G];
-            group_steps_<G, KIND>(au[G - 1], ab[G - 1], h, hh, hh2, hhh, h6, h2_6, ou, ob);
-#pragma unroll
-            for (int j = 0; j < G - 1; ++j) {
-                bu[j] = ou[j];
-                bb[j] = ob[j];
-            }
-            xu = ou[G - 1];
-            xb = ob[G - 1];
-        }
-        float tu[G], tb[G];
-#pragma unroll
-        for (int j = 0; j < G - 1; ++j) {
-            tu[j] = bu[j];
-            tb[j] = bb[j];
-        }
-        tu[G - 1] = xu;
-        tb[G - 1] = xb;
-        hit = group_stop_<G, KIND, LAST_ONLY>(stop_at, tu, tb) & live;
-        if (hit != 0) {
-            if (in_ballot_(hit)) {
-                GEO_RARE();
-                it = q * (uint32_t)G;
-            }
-            live &= ~hit;
-        }
-        ++q;
-        if (live == 0) break;
-    }
-#endif
-#else
-    // the loop carries one lane flag (`done`), which keeps the lane-mask
-    // merges at its joins to a minimum
-    bool done = false;
-    uint64_t live = ballot_(true);  // wave-uniform: the lanes still integrating
-    uint32_t it = all;
-    uint32_t q = 0;                 // wave-uniform: groups run
-    // The stop test runs outside the `if (!done)` regions, on every lane: its
-    // ballot is then the compare mask itself (a flag merged out of the region
-    // would be rematerialised by two VALU ops per group).  A finished lane's
-    // flag is garbage but harmless: `live` only ever loses bits.
-    while (q < ngroups) {
-        if (!done) group_steps_<G, KIND>(xu, xb, h, hh, hh2, hhh, h6, h2_6, au, ab);
-        uint64_t hit = group_stop_<G, KIND, LAST_ONLY>(stop_at, au, ab);
-        live &= ~hit;
-        if (in_ballot_(hit) && !done) {
-            GEO_RARE();
-            done = true;
-            it = q * (uint32_t)G;
-        }
-        // two uniform branches (one `||` is lowered through lane masks)
-        if (++q >= ngroups) break;
-        if (live == 0) break;
-        if (!done) {
-            float ou[G], ob[G];
-            group_steps_<G, KIND>(au[G - 1], ab[G - 1], h, hh, hh2, hhh, h6, h2_6, ou, ob);
-#pragma unroll
-            for (int j = 0; j < G - 1; ++j) {
-                bu[j] = ou[j];
-                bb[j] = ob[j];
-            }
-            xu = ou[G - 1];
-            xb = ob[G - 1];
-        }
-        float tu[G], tb[G];
-#pragma unroll
-        for (int j = 0; j < G - 1; ++j) {
-            tu[j] = bu[j];
-            tb[j] = bb[j];
-        }
-        tu[G - 1] = xu;
-        tb[G - 1] = xb;
-        hit = group_stop_<G, KIND, LAST_ONLY>(stop_at, tu, tb);
-        live &= ~hit;
-        if (in_ballot_(hit) && !done) {
-            GEO_RARE();
-            done = true;
-            it = q * (uint32_t)G;
-        }
-        ++q;
-        if (live == 0) break;
-    }
-#endif
     // the set holding the stopping group (B: start a_G, then b_1..b_{G-1}, X);
     // a lane on the budget continues from the last group's end state, which
     // sits where a B group's start state (a_G, after an A group) or an A
@@ -698,20 +593,13 @@ GEO_HD uint32_t run_groups_pp(const StopTest<KIND>& stop_at, uint32_t ngroups, u
     return it;
 }
 
-#ifndef GEO_RISK_TEST
-#define GEO_RISK_TEST 1  // 0: the frame-uniform absorbing choice alone (A/B and fuzz switch)
-#endif
-#ifndef GEO_SCAN_BSEARCH
-#define GEO_SCAN_BSEARCH 1  // 0: the linear scan everywhere (A/B switch)
-#endif
-
-// After the group loop (run_groups): from the G + 1 states of the lane's
-// stopping group and `it` = the steps before it (or the whole-group budget),
-// the first stopping step, the budget tail of fewer than G steps, the
-// crossing test and Newton (sphere_ray_tracer.rs:150-191).  *steps =
-// executed main-loop RK4 steps.
+// After the group loop: from the G + 1 states of the lane's stopping group
+// and `it` = the steps before it (or the whole-group budget), the first
+// stopping step, the budget tail of fewer than G steps, the crossing test and
+// Newton (sphere_ray_tracer.rs:150-191).  *steps = executed main-loop RK4
+// steps.
 template <int G, int KIND>
-GEO_HD float geodesic_finish(const PixelConsts& k, const StopTest<KIND>& stop_at, bool absorbing, uint32_t it,
+GEO_HD float geodesic_finish(const PixelConsts& k, const StopTest<KIND>& stop_at, uint32_t it,
                              float (&su_)[G + 1], float (&sb_)[G + 1], uint32_t* steps) {
     const uint32_t ms = k.max_steps;
     // Opaque copies: the per-step flags are recomputed from the state rather
@@ -723,24 +611,7 @@ GEO_HD float geodesic_finish(const PixelConsts& k, const StopTest<KIND>& stop_at
     }
     GEO_OPAQUE(it);
     float ou = su_[0], oub = sb_[0], nu = su_[0], nub = sb_[0];
-    if (G == 4 && GEO_SCAN_BSEARCH && absorbing && GEO_ABSORBING_TEST && it + (uint32_t)G <= ms) {
-        // stopped inside the group, where the stop set is absorbing: the
-        // flags of states 1..4 are monotone (false.. then true.., state 4's
-        // true), so two tests find the first stopping state k -- state 2,
-        // then state 1 (k <= 2) or state 3 (k > 2) -- where the scan below
-        // makes four; the step is k, from state k - 1 to state k
-        const bool t2 = stop_at(su_[2], sb_[2]);
-        const bool tx = stop_at(t2 ? su_[1] : su_[3], t2 ? sb_[1] : sb_[3]);
-        const float lu = tx ? su_[0] : su_[1], lb = tx ? sb_[0] : sb_[1];  // k = 1 or 2
-        const float mu = tx ? su_[1] : su_[2], mb = tx ? sb_[1] : sb_[2];
-        const float hu = tx ? su_[2] : su_[3], hb = tx ? sb_[2] : sb_[3];  // k = 3 or 4
-        const float gu = tx ? su_[3] : su_[G], gb = tx ? sb_[3] : sb_[G];
-        ou = t2 ? lu : hu;
-        oub = t2 ? lb : hb;
-        nu = t2 ? mu : gu;
-        nub = t2 ? mb : gb;
-        it += (t2 ? 1u : 3u) + (tx ? 0u : 1u);
-    } else if (it + (uint32_t)G <= ms) {
+    if (it + (uint32_t)G <= ms) {
         // stopped inside the group: the first step j whose flag holds
         bool found = false;
 #pragma unroll
@@ -772,10 +643,15 @@ GEO_HD float geodesic_finish(const PixelConsts& k, const StopTest<KIND>& stop_at
     return newton_angle<KIND>(k, ou, oub, nu, nub, it);
 }
 
+// RK4 steps per exit test: 4 is the fastest on gfx950 (G = 5, 6, 8 +0.4, +5,
+// +6 % on config 3: the steps a lane wastes in its stopping group outweigh the
+// saved tests; DESIGN.md §4, tools/ubench/loop_ab.hip)
+constexpr int kGroup = 4;
+
 // Traveled angle of the ray at angle theta to the black hole, or kNoValue.
-// *steps = executed main-loop RK4 steps.  LOOP = RK4 steps per exit test
-// (tools/ubench/loop_ab.hip), KIND the integration kind (geodesic_kind).
-template <int LOOP, int KIND>
+// *steps = executed main-loop RK4 steps.  KIND: the integration kind
+// (geodesic_kind); LOOP = RK4 steps per exit test.
+template <int KIND, int LOOP = kGroup>
 GEO_HD float geodesic_angle_v(const PixelConsts& k, float st, float ct, float rct, uint32_t* steps) {
     *steps = 0;
     float U, UB, early;
@@ -785,7 +661,6 @@ GEO_HD float geodesic_angle_v(const PixelConsts& k, float st, float ct, float rc
     // lane-exit flag is StopTest (crossing | escape | horizon); the budget
     // (:135) is wave-uniform.
     StopTest<KIND> stop_at(k);
-#if GEO_VGPR_CONSTS
     // The loop's frame constants in VGPRs: on gfx950 a VALU op that reads an
     // SGPR issues at about half the rate of an all-VGPR one
     // (tools/ubench/op_rates.hip), and 6 of the step's 14 ops read one.
@@ -797,11 +672,8 @@ GEO_HD float geodesic_angle_v(const PixelConsts& k, float st, float ct, float rc
     GEO_OPAQUE(h2_6);
     GEO_OPAQUE(stop_at.lo);
     GEO_OPAQUE(stop_at.hi);
-#endif
-    // LOOP = G: G RK4 steps per exit test (the budget in whole groups is a
-    // wave-uniform bound); a lane that stops inside a group discards the rest
-    // of it.  Results equal the literal loop's (the oracle keeps that form;
-    // tests require bit equality).
+    // G RK4 steps per exit test (the budget in whole groups is a wave-uniform
+    // bound)
     constexpr int G = LOOP;
     const uint32_t ms = k.max_steps;
     const uint32_t ngroups = ms / (uint32_t)G;
@@ -813,47 +685,27 @@ GEO_HD float geodesic_angle_v(const PixelConsts& k, float st, float ct, float rc
         su_[j] = U;
         sb_[j] = UB;
     }
-    // The once-per-group test needs the stop set to be absorbing for the
-    // discrete RK4 map too: a wave with an outgoing ray fast enough to
-    // overshoot U = 0 and be pushed back (U' < -risk_ub: near-radial rays
-    // away from the black hole; none in the default scenes' views) takes the
-    // per-step test, which is exact for any ray.  Falling rays cannot leave
-    // the horizon side (F > 0 there, U keeps rising).
-#if GEO_RISK_TEST
-    const bool absorbing = stop_at.absorbing && ballot_(UB < -k.risk_ub) == 0;
-#else
-    const bool absorbing = stop_at.absorbing;
-#endif
     // per lane: steps before its stopping group (budget: all)
     uint32_t it;
-#if GEO_PINGPONG
-    if (absorbing)  // wave-uniform
-        it = run_groups_pp<G, KIND, GEO_ABSORBING_TEST != 0>(stop_at, ngroups, ngroups * (uint32_t)G, h, hh, hh2,
-                                                             hhh, h6, h2_6, su_, sb_);
+    if constexpr (KIND == kCurvedIn)
+        it = run_groups_pp<G, KIND, kTestEach>(stop_at, ngroups, ngroups * (uint32_t)G, h, hh, hh2, hhh, h6, h2_6,
+                                               su_, sb_);
+    else if (stop_at.above0)  // frame-uniform
+        it = run_groups_pp<G, KIND, kTestLow>(stop_at, ngroups, ngroups * (uint32_t)G, h, hh, hh2, hhh, h6, h2_6,
+                                              su_, sb_);
     else
-        it = run_groups_pp<G, KIND, false>(stop_at, ngroups, ngroups * (uint32_t)G, h, hh, hh2, hhh, h6, h2_6,
-                                           su_, sb_);
-#else
-    if (absorbing)  // wave-uniform
-        it = run_groups<G, KIND, GEO_ABSORBING_TEST != 0>(stop_at, ngroups, ngroups * (uint32_t)G, h, hh, hh2, hhh,
-                                                          h6, h2_6, su_, sb_);
-    else
-        it = run_groups<G, KIND, false>(stop_at, ngroups, ngroups * (uint32_t)G, h, hh, hh2, hhh, h6, h2_6, su_,
-                                        sb_);
-#endif
-    return geodesic_finish<G, KIND>(k, stop_at, absorbing, it, su_, sb_, steps);
+        it = run_groups_pp<G, KIND, kTestBoth>(stop_at, ngroups, ngroups * (uint32_t)G, h, hh, hh2, hhh, h6, h2_6,
+                                               su_, sb_);
+    return geodesic_finish<G, KIND>(k, stop_at, it, su_, sb_, steps);
 }
 
-#ifndef GEO_LOOP_VARIANT
-#define GEO_LOOP_VARIANT 4  // RK4 steps per exit test; fastest on gfx950 (tools/ubench/loop_ab.hip)
-#endif
 // Runtime-dispatched form (host tests); the kernel instantiates per kind.
 GEO_HD float geodesic_angle(const PixelConsts& k, float st, float ct, uint32_t* steps) {
     const float rct = rcpf_(ct);
     switch (geodesic_kind(k)) {
-        case kCurvedOut: return geodesic_angle_v<GEO_LOOP_VARIANT, kCurvedOut>(k, st, ct, rct, steps);
-        case kCurvedIn: return geodesic_angle_v<GEO_LOOP_VARIANT, kCurvedIn>(k, st, ct, rct, steps);
-        default: return geodesic_angle_v<GEO_LOOP_VARIANT, kFlat>(k, st, ct, rct, steps);
+        case kCurvedOut: return geodesic_angle_v<kCurvedOut>(k, st, ct, rct, steps);
+        case kCurvedIn: return geodesic_angle_v<kCurvedIn>(k, st, ct, rct, steps);
+        default: return geodesic_angle_v<kFlat>(k, st, ct, rct, steps);
     }
 }
 
@@ -905,9 +757,6 @@ GEO_HD void dp5_step(float U, float V, float h, float hh, float* NU, float* NV, 
     *SE = fmaf_(e6, g6, fmaf_(e5, g5, fmaf_(e4, g4, fmaf_(e3, g3, e1 * g1))));
 }
 
-#ifndef GEO_ADAPTIVE_HFACTOR
-#define GEO_ADAPTIVE_HFACTOR 1  // 0: the step update as h + h / h / h * 0.5 selects (A/B switch; same bits)
-#endif
 // Traveled angle with error-controlled steps, or kNoValue; *steps = step
 // attempts (accepted + rejected).  Same ray set-up, stop order and Newton
 // sphere crossing as the fixed-step path (sphere_ray_tracer.rs:60-193), with
@@ -937,13 +786,12 @@ GEO_HD float geodesic_angle_adaptive(const PixelConsts& k, float st, float ct, f
         dp5_step<KIND>(U, V, h, hh, &NU, &NV, &SE);
         const float err = __builtin_fabsf(SE) * hh;
         const bool acc = !(err > k.tolU);
-        if (acc && stop_at(NU, NV)) {
+        if (acc & stop_at.exact(NU, NV)) {  // `&`: both flags as lane masks, no branch between them
             stopped = true;
             break;
         }
         // min(2h, hmax) as a growth test: h is step/2^j or step*2^j <= hmax with
         // hmax = 16 step, so h < hmax implies 2h <= hmax (same bits, 2 fewer VALU)
-#if GEO_ADAPTIVE_HFACTOR
         // the new step as h times 2, 1 or 1/2 (exact: the same bits as h + h,
         // h and h * 0.5), one multiply after two selects of the factor
         const float grow = (err < k.tolG && h < k.hmax) ? 2.0f : 1.0f;
@@ -951,13 +799,6 @@ GEO_HD float geodesic_angle_adaptive(const PixelConsts& k, float st, float ct, f
         V = acc ? NV : V;
         ang = acc ? ang + h : ang;
         h = h * (acc ? grow : 0.5f);
-#else
-        const float hg = (err < k.tolG && h < k.hmax) ? h + h : h;
-        U = acc ? NU : U;
-        V = acc ? NV : V;
-        ang = acc ? ang + h : ang;
-        h = acc ? hg : h * 0.5f;
-#endif
     }
     *steps = it;
     if (!stopped || (NU > k.SU) == (U > k.SU)) return kNoValue;
@@ -1051,11 +892,8 @@ GEO_HD void pixel_central_dir(const CameraConsts& cc, const float* m1, float psi
 // floor(x) as an int32 for |x| < 2^31 (the sampler's texel coordinates):
 // one v_cvt_flr_i32_f32 on the device, where hipcc emits v_floor_f32 +
 // v_cvt_i32_f32 (two half-rate opcodes) for the cast of floorf.
-#ifndef GEO_CVT_FLR
-#define GEO_CVT_FLR 1  // 0: the cast of floorf (A/B switch)
-#endif
 GEO_HD int32_t floor_i32_(float x) {
-#if defined(__HIP_DEVICE_COMPILE__) && GEO_CVT_FLR
+#if defined(__HIP_DEVICE_COMPILE__)
     int32_t r;
     asm("v_cvt_flr_i32_f32 %0, %1" : "=v"(r) : "v"(x));
     return r;
@@ -1069,13 +907,10 @@ GEO_HD int32_t floor_i32_(float x) {
 // one fma correction (exhaustively equal to a / pi over fan_lerp's domain,
 // tests/native/divpi_exhaustive.hip), the index by v_cvt_flr_i32_f32 and the
 // weight by v_fract_f32 (t - floor(t), exact for t >= 0).
-#ifndef GEO_FAN_FAST
-#define GEO_FAN_FAST 1  // 0: the division and floorf (A/B switch; same values)
-#endif
 GEO_HD float fan_lerp(const float* fan, uint32_t n, float st) {
     const float theta = asinf_(st);
     const float a = kPi2 - theta;
-#if defined(__HIP_DEVICE_COMPILE__) && GEO_FAN_FAST
+#if defined(__HIP_DEVICE_COMPILE__)
     constexpr float kRcpPi = 1.0f / kPi;
     const float q0 = a * kRcpPi;
     const float quot = fmaf_(fmaf_(-q0, kPi, a), kRcpPi, q0);
@@ -1084,7 +919,7 @@ GEO_HD float fan_lerp(const float* fan, uint32_t n, float st) {
 #endif
     float t = clampf_(quot, 0.0f, 1.0f);
     t = t * (float)(n - 1u);
-#if defined(__HIP_DEVICE_COMPILE__) && GEO_FAN_FAST
+#if defined(__HIP_DEVICE_COMPILE__)
     const uint32_t i = (uint32_t)floor_i32_(t);
     const float w = __builtin_amdgcn_fractf(t);
 #else
@@ -1136,11 +971,8 @@ GEO_HD uint32_t ga_(uint32_t t) { return (t >> 8) & 0x00FF00FFu; }
 // Operands < 2^24 (packed pairs <= 0x00FF00FF, weights <= 256): the 24-bit
 // multiply (v_mul_u32_u24 / v_mad_u32_u24, full rate) gives the same low 32
 // bits as v_mul_lo_u32 (quarter rate), which is what hipcc picks otherwise.
-#ifndef GEO_MUL24
-#define GEO_MUL24 1  // 0: plain 32-bit multiplies (A/B switch, tools/gpu_ab.sh)
-#endif
 GEO_HD uint32_t mul24_(uint32_t a, uint32_t b) {
-#if defined(__HIP_DEVICE_COMPILE__) && GEO_MUL24
+#if defined(__HIP_DEVICE_COMPILE__)
     return (uint32_t)__umul24(a, b);
 #else
     return a * b;

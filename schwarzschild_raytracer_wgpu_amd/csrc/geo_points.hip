@@ -29,15 +29,10 @@
 
 namespace {
 
-#ifndef GEO_RAYS_BLOCK
-#define GEO_RAYS_BLOCK 64  // one wave per block: +2 % over 256 (tools/gpu_ab.sh)
-#endif
-constexpr int kRaysBlock = GEO_RAYS_BLOCK;
-#ifndef GEO_RAYS_TILED
-// node-value layout (tools/gpu_ab.sh): 2 = 64-connector tiles of node quads (16-B loads and stores),
-// 1 = 64-connector tiles of single nodes (+4.5 % over 0), 0 = node-major SoA
-#define GEO_RAYS_TILED 2
-#endif
+// one wave per block: +2 % over 256 (tools/gpu_ab.sh).  Node values in
+// 64-connector tiles of node quads (16-B loads and stores): +4.5 % over
+// single-node tiles, which were +4.5 % over node-major SoA.
+constexpr int kRaysBlock = 64;
 constexpr int kOrbitBlock = 64;  // f64 orbit lanes: few points, long serial chains
 
 // fastrand 2.0.1's generator (wyrand) and its f64 mapping, restated: one
@@ -88,38 +83,14 @@ struct RaysArgs {
     float4* out;                 // [n_conn]
 };
 
-// Node-value stream: read once and written once per call (GEO_RAYS_NT: non-temporal hints).
-#ifndef GEO_RAYS_NT
-#define GEO_RAYS_NT 1  // +5.5 % (tools/gpu_ab.sh, bench_points)
-#endif
-__device__ __forceinline__ float ld_(const float* p) {
-#if GEO_RAYS_NT
-    return __builtin_nontemporal_load(p);
-#else
-    return *p;
-#endif
-}
-__device__ __forceinline__ void st_(float* p, float v) {
-#if GEO_RAYS_NT
-    __builtin_nontemporal_store(v, p);
-#else
-    *p = v;
-#endif
-}
+// Node-value stream: read once and written once per call, with non-temporal
+// hints (+5.5 %, tools/gpu_ab.sh, bench_points).
 typedef float f4_ __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ f4_ ld4_(const float* p) {
-#if GEO_RAYS_NT
     return __builtin_nontemporal_load(reinterpret_cast<const f4_*>(p));
-#else
-    return *reinterpret_cast<const f4_*>(p);
-#endif
 }
 __device__ __forceinline__ void st4_(float* p, f4_ v) {
-#if GEO_RAYS_NT
     __builtin_nontemporal_store(v, reinterpret_cast<f4_*>(p));
-#else
-    *reinterpret_cast<f4_*>(p) = v;
-#endif
 }
 
 // RESPAWN = false: one RayConnector call per connector (update_ray / reset_ray).
@@ -128,17 +99,7 @@ __device__ __forceinline__ void st4_(float* p, f4_ v) {
 // reset_ray at the new position; the regular pass follows.  Two launches keep
 // one solve per lane (VGPR budget: 48 nodes + 46 + 46 Thomas values).
 template <bool RESPAWN>
-#ifndef GEO_RAYS_NOCOMPUTE
-#define GEO_RAYS_NOCOMPUTE 0
-#endif
-#ifndef GEO_RAYS_MINW
-#define GEO_RAYS_MINW 0  // > 0: __launch_bounds__ min waves per SIMD (VGPR cap; A/B switch)
-#endif
-#if GEO_RAYS_MINW > 0
-__global__ __launch_bounds__(kRaysBlock, GEO_RAYS_MINW) void geo_rays_kernel(const RaysArgs a) {
-#else
 __global__ __launch_bounds__(kRaysBlock) void geo_rays_kernel(const RaysArgs a) {
-#endif
     const uint32_t c = blockIdx.x * kRaysBlock + threadIdx.x;
     if (c >= a.n_conn) return;
     // connector c: point c mod n, near side (less_than_180) first
@@ -157,14 +118,13 @@ __global__ __launch_bounds__(kRaysBlock) void geo_rays_kernel(const RaysArgs a) 
     const float* src = RESPAWN ? a.respawn_pos : a.pos;
     const float px = src[p], py = src[n + p], pz = src[2 * n + p];
     const bool reset = RESPAWN || a.reset != 0;
-#if GEO_RAYS_TILED == 2
     // node quads in 64-connector tiles, u[(c/64)*48*64 + (i/4)*256 + (c%64)*4 + i%4]: a lane moves
     // its 48 nodes with 12 16-B loads and stores, a wave's quad q is one contiguous 1-KB block.
     // Without a reset pending, ray_connect reads every node (the jump test reads node 0 first),
     // so they are loaded up front; with one, none is read.
     float* const ug = a.u + (size_t)(c / 64u) * (geo::kRayNodes * 64u) + (c % 64u) * 4u;
     float v[geo::kRayNodes];
-    if (GEO_RAYS_NOCOMPUTE || (!reset && !needs)) {
+    if (!reset && !needs) {
 #pragma unroll
         for (int q = 0; q < geo::kRayNodes / 4; ++q) {
             const f4_ t = ld4_(ug + q * 256);
@@ -174,111 +134,13 @@ __global__ __launch_bounds__(kRaysBlock) void geo_rays_kernel(const RaysArgs a) 
             v[4 * q + 3] = t.w;
         }
     }
-#if GEO_RAYS_NOCOMPUTE  // diagnostic only: the memory traffic without the solve (outputs are wrong)
-    float angle = px + py + pz + ox + oy + oz;
-#pragma unroll
-    for (int i = 0; i < geo::kRayNodes; ++i) u[i] = v[i] + angle;
-#else
     const float angle = geo::ray_connect(a.rs, !far, px, py, pz, ox, oy, oz, reset, a.iterations, &needs,
                                          [&](int i) { return v[i]; }, u);
-#endif
 #pragma unroll
     for (int q = 0; q < geo::kRayNodes / 4; ++q)
         st4_(ug + q * 256, f4_{u[4 * q], u[4 * q + 1], u[4 * q + 2], u[4 * q + 3]});
-#else
-#if GEO_RAYS_TILED == 1
-    // node values in 64-connector tiles: a wave's 48 loads cover one contiguous 12-KB block
-    float* const ug = a.u + (size_t)(c / 64u) * (geo::kRayNodes * 64u) + (c % 64u);
-    const size_t stride = 64;
-#else
-    float* const ug = a.u + c;
-    const size_t stride = a.n_conn;
-#endif
-    const float angle = geo::ray_connect(a.rs, !far, px, py, pz, ox, oy, oz, reset, a.iterations, &needs,
-                                         [=](int i) { return ld_(ug + (size_t)i * stride); }, u);
-#pragma unroll
-    for (int i = 0; i < geo::kRayNodes; ++i) st_(ug + (size_t)i * stride, u[i]);
-#endif
     a.needs_reset[c] = needs ? 1 : 0;
     if (!RESPAWN && a.out) a.out[c] = make_float4(px, py, pz, angle);
-}
-
-#ifndef GEO_RAYS_PREFETCH
-#define GEO_RAYS_PREFETCH 0  // 1: geo_rays_pf_kernel for the regular pass (A/B switch)
-#endif
-#ifndef GEO_RAYS_PF_BLOCKS_PER_CU
-#define GEO_RAYS_PF_BLOCKS_PER_CU 12  // resident 1-wave blocks per CU (160 VGPRs: 3 waves/SIMD)
-#endif
-// The regular pass with the next tile's state in flight during the solve: a
-// grid of resident 1-wave blocks walks the 64-connector tiles; each tile's 48
-// node quads (12 KB) arrive in LDS by LDS-DMA (global_load_lds_dwordx4, one
-// 1-KB quad per wave instruction, lane-linear = the tile's own layout) issued
-// before the previous tile's solve.  Small per-connector inputs use ordinary
-// loads, waited before the DMA is issued (hipcc would otherwise drain the DMA
-// at their first use).
-__global__ __launch_bounds__(64) void geo_rays_pf_kernel(const RaysArgs a, uint32_t n_tiles) {
-    __shared__ __attribute__((aligned(16))) float s_u[geo::kRayNodes * 64];
-    const uint32_t lane = threadIdx.x;
-    const uint32_t n = a.n_points;
-    auto prefetch = [&](uint32_t tile) {
-        const float* src = a.u + (size_t)tile * (geo::kRayNodes * 64u) + lane * 4u;
-#pragma unroll
-        for (int q = 0; q < geo::kRayNodes / 4; ++q)
-            __builtin_amdgcn_global_load_lds(src + q * 256, (__attribute__((address_space(3))) void*)(s_u + q * 256),
-                                             16, 0, GEO_RAYS_NT ? 2 : 0);
-    };
-    uint32_t t = blockIdx.x;
-    if (t < n_tiles) prefetch(t);
-    for (; t < n_tiles; t += gridDim.x) {
-        const uint32_t c = t * 64u + lane;
-        const bool live = c < a.n_conn;
-        const uint32_t cc = live ? c : 0u;
-        const bool far = a.sides == GEO_RAYS_FAR ? true : cc >= n;
-        const uint32_t p = cc >= n ? cc - n : cc;
-        bool needs = a.needs_reset[cc] != 0;
-        float ox = a.ox, oy = a.oy, oz = a.oz;
-        if (a.other) {
-            ox = a.other[3 * (size_t)p];
-            oy = a.other[3 * (size_t)p + 1];
-            oz = a.other[3 * (size_t)p + 2];
-        }
-        float px = a.pos[p], py = a.pos[n + p], pz = a.pos[2 * n + p];
-        GEO_OPAQUE(px);
-        GEO_OPAQUE(py);
-        GEO_OPAQUE(pz);
-        GEO_OPAQUE(ox);
-        GEO_OPAQUE(oy);
-        GEO_OPAQUE(oz);
-        uint32_t nb = needs ? 1u : 0u;
-        GEO_OPAQUE(nb);
-        needs = nb != 0;
-        // this tile's DMA (issued one tile ago) and the previous stores
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const bool reset = a.reset != 0;
-        float v[geo::kRayNodes];
-        if (!reset && !needs) {  // as geo_rays_kernel: no node is read when a reset is pending
-#pragma unroll
-            for (int q = 0; q < geo::kRayNodes / 4; ++q) {
-                const float4 w = *reinterpret_cast<const float4*>(s_u + q * 256 + lane * 4);
-                v[4 * q] = w.x;
-                v[4 * q + 1] = w.y;
-                v[4 * q + 2] = w.z;
-                v[4 * q + 3] = w.w;
-            }
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // LDS read before the DMA rewrites it
-        if (t + gridDim.x < n_tiles) prefetch(t + gridDim.x);
-        if (!live) continue;
-        float u[geo::kRayNodes];
-        const float angle = geo::ray_connect(a.rs, !far, px, py, pz, ox, oy, oz, reset, a.iterations, &needs,
-                                             [&](int i) { return v[i]; }, u);
-        float* const ug = a.u + (size_t)t * (geo::kRayNodes * 64u) + lane * 4u;
-#pragma unroll
-        for (int q = 0; q < geo::kRayNodes / 4; ++q)
-            st4_(ug + q * 256, f4_{u[4 * q], u[4 * q + 1], u[4 * q + 2], u[4 * q + 3]});
-        a.needs_reset[c] = needs ? 1 : 0;
-        if (a.out) a.out[c] = make_float4(px, py, pz, angle);
-    }
 }
 
 // PointCloud::update, orbit half (point_cloud.rs:119-141): step, then respawn
@@ -435,17 +297,7 @@ int rays_launch(geo_rays* r, float ox, float oy, float oz, const float* other_de
         hipLaunchKernelGGL(geo_rays_kernel<true>, grid, dim3(kRaysBlock), 0, s, a);
         if (hipGetLastError() != hipSuccess) return GEO_EHIP;
     }
-#if GEO_RAYS_PREFETCH && GEO_RAYS_TILED == 2
-    {
-        const uint32_t n_tiles = (r->n_conn + 63u) / 64u;
-        int cus = 256;
-        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, r->device);
-        const uint32_t blocks = std::min<uint32_t>(n_tiles, (uint32_t)cus * GEO_RAYS_PF_BLOCKS_PER_CU);
-        hipLaunchKernelGGL(geo_rays_pf_kernel, dim3(blocks), dim3(64), 0, s, a, n_tiles);
-    }
-#else
     hipLaunchKernelGGL(geo_rays_kernel<false>, grid, dim3(kRaysBlock), 0, s, a);
-#endif
     return hipGetLastError() == hipSuccess ? GEO_OK : GEO_EHIP;
 }
 

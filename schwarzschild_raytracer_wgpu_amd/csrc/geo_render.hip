@@ -27,54 +27,33 @@
 #include "geo_ctx.h"
 #include "geo_pixel.h"
 
-// fan mode: 0 reads the two nodes of a pixel's lerp from the context's
-// device copy (1.6 KB for 400 nodes, cache-resident; as the reference's
-// shader reads its fan texture); 1 stages the fan in LDS per workgroup, a
-// global load and a barrier before any pixel work: 6 % slower at 4K
-// (0.0464 vs 0.0492 ms)
-#ifndef GEO_FAN_LDS
-#define GEO_FAN_LDS 0
-#endif
-#ifndef GEO_BH_SKIP_UV
-#define GEO_BH_SKIP_UV 1
-#endif
-// A workgroup's tile: GEO_TILE_WAVES_X waves side by side, GEO_TILE_H rows
-// (a multiple of a wave's rows).  32 x 8: a tile row spans 32 sky
-// texels = one 128-B line, so neighbouring waves share their sky lines in one
-// CU instead of fetching them on up to 4 XCDs' L2s (102.8 -> 59.5 MB of L2
-// fabric reads per 4K frame, config 3 -2 to -5 %, config 5 -2 %, config 2
-// -1.5 % against 8 x 32; 16 x 16, 64 x 8 and 32 x 16 in between)
-#ifndef GEO_TILE_H
-#define GEO_TILE_H 8
-#endif
-#ifndef GEO_TILE_WAVES_X
-#define GEO_TILE_WAVES_X 2
-#endif
-// pixels across one wave, 64 / GEO_WAVE_W rows: 16 x 4 in the 32 x 8 tile
-// (-0.5 % on config 3 against four 8 x 8 squares, configs 5 and 2 the same;
-// 32 x 2 is +2.5 %)
-#ifndef GEO_WAVE_W
-#define GEO_WAVE_W 16
-#endif
-// consecutive tiles per XCD run (xcd_tile; 0 or 1: the hardware's round-robin)
-#ifndef GEO_XCD_CHUNK
-#define GEO_XCD_CHUNK 1
-#endif
+// Work decomposition (measured): 32 x 8-pixel workgroup tiles
+// of 2 x 2 waves of 16 x 4 pixels.  A tile row spans 32 sky texels = one
+// 128-B line, so neighbouring waves share their sky lines in one CU instead of
+// fetching them on up to 4 XCDs' L2s (102.8 -> 59.5 MB of L2 fabric reads per
+// 4K frame against 8 x 32 tiles; config 3 -2 to -5 %, config 5 -2 %, config 2
+// -1.5 %; 16 x 16, 64 x 8 and 32 x 16 in between); the 16 x 4 wave shape is
+// -0.5 % on config 3 against 8 x 8, 32 x 2 is +2.5 % (steps diverge more
+// within a wave).  Tiles keep the hardware's round-robin placement over the
+// XCDs: runs of consecutive tiles per XCD were slower on every config.  The
+// fan (fan mode) is read from its cache-resident device copy: staging it in
+// LDS per workgroup put a load and a barrier before every block's pixel work
+// (+6 % per 4K fan-mode frame).
 
 namespace {
 
-constexpr int kWaveW = GEO_WAVE_W;      // a wave64 covers a compact 16x4 block (few divergent
+constexpr int kWaveW = 16;             // a wave64 covers a compact 16x4 block (few divergent
 constexpr int kWaveRows = 64 / kWaveW;  // steps per wave; tools/ubench/loop_ab.hip)
-constexpr int kWavesX = GEO_TILE_WAVES_X;  // waves side by side in a tile
+constexpr int kWavesX = 2;              // waves side by side in a tile
 constexpr int kTileW = kWaveW * kWavesX;
-constexpr int kTileH = GEO_TILE_H;  // a block kTileW x kTileH
+constexpr int kTileH = 8;               // a block kTileW x kTileH
 constexpr int kBlock = kTileW * kTileH;  // 256 threads = 4 waves (32 x 8, 2 x 2 waves of 16 x 4)
 static_assert(kTileH % kWaveRows == 0 && kBlock % 64 == 0, "tile of whole waves");
 // band heights are multiples of 8 (the C-ABI's contract, geo.h), so a wave's
 // rows never straddle a band for any wave shape up to 8 rows
 constexpr uint32_t kBandRowAlign = 8;
 static_assert(kBandRowAlign % kWaveRows == 0, "a wave's rows lie in one band");
-constexpr uint32_t kMaxFan = 4096;       // LDS fan capacity (16 KiB)
+constexpr uint32_t kMaxFan = 4096;       // fan nodes (16 KiB)
 constexpr int kStepSlots = 256;          // sharded step counters (one per 128-B line)
 constexpr int kSlotStride = 16;          // u64 per slot = 128 B (own cache line)
 constexpr size_t kSlotSetU64 = (size_t)kStepSlots * kSlotStride;  // one set of sharded counters
@@ -145,11 +124,9 @@ __device__ __forceinline__ void shade_pixel(const RenderArgs& a, float c2x, floa
     const bool bh = lam < geo::kBlackHoleLambda;
     // A black-hole pixel is discarded (shader.wgsl:88): it needs its UV
     // only when the caller asks for it, so a wave inside the shadow skips
-    // the sincos/atan2/asin and the sample (GEO_BH_SKIP_UV 0: always compute)
+    // the sincos/atan2/asin and the sample (config 3 -0.3 %, config 5 -4.4 %)
     float U = 0.0f, V = 0.0f;
-#if GEO_BH_SKIP_UV
     if (!bh || a.out_uv)
-#endif
         geo::sky_uv(a.frame.central_to_uv, c2x, c2y, ct, rct, lam, &U, &V);
     const PaddedSkyQuad quad{__builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(a.sky), 0,
                                                                (int)a.sky_bytes, kBufferRsrcWord3),
@@ -168,40 +145,9 @@ __device__ __forceinline__ void shade_pixel(const RenderArgs& a, float c2x, floa
     if (a.out_steps) a.out_steps[o] = steps;
 }
 
-// Workgroups are dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md,
-// "blocks b and b + 8 share one"), each with its own L2.  The remap hands
-// each XCD runs of GEO_XCD_CHUNK consecutive tiles (chunk c to the XCD of
-// c % 8), so neighbouring tiles share an L2's sky lines; every XCD still gets
-// every 8th chunk of the frame.  Off by default: with 8 x 32 tiles, chunks of
-// 4-16 cut the fabric reads as the 32 x 8 tile does but timed -1 % on config
-// 3 and +2-4 % on config 2; on 32 x 8 tiles chunks of 4 are slower on every
-// config.  Bijective: the first n - n % (8 * chunk)
-// workgroups are permuted among themselves, the rest keep their own tile.
-// Placement only changes speed.
-template <uint32_t kC>
-__device__ __forceinline__ uint2 xcd_tile() {
-    if constexpr (kC <= 1) return make_uint2(blockIdx.x, blockIdx.y);
-    constexpr uint32_t kSpan = 8u * kC;
-    const uint32_t gx = gridDim.x, n = gx * gridDim.y;
-    const uint32_t l = blockIdx.y * gx + blockIdx.x;
-    uint32_t t = l;
-    if (l < n - n % kSpan) {
-        const uint32_t q = l / 8u;
-        t = ((q / kC) * 8u + l % 8u) * kC + q % kC;
-    }
-    return make_uint2(t % gx, t / gx);
-}
-
 template <int MODE, int KIND>
 __global__ __launch_bounds__(kBlock) void geo_render_kernel(const RenderArgs a) {
-#if GEO_FAN_LDS
-    __shared__ float s_fan[MODE == GEO_MODE_FAN ? kMaxFan : 1];
-    if constexpr (MODE == GEO_MODE_FAN) {
-        for (uint32_t i = threadIdx.x; i < a.n_fan; i += kBlock) s_fan[i] = a.fan[i];
-        __syncthreads();
-    }
-#endif
-    const uint2 tile = xcd_tile<GEO_XCD_CHUNK>();
+    const uint2 tile = make_uint2(blockIdx.x, blockIdx.y);
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x) >> 6;
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t px = tile.x * kTileW + (wave % kWavesX) * kWaveW + lane % kWaveW;
@@ -222,15 +168,11 @@ __global__ __launch_bounds__(kBlock) void geo_render_kernel(const RenderArgs a) 
         const float rct = geo::rcpf_(ct);  // shared by the ray's 1/b^2 and its sky direction
         float lam;
         if constexpr (MODE == GEO_MODE_FAN) {
-#if GEO_FAN_LDS
-            lam = geo::fan_lerp(s_fan, a.n_fan, st);
-#else
             lam = geo::fan_lerp(a.fan, a.n_fan, st);
-#endif
         } else if constexpr (MODE == GEO_MODE_ADAPTIVE) {
             lam = geo::kPi2 - geo::geodesic_angle_adaptive<KIND>(a.k, st, ct, rct, &steps);
         } else {
-            lam = geo::kPi2 - geo::geodesic_angle_v<GEO_LOOP_VARIANT, KIND>(a.k, st, ct, rct, &steps);
+            lam = geo::kPi2 - geo::geodesic_angle_v<KIND>(a.k, st, ct, rct, &steps);
         }
         shade_pixel(a, c2x, c2y, ct, rct, lam, steps, (size_t)ly * a.width + px);
     }
@@ -404,71 +346,8 @@ __device__ bool solve_geodesic_f64_init(double sphere_r, double schwarz_r, doubl
     return true;
 }
 
-// The literal main loop (:121-193) from the initial state (GEO_FAN_LITERAL 1).
-__device__ double solve_geodesic_f64_loop(double sphere_r, double schwarz_r, uint32_t max_iter,
-                                          double default_step, double r, double u_bar0) {
-    const double NO_VALUE = GEO_NO_VALUE;
-    const double r3_2 = 3. * schwarz_r / 2.;
-    double u_k = 1. / r;
-    double u_bar_k = u_bar0;
-    double angle = 0.;
-    uint32_t iteration = 0;
-    const double bound = 0.9 * fmin(u_k, 1. / fmax(sphere_r, r3_2));
-    const double step = default_step;
-    const double step_half = step / 2.;
-    const double sphere_u = 1. / sphere_r;
-    const double schwarz_u = 1. / schwarz_r;
-    while (!(schwarz_r != 0. && u_k > schwarz_u && u_bar_k > 0.) && iteration < max_iter &&
-           u_k > 0.) {
-        double a_u = u_k + step_half * u_bar_k;
-        double a_u_bar = u_bar_k + step_half * (-u_k + r3_2 * u_k * u_k);
-        double b_u = u_k + step_half * a_u_bar;
-        double b_u_bar = u_bar_k + step_half * (-a_u + r3_2 * a_u * a_u);
-        double c_u = u_k + step * b_u_bar;
-        double c_u_bar = u_bar_k + step * (-b_u + r3_2 * b_u * b_u);
-        const double next_u = u_k + step * (u_bar_k + 2. * a_u_bar + 2. * b_u_bar + c_u_bar) / 6.;
-        const double next_u_bar =
-            u_bar_k + step * ((-u_k + r3_2 * u_k * u_k) + 2. * (-a_u + r3_2 * a_u * a_u) +
-                              2. * (-b_u + r3_2 * b_u * b_u) + (-c_u + r3_2 * c_u * c_u)) / 6.;
-        if ((next_u > sphere_u) != (u_k > sphere_u)) {
-            double newton_u, newton_u_bar, newton_step;
-            if (fabs(u_bar_k) > fabs(next_u_bar)) {
-                newton_step = 0.;
-                newton_u = u_k;
-                newton_u_bar = u_bar_k;
-            } else {
-                newton_step = step;
-                newton_u = next_u;
-                newton_u_bar = next_u_bar;
-            }
-            for (int n = 0; n < 3; ++n) {
-                newton_step -= (newton_u - sphere_u) / newton_u_bar;
-                const double nsh = newton_step / 2.;
-                a_u = u_k + nsh * u_bar_k;
-                a_u_bar = u_bar_k + nsh * (-u_k + r3_2 * u_k * u_k);
-                b_u = u_k + nsh * a_u_bar;
-                b_u_bar = u_bar_k + nsh * (-a_u + r3_2 * a_u * a_u);
-                c_u = u_k + newton_step * b_u_bar;
-                c_u_bar = u_bar_k + newton_step * (-b_u + r3_2 * b_u * b_u);
-                newton_u = u_k + newton_step * (u_bar_k + 2. * a_u_bar + 2. * b_u_bar + c_u_bar) / 6.;
-                newton_u_bar = u_bar_k + newton_step *
-                                             ((-u_k + r3_2 * u_k * u_k) + 2. * (-a_u + r3_2 * a_u * a_u) +
-                                              2. * (-b_u + r3_2 * b_u * b_u) + (-c_u + r3_2 * c_u * c_u)) /
-                                             6.;
-            }
-            return angle + newton_step;
-        }
-        if (next_u < bound) return NO_VALUE;
-        u_k = next_u;
-        u_bar_k = next_u_bar;
-        iteration += 1;
-        angle += step;
-    }
-    return NO_VALUE;
-}
-
-// The same f64 solve, restructured for latency (GEO_FAN_LITERAL 0, the
-// default).  A fan is one lane per node, 400 lanes = 7 waves, so its time is
+// The f64 solve (sphere_ray_tracer.rs:121-193), restructured for latency.
+// A fan is one lane per node, 400 lanes = 7 waves, so its time is
 // the longest node's dependent chain: the literal loop spends ~60 f64
 // instructions per step (two f64 divisions by 6 among them), this one the
 // scaled 14-op RK4 of the f32 kernel (geo_pixel.h rk4_step) in f64 --
@@ -477,9 +356,6 @@ __device__ double solve_geodesic_f64_loop(double sphere_r, double schwarz_r, uin
 // algorithm (stages, tests, Newton) with a different rounding of the f64
 // intermediates: the fan agrees with the literal f64 restatement to within
 // one f32 ulp (tests/test_gpu_parity.py, the fan tolerance).
-#ifndef GEO_FAN_LITERAL
-#define GEO_FAN_LITERAL 0
-#endif
 template <bool FLAT>
 __device__ __forceinline__ double fan_F(double U) {
     return FLAT ? -U : __builtin_fma(U, U, -U);
@@ -512,11 +388,9 @@ __device__ __forceinline__ int fan_test(double U, double V, double NU, double SU
 // (which waits for the newest state's compares) is taken once per kFanGroup
 // steps: the group's flags are formed without branches, and a group that
 // stops is replayed step by step from its start (the same arithmetic, so the
-// same result as testing every step).
-#ifndef GEO_FAN_GROUP
-#define GEO_FAN_GROUP 4
-#endif
-constexpr int kFanGroup = GEO_FAN_GROUP;
+// same result as testing every step).  Groups of 8 and 16 are +-4 % and up
+// to +22 %.
+constexpr int kFanGroup = 4;
 template <bool FLAT>
 __device__ double fan_integrate(double sphere_r, double schwarz_r, uint32_t max_iter, double step, double r,
                                 double u_bar0) {
@@ -605,12 +479,8 @@ __global__ void geo_fan_kernel(double sphere_r, double schwarz_r, uint32_t max_i
     }
     double angle, u_bar0;
     if (solve_geodesic_f64_init(sphere_r, schwarz_r, r, energy, rotation, r_falling, &angle, &u_bar0)) {
-#if GEO_FAN_LITERAL
-        angle = solve_geodesic_f64_loop(sphere_r, schwarz_r, max_iter, step, r, u_bar0);
-#else
         angle = schwarz_r == 0. ? fan_integrate<true>(sphere_r, schwarz_r, max_iter, step, r, u_bar0)
                                 : fan_integrate<false>(sphere_r, schwarz_r, max_iter, step, r, u_bar0);
-#endif
     }
     fan[i] = (float)(FRAC_PI_2 - angle);
 }

@@ -13,7 +13,8 @@ from schwarzschild_raytracer_wgpu_amd._lib import GEO_MODE_ADAPTIVE, GEO_MODE_DI
 # seeds that once differed, kept in both fuzz tests: 70751 (64 x 36, step 0.093,
 # observer inside the photon sphere) has a near-radial outgoing ray whose first
 # RK4 step overshoots U = 0 and is pushed back above the sphere within its group
-# of 4 (the once-per-group test's absorbing assumption; geo_pixel.h kRiskK)
+# of 4 (round 2's last-state-only group test; now the exact group test of
+# geo_pixel.h group_stop_)
 REGRESSION_SEEDS = (70751,)
 
 KINDS = ("sky", "near_ring", "inside_photon_sphere", "inside_horizon", "flat", "outside_sphere", "small_sphere")
@@ -61,5 +62,48 @@ def random_scene(seed: int, w: int, h: int, adaptive: bool = False):
     else:
         scene = make_scene(rs, sphere_r, o.get_radial_position(), step, max_steps, GEO_MODE_DIRECT)
     desc = (f"seed={seed} kind={kind} r={r:.4f} sphere_r={sphere_r:.3f} rs={rs} fov={fov:.3f} "
+            f"unmoving={unmoving} steps={max_steps} step={step:.4f} adaptive={adaptive}")
+    return frame, scene, desc
+
+
+def adversarial_scene(seed: int, w: int, h: int, adaptive: bool = False):
+    """(frame, scene, description): the rays that break a group exit test
+    which reads fewer states than the per-step test.  The observer sits on the
+    x axis looking away from the black hole through a narrow field of view, so
+    the frame's rays are near-radial outgoing ones (theta ~ -pi/2, |U'| up to
+    ~1e9): with a large step their first RK4 step carries U far below 0, where
+    F(U) = U^2 - U > 0 pushes it back up within a group.  Odd seeds look at
+    the black hole instead (falling rays entering U > HU at large steps).  Steps span 0.01..3
+    (the fast kCurvedOut kind up to 1/2, the general kCurvedIn test beyond);
+    budgets 1..4096."""
+    rng = np.random.default_rng(seed)
+    rs = 1.0
+    sphere_r = 50.0 if rng.random() < 0.75 else float(rng.uniform(1.05, 3.0))
+    hi = min(40.0, sphere_r * 0.99)
+    lo = 1.01 if rng.random() < 0.3 or hi <= 1.6 else 1.6
+    r = float(rng.uniform(lo, hi))
+    # odd seeds look at the black hole instead, through a wider view: falling
+    # rays at large steps, which enter U > HU (the horizon side of the test)
+    toward = seed % 2 == 1
+    off = 10.0 ** rng.uniform(-7.0, -2.0)
+    fov = float(10.0 ** rng.uniform(-3.0, 0.3)) if toward else float(10.0 ** rng.uniform(-6.0, -1.0))
+    o = Observer(rs, fov, w, h)
+    o.set_position(r, 0.0, 0.0)
+    o.set_camera(float(rng.normal(math.pi if toward else 0.0, off)), float(rng.normal(0.0, off)))
+    o.set_energy(float(rng.uniform(1.0, 1.6)))
+    unmoving = rng.random() < 0.3
+    if unmoving:
+        o.start_unmoving()
+    else:
+        o.start_frozen_fall()
+    frame = o.calc_transformation_pipeline()
+    max_steps = int(rng.choice([1, 2, 3, 4, 5, 7, 8, 9, 17, 300, 2048, 4096]))
+    step = float(10.0 ** rng.uniform(-2.0, math.log10(3.0)))
+    if adaptive:
+        tol = float(10.0 ** rng.uniform(-7.5, -4.0)) if rng.random() < 0.8 else 0.0
+        scene = make_scene(rs, sphere_r, o.get_radial_position(), step, max_steps, GEO_MODE_ADAPTIVE, tol=tol)
+    else:
+        scene = make_scene(rs, sphere_r, o.get_radial_position(), step, max_steps, GEO_MODE_DIRECT)
+    desc = (f"adversarial seed={seed} toward={toward} r={r:.4f} sphere_r={sphere_r:.3f} fov={fov:.2e} off={off:.1e} "
             f"unmoving={unmoving} steps={max_steps} step={step:.4f} adaptive={adaptive}")
     return frame, scene, desc

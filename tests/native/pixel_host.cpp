@@ -10,9 +10,9 @@
 template <int LOOP>
 static float geo_v(const geo::PixelConsts& k, float st, float ct, float rct, uint32_t* n) {
     switch (geo::geodesic_kind(k)) {
-        case geo::kCurvedOut: return geo::geodesic_angle_v<LOOP, geo::kCurvedOut>(k, st, ct, rct, n);
-        case geo::kCurvedIn: return geo::geodesic_angle_v<LOOP, geo::kCurvedIn>(k, st, ct, rct, n);
-        default: return geo::geodesic_angle_v<LOOP, geo::kFlat>(k, st, ct, rct, n);
+        case geo::kCurvedOut: return geo::geodesic_angle_v<geo::kCurvedOut, LOOP>(k, st, ct, rct, n);
+        case geo::kCurvedIn: return geo::geodesic_angle_v<geo::kCurvedIn, LOOP>(k, st, ct, rct, n);
+        default: return geo::geodesic_angle_v<geo::kFlat, LOOP>(k, st, ct, rct, n);
     }
 }
 

@@ -18,13 +18,13 @@ static float angle_for(const geo::PixelConsts& k, uint32_t mode, float st, float
     switch (geo::geodesic_kind(k)) {
         case geo::kCurvedOut:
             return mode == GEO_MODE_ADAPTIVE ? geo::geodesic_angle_adaptive<geo::kCurvedOut>(k, st, ct, rct, n)
-                                             : geo::geodesic_angle_v<4, geo::kCurvedOut>(k, st, ct, rct, n);
+                                             : geo::geodesic_angle_v<geo::kCurvedOut>(k, st, ct, rct, n);
         case geo::kCurvedIn:
             return mode == GEO_MODE_ADAPTIVE ? geo::geodesic_angle_adaptive<geo::kCurvedIn>(k, st, ct, rct, n)
-                                             : geo::geodesic_angle_v<4, geo::kCurvedIn>(k, st, ct, rct, n);
+                                             : geo::geodesic_angle_v<geo::kCurvedIn>(k, st, ct, rct, n);
         default:
             return mode == GEO_MODE_ADAPTIVE ? geo::geodesic_angle_adaptive<geo::kFlat>(k, st, ct, rct, n)
-                                             : geo::geodesic_angle_v<4, geo::kFlat>(k, st, ct, rct, n);
+                                             : geo::geodesic_angle_v<geo::kFlat>(k, st, ct, rct, n);
     }
 }
 

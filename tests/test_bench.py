@@ -35,7 +35,7 @@ def test_bench_short_run_prints_the_contract_line():
     if not torch.cuda.is_available():
         pytest.skip("no HIP device")
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "20", "--warmup", "5",
-                        "--spinup-frames", "60", "--cpu-seconds", "0.2"],
+                        "--spinup-frames", "60", "--cpu-row-step", "8"],
                        cwd=ROOT, capture_output=True, text=True, timeout=110)
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
@@ -56,4 +56,7 @@ def test_bench_short_run_prints_the_contract_line():
     assert abs(rf["achieved"] - rf["algorithmic_flops_per_launch"] / (d["kernel_ms"]["avg"] * 1e-3) / 1e12) < 1e-6
     assert 0.3 < rf["frac"] < 1.0
     cb = d["cpu_baseline"]
-    assert cb["kind"] == "port" and cb["cores"] >= 1 and cb["value"] > 0
+    assert cb["kind"] == "port" and cb["cores"] >= 1 and cb["value"] > 0 and cb["cpu_model"]
+    assert len(cb["seconds_per_run"]) == 3
+    # the frames of the timed run's last batch equal a single-launch frame
+    assert d["frame_check"]["ok"] is True and d["frame_check"]["frames"] >= 1

@@ -7,7 +7,7 @@ import numpy as np
 import pytest
 
 import oracle as O
-from fuzz_scenes import REGRESSION_SEEDS, random_scene
+from fuzz_scenes import REGRESSION_SEEDS, adversarial_scene, random_scene
 from test_gpu_parity import geo, make_ctx, render, torch_mod  # noqa: F401  (fixtures)
 
 pytestmark = pytest.mark.gpu
@@ -36,6 +36,30 @@ def test_gpu_fuzz_bitexact(geo, torch_mod, adaptive):  # noqa: F811
             bad.append(desc)
     print(f"fuzz {'adaptive' if adaptive else 'direct'}: {len(seeds)} scenes at {W}x{H}, {len(bad)} differ")
     assert not bad, f"{len(bad)} of {len(seeds)} scenes differ: {bad[:5]}"
+
+
+@pytest.mark.parametrize("adaptive", [False, True], ids=["direct", "adaptive"])
+def test_gpu_fuzz_adversarial_bitexact(geo, torch_mod, adaptive):  # noqa: F811
+    """Near-radial outgoing rays and falling rays at large steps
+    (fuzz_scenes.adversarial_scene: steps 0.01..3, budgets 1..4096): the
+    exact group exit test against the oracle's literal per-step loop."""
+    from schwarzschild_raytracer_wgpu_amd.scenes import make_sky
+
+    sky = make_sky("equirect", (256, 128))
+    ctx = make_ctx(geo, sky)
+    bad = []
+    n = int(os.environ.get("GEO_FUZZ_N", 400 if not adaptive else 200))
+    base = int(os.environ.get("GEO_FUZZ_BASE", 0))
+    for seed in range(base, base + n):
+        frame, scene, desc = adversarial_scene(seed, W, H, adaptive=adaptive)
+        hip = render(geo, torch_mod, ctx, frame, scene, W, H)
+        ref = O.render_f32(frame, scene, sky, W, H, threads=4)
+        same = all(np.array_equal(hip[f], ref[f]) for f in ("mask", "steps", "rgba")) and np.array_equal(
+            hip["uv"].view(np.uint32), ref["uv"].view(np.uint32)) and hip["total"] == ref["steps_total"]
+        if not same:
+            bad.append(desc)
+    print(f"fuzz adversarial {'adaptive' if adaptive else 'direct'}: {n} scenes at {W}x{H}, {len(bad)} differ")
+    assert not bad, f"{len(bad)} of {n} scenes differ: {bad[:5]}"
 
 
 def test_gpu_fuzz_fan_mode_bitexact(geo, torch_mod):  # noqa: F811

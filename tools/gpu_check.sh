@@ -11,7 +11,7 @@ TAG=${1:-r01}
 
 fatal() { local rc=$1; [ "$rc" -ge 124 ] || [ "$rc" -ge 128 ]; }
 
-timeout -k 10 420 python -m pytest tests -m gpu -q -rf > "$OUT/pytest_gpu_$TAG.log" 2>&1
+GEO_F64_BAR_OUT="$OUT/f64bar_$TAG" timeout -k 10 420 python -u -m pytest tests -m gpu -q -rf --timeout 120 --timeout-method thread > "$OUT/pytest_gpu_$TAG.log" 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -5 "$OUT/pytest_gpu_$TAG.log"
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 

@@ -351,8 +351,13 @@ def main():
         return
 
     value = total_steps / elapsed_max
-    # roofline for the dominant kernel, on this rank: algorithmic flops per launch / avg launch time
+    # roofline for the dominant kernel, on this rank: algorithmic flops per
+    # launch / avg launch time (event pairs, which add ~2 % to what they time:
+    # DESIGN.md §4), and the same flops per frame of the compute-only pass's
+    # wall time (no events; includes launch gaps)
     achieved_tflops = flops_per_launch / (kernel_ms_avg * 1e-3) / 1e12
+    wall_tflops = flops_per_launch / (compute_max / args.steps) / 1e12
+    pmc_file, pmc = pmc_profile(args.config, args.mode, world)
     if mode == g.GEO_MODE_ADAPTIVE:
         metric = (f"geodesic-step-attempts·pixels/sec at {W}x{H}, adaptive RK5(4) tol {cfg.tol:g} "
                   f"(whole job; /GPU = value/n_gpus)")
@@ -412,10 +417,21 @@ def main():
             "peak": PEAK_FP32_TFLOPS,
             "unit": "TFLOP/s",
             "frac": achieved_tflops / PEAK_FP32_TFLOPS,
-            "traffic": pmc_traffic(args.config, args.mode, world),
+            "traffic": pmc.get("traffic_bytes"),
             "kernel": f"geo_render_kernel<{mode}>",
+            "flops": ("reference-equivalent algorithmic FP32 flops (FMA = 2): %s; the kernel executes fewer "
+                      "instructions for the same arithmetic (14 VALU per RK4 step), so frac is not hardware VALU "
+                      "utilisation: see hw_fp32_tflops_pmc and valu_per_simd_cycle_pmc"
+                      % ("77 per RK5(4) attempt, 67 per Newton evaluation" if mode == g.GEO_MODE_ADAPTIVE else
+                         "40 per RK4 evaluation of the reference's literal form, SURVEY.md §8d")),
             "algorithmic_flops_per_launch": flops_per_launch,
             "evals_per_launch": evals_per_launch,
+            "achieved_wall": wall_tflops,
+            "frac_wall": wall_tflops / PEAK_FP32_TFLOPS,
+            "wall": "flops per launch / (compute-only wall time per frame): no event pairs, launch gaps included",
+            "hw_fp32_tflops_pmc": pmc.get("hw_fp32_tflops"),
+            "valu_per_simd_cycle_pmc": pmc.get("valu_per_simd_cycle"),
+            "pmc_profile": pmc_file,
         },
     }
     if world == 1 and not args.no_cpu_baseline and mode != g.GEO_MODE_FAN:
@@ -470,24 +486,24 @@ def present_link_probe(sf, dist, args, reps=10):
             "per_peer_gb_s": nbytes / dt / 1e9, "into_rank0_gb_s": nbytes * (sf.world - 1) / dt / 1e9}
 
 
-def pmc_traffic(config, mode, world):
-    """HBM bytes per launch of the render kernel from the committed rocprofv3
-    PMC summary of this workload (profiles/*_<config>_pmc.json, made by
-    tools/gpu_pmc.sh + tools/pmc_to_profile.py), or None.  Only a profile
-    taken on this exact workload counts: same config, same mode (its
-    workload string ends in ", <mode>)"), one GPU (the profiles hold
-    full-frame bytes; at N > 1 a launch renders a partial share)."""
+def pmc_profile(config, mode, world):
+    """The committed rocprofv3 PMC summary of this workload
+    (profiles/*_<config>_pmc.json, made by tools/gpu_pmc.sh +
+    tools/pmc_to_profile.py): (file name, its derived figures), or (None, {}).
+    Only a profile taken on this exact workload counts: same config, same
+    mode (its workload string ends in ", <mode>)"), one GPU (the profiles
+    hold full-frame figures; at N > 1 a launch renders a partial share)."""
     import glob
 
     if world != 1:
-        return None
+        return None, {}
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_{config}_pmc.json")))
     for path in reversed(files):
         with open(path) as f:
             d = json.load(f)
         if d.get("workload", "").startswith(config) and d["workload"].endswith(f", {mode})"):
-            return d["derived"]["traffic_bytes"]
-    return None
+            return os.path.basename(path), d["derived"]
+    return None, {}
 
 
 def reference_fan_cost(ctx, cfg, r):

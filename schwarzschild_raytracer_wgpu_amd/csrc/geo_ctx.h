@@ -36,6 +36,17 @@ struct geo_ctx {
     hipEvent_t step_set_free[kStepCallSets];
     bool step_set_rec[kStepCallSets];
     int step_set_next;
+    // The last render of this context on each stream it has rendered on, so
+    // that a sky upload or a fan regrow waits for the renders that may read
+    // the buffer it replaces, and for nothing else (a device-wide wait would
+    // also wait for other contexts' work and for collectives in flight that
+    // need peers, which can hang a rank).  More than kRenderStreams streams:
+    // a new stream takes slot render_next after waiting for that slot's event,
+    // so the event it records covers the evicted stream's render too.
+    static constexpr int kRenderStreams = 8;
+    hipStream_t render_stream[kRenderStreams];
+    hipEvent_t render_done[kRenderStreams];
+    int n_render_streams, render_next;
 };
 
 // Makes `dev` current for the scope of a C-ABI call, restoring the caller's device.

@@ -428,6 +428,30 @@ GEO_HD void group_steps_(float u, float b, float h, float hh, float hh2, float h
         rk4_step<KIND>(j ? ou[j - 1] : u, j ? ob[j - 1] : b, h, hh, hh2, hhh, h6, h2_6, &ou[j], &ob[j]);
 }
 
+// IEEE minNum/maxNum of three floats (a NaN operand yields the min/max of the
+// others) as one v_min3_f32 / v_max3_f32.  hipcc lowers fminf chains on
+// loop-carried values with a canonicalising v_max_f32 x, x per operand first
+// (2 extra VALU per group, measured); the states are arithmetic results, never
+// signaling NaNs, so the canonicalisation is a no-op here.
+GEO_HD float min3_(float a, float b, float c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    float r;
+    asm("v_min3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+#else
+    return __builtin_fminf(__builtin_fminf(a, b), c);
+#endif
+}
+GEO_HD float max3_(float a, float b, float c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    float r;
+    asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+#else
+    return __builtin_fmaxf(__builtin_fmaxf(a, b), c);
+#endif
+}
+
 // The exit test of a group of G RK4 steps, exact: it holds iff the per-step
 // StopTest holds for one of the group's G states (the group's start state is
 // inside the interval, or the previous group would have stopped).  Three
@@ -437,14 +461,18 @@ GEO_HD void group_steps_(float u, float b, float h, float hh, float hh2, float h
 //             A state above hi = HU needs no test of its own: it has U' > 0,
 //             and U > HU with U' >= 0 maps to U' >= U, U'' >= U' under the
 //             f32 RK4 map (all stage values exceed 1, so every F >= 0), so
-//             state G is above HU too.  NaN propagates to state G.
+//             state G is above HU too.  A NaN state makes every later state
+//             NaN, state G included, which the range test sees (the minimum
+//             ignores NaN operands).
 //   kTestBoth (kCurvedOut/kFlat, observer outside the sphere): the minimum
 //             below lo or the maximum above hi (the ray can graze the sphere,
 //             entering and leaving within a group), or state G outside.
 //   kTestEach (kCurvedIn): the reference's compound test on every state.
-// (round 2 tested the last state alone, exact only while no state left the
-// interval and came back within a group, which a near-radial outgoing ray at
-// a large step breaks; the minimum costs 2 VALU per group more)
+// Round 2 tested state G alone, which is exact only while no state leaves the
+// interval and comes back within a group; a near-radial outgoing ray at a
+// large step breaks that (RK4 overshoots U = 0, where F(U) = U^2 - U > 0
+// turns it back: seed 70751).  For G = 4 the minimum is one v_min3_f32: 4
+// VALU per group against 2 for state G alone.
 // hipcc takes the ballot of a single compare as its mask but rebuilds any
 // other condition through a VGPR (two VALU), so the compares are balloted one
 // by one and ORed in scalar ops; the compound test is ORed first and balloted
@@ -461,18 +489,20 @@ GEO_HD uint64_t group_stop_(const StopTest<KIND>& stop_at, const float (&ou)[G],
         for (int j = 0; j < G; ++j) s = s | stop_at(ou[j], ob[j]);
         return ballot_(s);
     } else {
-        // the minimum of all G states (v_min3_f32: one op for G = 3, two for
-        // 4), NaN-free; a NaN state makes state G NaN, which `!(<= hi)` sees
-        float mn = ou[0];
-#pragma unroll
-        for (int j = 1; j < G; ++j) mn = __builtin_fminf(mn, ou[j]);
-        uint64_t m = ballot_(!(mn >= stop_at.lo)) | ballot_(!(ou[G - 1] <= stop_at.hi));
-        if constexpr (TEST == kTestBoth) {
-            float mx = ou[0];
-#pragma unroll
-            for (int j = 1; j < G - 1; ++j) mx = __builtin_fmaxf(mx, ou[j]);  // v_max3_f32
-            m |= ballot_(mx > stop_at.hi);
+        // states 1..G-1 (ou[0..G-2]): their minimum (and maximum)
+        float mn = ou[0], mx = ou[0];
+        int j = 1;
+        for (; j + 2 <= G - 1; j += 2) {
+            mn = min3_(mn, ou[j], ou[j + 1]);
+            if constexpr (TEST == kTestBoth) mx = max3_(mx, ou[j], ou[j + 1]);
         }
+        for (; j < G - 1; ++j) {
+            mn = __builtin_fminf(mn, ou[j]);
+            if constexpr (TEST == kTestBoth) mx = __builtin_fmaxf(mx, ou[j]);
+        }
+        const float last = ou[G - 1];
+        uint64_t m = ballot_(mn < stop_at.lo) | ballot_(med3_(last, stop_at.lo, stop_at.hi) != last);
+        if constexpr (TEST == kTestBoth) m |= ballot_(mx > stop_at.hi);
         return m;
     }
 }

@@ -427,7 +427,7 @@ int geo_points_create(geo_ctx* ctx, float schwarz_r, const float* model_xyz, uin
         st = GEO_EHIP;
     // reset_ray(observer_pos) for every connector (:43, :46)
     if (!st) st = rays_launch(r, observer_xyz[0], observer_xyz[1], observer_xyz[2], nullptr, 0u, 1, false, nullptr, 0);
-    if (!st && hipDeviceSynchronize() != hipSuccess) st = GEO_EHIP;
+    if (!st && hipStreamSynchronize(nullptr) != hipSuccess) st = GEO_EHIP;  // the reset above, not the device
     if (st) {
         for (hipEvent_t e : {p->updated, p->drawn})
             if (e) (void)hipEventDestroy(e);

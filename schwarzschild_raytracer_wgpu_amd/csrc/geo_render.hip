@@ -63,6 +63,7 @@ struct RenderArgs {
     geo_frame frame;
     geo::PixelConsts k;  // frame constants, evaluated once on the host (IEEE f32, same bits)
     uint32_t width, height, row0, nrows;
+    uint32_t tile_y0;  // first tile row of this launch (launch_tiles)
     // local row lr -> row0 + b*band_stride + (lr - b*band_rows), b = lr / band_rows
     // = umulhi(lr, band_magic) (band_rows_magic)
     uint32_t band_rows, band_magic, band_stride;
@@ -147,7 +148,7 @@ __device__ __forceinline__ void shade_pixel(const RenderArgs& a, float c2x, floa
 
 template <int MODE, int KIND>
 __global__ __launch_bounds__(kBlock) void geo_render_kernel(const RenderArgs a) {
-    const uint2 tile = make_uint2(blockIdx.x, blockIdx.y);
+    const uint2 tile = make_uint2(blockIdx.x, a.tile_y0 + blockIdx.y);
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x) >> 6;
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t px = tile.x * kTileW + (wave % kWavesX) * kWaveW + lane % kWaveW;
@@ -504,6 +505,12 @@ const char* geo_status_str(int status) {
     }
 }
 
+// The context's ordering events: no timestamps, and no system-scope fence
+// (they order device work on one device and let the host wait for it; a
+// system-scope release after every render writes back the caches again and
+// cost ~2 % per 4K frame)
+constexpr unsigned kCtxEventFlags = hipEventDisableTiming | hipEventDisableSystemFence;
+
 int geo_ctx_create(int device, geo_ctx** out) {
     if (!out) return GEO_EINVAL;
     *out = nullptr;
@@ -523,10 +530,12 @@ int geo_ctx_create(int device, geo_ctx** out) {
     c->fan_cur = -1;
     bool ok = true;
     for (int b = 0; b < 2 && ok; ++b)
-        ok = hipEventCreateWithFlags(&c->fan_written[b], hipEventDisableTiming) == hipSuccess &&
-             hipEventCreateWithFlags(&c->fan_read[b], hipEventDisableTiming) == hipSuccess;
+        ok = hipEventCreateWithFlags(&c->fan_written[b], kCtxEventFlags) == hipSuccess &&
+             hipEventCreateWithFlags(&c->fan_read[b], kCtxEventFlags) == hipSuccess;
     for (int i = 0; i < geo_ctx::kStepCallSets && ok; ++i)
-        ok = hipEventCreateWithFlags(&c->step_set_free[i], hipEventDisableTiming) == hipSuccess;
+        ok = hipEventCreateWithFlags(&c->step_set_free[i], kCtxEventFlags) == hipSuccess;
+    for (int i = 0; i < geo_ctx::kRenderStreams && ok; ++i)
+        ok = hipEventCreateWithFlags(&c->render_done[i], kCtxEventFlags) == hipSuccess;
     int st = ok ? GEO_OK : GEO_EHIP;
     if (ok && hipMalloc(&c->step_slots, sizeof(unsigned long long) * kSlotSetU64 * kSlotSets) != hipSuccess) {
         c->step_slots = nullptr;
@@ -543,6 +552,8 @@ int geo_ctx_create(int device, geo_ctx** out) {
         }
         for (int i = 0; i < geo_ctx::kStepCallSets; ++i)
             if (c->step_set_free[i]) (void)hipEventDestroy(c->step_set_free[i]);
+        for (int i = 0; i < geo_ctx::kRenderStreams; ++i)
+            if (c->render_done[i]) (void)hipEventDestroy(c->render_done[i]);
         delete c;
         return st;
     }
@@ -550,11 +561,50 @@ int geo_ctx_create(int device, geo_ctx** out) {
     return GEO_OK;
 }
 
+// The context's renders (and step flushes) in flight, on every stream it has
+// rendered on: after this, nothing of the context's reads the sky, the fan
+// buffers or the step counters.
+static int wait_renders(geo_ctx* c) {
+    for (int i = 0; i < c->n_render_streams; ++i)
+        if (hipEventSynchronize(c->render_done[i]) != hipSuccess) return GEO_EHIP;
+    return GEO_OK;
+}
+
+// The fan buffer b's last writer and readers.
+static int wait_fan(geo_ctx* c, int b) {
+    if (c->fan_written_rec[b] && hipEventSynchronize(c->fan_written[b]) != hipSuccess) return GEO_EHIP;
+    if (c->fan_read_rec[b] && hipEventSynchronize(c->fan_read[b]) != hipSuccess) return GEO_EHIP;
+    return GEO_OK;
+}
+
+// Records the context's latest work on stream s (geo_ctx::render_done).
+static int note_render(geo_ctx* c, hipStream_t s) {
+    int i = 0;
+    while (i < c->n_render_streams && c->render_stream[i] != s) ++i;
+    if (i == c->n_render_streams) {
+        if (c->n_render_streams < geo_ctx::kRenderStreams) {
+            ++c->n_render_streams;
+        } else {
+            // evict a slot: s first waits for its event, so the event s
+            // records next covers the evicted stream's last render as well
+            i = c->render_next;
+            c->render_next = (i + 1) % geo_ctx::kRenderStreams;
+            if (hipStreamWaitEvent(s, c->render_done[i], 0) != hipSuccess) return GEO_EHIP;
+        }
+        c->render_stream[i] = s;
+    }
+    return hipEventRecord(c->render_done[i], s) == hipSuccess ? GEO_OK : GEO_EHIP;
+}
+
 void geo_ctx_destroy(geo_ctx* c) {
     if (!c) return;
     DeviceGuard g(c->device);
-    // work in flight may still read the buffers or record the events
-    (void)hipDeviceSynchronize();
+    // work in flight may still read the buffers or record the events: the
+    // context's own work, not the device's (no device-wide wait, see geo_ctx)
+    (void)wait_renders(c);
+    for (int b = 0; b < 2; ++b) (void)wait_fan(c, b);
+    for (int i = 0; i < geo_ctx::kStepCallSets; ++i)
+        if (c->step_set_rec[i]) (void)hipEventSynchronize(c->step_set_free[i]);
     if (c->sky) (void)hipFree(c->sky);
     for (int b = 0; b < 2; ++b) {
         if (c->fan[b]) (void)hipFree(c->fan[b]);
@@ -562,6 +612,7 @@ void geo_ctx_destroy(geo_ctx* c) {
         (void)hipEventDestroy(c->fan_read[b]);
     }
     for (int i = 0; i < geo_ctx::kStepCallSets; ++i) (void)hipEventDestroy(c->step_set_free[i]);
+    for (int i = 0; i < geo_ctx::kRenderStreams; ++i) (void)hipEventDestroy(c->render_done[i]);
     if (c->step_slots) (void)hipFree(c->step_slots);
     delete c;
 }
@@ -577,13 +628,12 @@ int geo_set_sky(geo_ctx* c, const uint8_t* rgba8, uint32_t w, uint32_t h) {
     const size_t padded = ((size_t)w + 2u) * ((size_t)h + 2u);
     std::vector<uint32_t> pad(padded);
     geo::pad_sky(rgba8, w, h, pad.data());
-    // Renders still running on any of the caller's streams (non-blocking ones
-    // do not order against a blocking copy) may be reading the current sky:
-    // let them finish before it is overwritten or freed.  A sky change is a
-    // set-up call (the reference builds its texture once,
-    // basic_sphere_buffer.rs:29-36), so the device-wide wait costs nothing
-    // per frame.
-    if (hipDeviceSynchronize() != hipSuccess) return GEO_EHIP;
+    // Renders of this context still running on any of the caller's streams
+    // (non-blocking ones do not order against a blocking copy) may be reading
+    // the current sky: let them finish before it is overwritten or freed.  A
+    // sky change is a set-up call (the reference builds its texture once,
+    // basic_sphere_buffer.rs:29-36), so the wait costs nothing per frame.
+    if (wait_renders(c) != GEO_OK) return GEO_EHIP;
     if (c->sky && ((size_t)c->sky_w + 2u) * ((size_t)c->sky_h + 2u) != padded) {
         (void)hipFree(c->sky);
         c->sky = nullptr;
@@ -613,7 +663,8 @@ int geo_set_sky(geo_ctx* c, const uint8_t* rgba8, uint32_t w, uint32_t h) {
 // (renders in flight may read the old buffers); 400-node fans never regrow.
 static int ensure_fan(geo_ctx* c, uint32_t n) {
     if (c->fan[0] && c->fan_cap >= n) return GEO_OK;
-    if (hipDeviceSynchronize() != hipSuccess) return GEO_EHIP;
+    for (int b = 0; b < 2; ++b)
+        if (wait_fan(c, b) != GEO_OK) return GEO_EHIP;
     for (int b = 0; b < 2; ++b) {
         if (c->fan[b]) (void)hipFree(c->fan[b]);
         c->fan[b] = nullptr;
@@ -646,9 +697,10 @@ int geo_set_fan(geo_ctx* c, const float* fan, uint32_t n) {
     if (!g.ok) return GEO_EHIP;
     int st = ensure_fan(c, n);
     if (st) return st;
-    // a synchronous upload: into the free buffer once nothing reads it
+    // a synchronous upload: into the free buffer once its last solve and
+    // draws are done
     const int b = c->fan_cur < 0 ? 0 : 1 - c->fan_cur;
-    if (hipDeviceSynchronize() != hipSuccess) return GEO_EHIP;
+    if (wait_fan(c, b) != GEO_OK) return GEO_EHIP;
     if (hipMemcpy(c->fan[b], fan, sizeof(float) * n, hipMemcpyHostToDevice) != hipSuccess) return GEO_EHIP;
     c->n_fan[b] = n;
     c->fan_cur = b;
@@ -687,6 +739,23 @@ int geo_solve_ray_fan(geo_ctx* c, double sphere_r, double schwarz_r, uint32_t ma
 // (d <= 4096, checked by the caller).
 static uint32_t band_rows_magic(uint32_t d) {
     return (d & (d - 1u)) == 0u ? (uint32_t)((1ull << 32) / d) : (uint32_t)((1ull << 32) / d + 1u);
+}
+
+// One frame's tiles: grid.y is limited to 65535, so a taller tile grid (more
+// than 524280 rows; the C-ABI takes 2^20) goes out as several launches, each
+// with its first tile row in tile_y0.  The kernel's mapping is the same.
+constexpr uint32_t kMaxGridY = 65535;
+extern "C++" {
+template <int MODE, int KIND>
+static int launch_tiles(RenderArgs a, uint32_t tiles_x, uint32_t tiles_y, hipStream_t s) {
+    for (uint32_t y0 = 0; y0 < tiles_y; y0 += kMaxGridY) {
+        a.tile_y0 = y0;
+        const uint32_t ny = tiles_y - y0 < kMaxGridY ? tiles_y - y0 : kMaxGridY;
+        hipLaunchKernelGGL((geo_render_kernel<MODE, KIND>), dim3(tiles_x, ny), dim3(kBlock), 0, s, a);
+        if (hipGetLastError() != hipSuccess) return GEO_EHIP;
+    }
+    return GEO_OK;
+}
 }
 
 static int render_impl(geo_ctx* c, const geo_frame* frame, const geo_scene* scene, uint32_t width,
@@ -752,48 +821,38 @@ static int render_impl(geo_ctx* c, const geo_frame* frame, const geo_scene* scen
             return GEO_EHIP;
         a.step_slots = c->step_slots + (size_t)(1 + call_set) * kSlotSetU64;
     }
-    const dim3 grid(tiles_x, tiles_y);
+    int st;
     if (scene->mode == GEO_MODE_FAN) {
         // after the solve that wrote the buffer; then this render joins the
         // buffer's chain of readers (the wait is queued after the launch, so
         // it holds back only later work on s, never this render)
         if (c->fan_written_rec[fb] && hipStreamWaitEvent(s, c->fan_written[fb], 0) != hipSuccess) return GEO_EHIP;
-        hipLaunchKernelGGL((geo_render_kernel<GEO_MODE_FAN, geo::kCurvedOut>), grid, dim3(kBlock), 0, s, a);
-        if (hipGetLastError() != hipSuccess) return GEO_EHIP;
+        st = launch_tiles<GEO_MODE_FAN, geo::kCurvedOut>(a, tiles_x, tiles_y, s);
+        if (st) return st;
         if (c->fan_read_rec[fb] && hipStreamWaitEvent(s, c->fan_read[fb], 0) != hipSuccess) return GEO_EHIP;
         if (hipEventRecord(c->fan_read[fb], s) != hipSuccess) return GEO_EHIP;
         c->fan_read_rec[fb] = true;
     } else if (adaptive) {
         switch (geo::geodesic_kind(a.k)) {
-            case geo::kCurvedOut:
-                hipLaunchKernelGGL((geo_render_kernel<GEO_MODE_ADAPTIVE, geo::kCurvedOut>), grid, dim3(kBlock), 0, s, a);
-                break;
-            case geo::kCurvedIn:
-                hipLaunchKernelGGL((geo_render_kernel<GEO_MODE_ADAPTIVE, geo::kCurvedIn>), grid, dim3(kBlock), 0, s, a);
-                break;
-            default:
-                hipLaunchKernelGGL((geo_render_kernel<GEO_MODE_ADAPTIVE, geo::kFlat>), grid, dim3(kBlock), 0, s, a);
+            case geo::kCurvedOut: st = launch_tiles<GEO_MODE_ADAPTIVE, geo::kCurvedOut>(a, tiles_x, tiles_y, s); break;
+            case geo::kCurvedIn: st = launch_tiles<GEO_MODE_ADAPTIVE, geo::kCurvedIn>(a, tiles_x, tiles_y, s); break;
+            default: st = launch_tiles<GEO_MODE_ADAPTIVE, geo::kFlat>(a, tiles_x, tiles_y, s);
         }
     } else {
         switch (geo::geodesic_kind(a.k)) {
-            case geo::kCurvedOut:
-                hipLaunchKernelGGL((geo_render_kernel<GEO_MODE_DIRECT, geo::kCurvedOut>), grid, dim3(kBlock), 0, s, a);
-                break;
-            case geo::kCurvedIn:
-                hipLaunchKernelGGL((geo_render_kernel<GEO_MODE_DIRECT, geo::kCurvedIn>), grid, dim3(kBlock), 0, s, a);
-                break;
-            default:
-                hipLaunchKernelGGL((geo_render_kernel<GEO_MODE_DIRECT, geo::kFlat>), grid, dim3(kBlock), 0, s, a);
+            case geo::kCurvedOut: st = launch_tiles<GEO_MODE_DIRECT, geo::kCurvedOut>(a, tiles_x, tiles_y, s); break;
+            case geo::kCurvedIn: st = launch_tiles<GEO_MODE_DIRECT, geo::kCurvedIn>(a, tiles_x, tiles_y, s); break;
+            default: st = launch_tiles<GEO_MODE_DIRECT, geo::kFlat>(a, tiles_x, tiles_y, s);
         }
     }
-    if (hipGetLastError() != hipSuccess) return GEO_EHIP;
+    if (st) return st;
     if (call_set >= 0) {
         hipLaunchKernelGGL(geo_steps_finalize, dim3(1), dim3(kStepSlots), 0, s, a.step_slots, steps_total);
         if (hipGetLastError() != hipSuccess) return GEO_EHIP;
         if (hipEventRecord(c->step_set_free[call_set], s) != hipSuccess) return GEO_EHIP;
         c->step_set_rec[call_set] = true;
     }
-    return GEO_OK;
+    return note_render(c, s);
 }
 
 int geo_assemble_bands(geo_ctx* c, const uint8_t* src, size_t rank_stride, size_t frame_stride, uint32_t world,
@@ -891,7 +950,8 @@ int geo_steps_flush(geo_ctx* c, unsigned long long* steps_total, void* stream) {
     if (!g.ok) return GEO_EHIP;
     hipLaunchKernelGGL(geo_steps_finalize, dim3(1), dim3(kStepSlots), 0, (hipStream_t)stream, c->step_slots,
                        steps_total);
-    return hipGetLastError() == hipSuccess ? GEO_OK : GEO_EHIP;
+    if (hipGetLastError() != hipSuccess) return GEO_EHIP;
+    return note_render(c, (hipStream_t)stream);
 }
 
 int geo_render_rows(geo_ctx* c, const geo_frame* frame, const geo_scene* scene, uint32_t width,

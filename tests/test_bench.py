@@ -17,15 +17,15 @@ import bench
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def test_pmc_traffic_only_for_the_profiled_workload():
-    t = bench.pmc_traffic("cfg3_4k", "direct", 1)
+def test_pmc_profile_only_for_the_profiled_workload():
+    t = bench.pmc_profile("cfg3_4k", "direct", 1)[1].get("traffic_bytes")
     assert t is not None and 5e7 < t < 2e8  # ~90 MB per 4K frame
-    assert bench.pmc_traffic("cfg3_4k", "adaptive", 1) is None  # a direct-mode profile
-    assert bench.pmc_traffic("cfg3_4k", "fan", 1) is None
-    assert bench.pmc_traffic("cfg3_4k", "direct", 2) is None  # full-frame bytes vs a rank's share
-    assert bench.pmc_traffic("cfg5_8k_adaptive", "adaptive", 1) is not None
-    assert bench.pmc_traffic("cfg2_1080p", "direct", 1) is not None
-    assert bench.pmc_traffic("cfg1_256_cpu", "direct", 1) is None  # never profiled
+    assert bench.pmc_profile("cfg3_4k", "adaptive", 1) == (None, {})  # a direct-mode profile
+    assert bench.pmc_profile("cfg3_4k", "fan", 1) == (None, {})
+    assert bench.pmc_profile("cfg3_4k", "direct", 2) == (None, {})  # full-frame bytes vs a rank's share
+    assert bench.pmc_profile("cfg5_8k_adaptive", "adaptive", 1)[0] is not None
+    assert bench.pmc_profile("cfg2_1080p", "direct", 1)[0] is not None
+    assert bench.pmc_profile("cfg1_256_cpu", "direct", 1) == (None, {})  # never profiled
 
 
 @pytest.mark.gpu

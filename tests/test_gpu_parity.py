@@ -144,6 +144,34 @@ def test_row_blocks_compose_full_frame(geo, torch_mod):
     assert sum(p["total"] for p in parts) == full["total"]
 
 
+def test_tallest_frame_takes_several_launches(geo, torch_mod):
+    """A narrow frame of the C-ABI's maximum height, 2^20 rows: 131072 tile
+    rows, more than grid.y's 65535, so the render goes out as three launches
+    (ADVICE r02).  Sampled rows from every launch equal the oracle, a row
+    block across a launch boundary equals its own render, and the step total
+    covers every launch."""
+    from schwarzschild_raytracer_wgpu_amd.scenes import make_sky
+
+    w, h = 4, 1 << 20
+    sky = make_sky("equirect", (256, 128))
+    frame, scene = default_frame(w, h), default_scene(64)
+    ctx = make_ctx(geo, sky)
+    full = render(geo, torch_mod, ctx, frame, scene, w, h)
+    assert full["total"] == int(full["steps"].astype(np.int64).sum()) > 0
+    row0, step = 3, 4099
+    ref = O.render_f32(frame, scene, sky, w, h, row0=row0, nrows=(h - row0 + step - 1) // step, row_step=step,
+                       threads=8)
+    for f in ("rgba", "mask", "uv", "steps"):
+        a = full[f][row0::step]
+        assert np.array_equal(a.view(np.uint32) if f == "uv" else a, ref[f].view(np.uint32) if f == "uv" else ref[f]), f
+    b0 = 65535 * 8 - 20  # the first launch's last tile rows and the second's first
+    part = render(geo, torch_mod, ctx, frame, scene, w, h, b0, 40)
+    for f in ("rgba", "mask", "uv", "steps"):
+        assert np.array_equal(part[f], full[f][b0:b0 + 40]), f
+    last = render(geo, torch_mod, ctx, frame, scene, w, h, h - 9, 9)
+    assert np.array_equal(last["rgba"], full["rgba"][h - 9:])
+
+
 def test_render_bands_interleaved(geo, torch_mod):
     """geo_render_bands for 3 ranks x 8-row bands == the full frame's rows."""
     from schwarzschild_raytracer_wgpu_amd.dist import BandLayout

@@ -363,6 +363,20 @@ GEO_HD bool geodesic_init(const PixelConsts& k, float st, float ct, float rct, f
     return true;
 }
 
+// The lanes of the wave for which p holds (a uniform SGPR mask), and the
+// rarely taken arm of a branch that must stay a branch: a volatile asm cannot
+// be speculated, so the compiler cannot turn the arm into a select that every
+// group would pay for.
+#if defined(__HIP_DEVICE_COMPILE__)
+GEO_HD uint64_t ballot_(bool p) { return __builtin_amdgcn_ballot_w64(p); }
+GEO_HD bool in_ballot_(uint64_t m) { return __builtin_amdgcn_inverse_ballot_w64(m); }
+#define GEO_RARE() asm volatile("")
+#else
+GEO_HD uint64_t ballot_(bool p) { return p ? 1u : 0u; }
+GEO_HD bool in_ballot_(uint64_t m) { return m != 0; }
+#define GEO_RARE() ((void)0)
+#endif
+
 // Stop flag of one accepted step (reference order: crossing :150, escape
 // :184, loop test :134-135).  The integration ends at the first crossing, so
 // "above the sphere" (U > SU) is fixed for the whole integration and frame-
@@ -404,21 +418,16 @@ struct StopTest {
         else
             return (*this)(NU, NUB);
     }
+    // exact() as a wave mask, each compare balloted on its own (hipcc
+    // rebuilds a compound condition through a VGPR before its ballot)
+    GEO_HDM uint64_t exact_mask(float NU, float NUB) const {
+        if constexpr (KIND == kCurvedOut)
+            return ballot_(!(NU >= lo)) | (ballot_(NU > hi) & ballot_(NUB > vmin));
+        else
+            return ballot_((*this)(NU, NUB));
+    }
 };
 
-// The lanes of the wave for which p holds (a uniform SGPR mask), and the
-// rarely taken arm of a branch that must stay a branch: a volatile asm cannot
-// be speculated, so the compiler cannot turn the arm into a select that every
-// group would pay for.
-#if defined(__HIP_DEVICE_COMPILE__)
-GEO_HD uint64_t ballot_(bool p) { return __builtin_amdgcn_ballot_w64(p); }
-GEO_HD bool in_ballot_(uint64_t m) { return __builtin_amdgcn_inverse_ballot_w64(m); }
-#define GEO_RARE() asm volatile("")
-#else
-GEO_HD uint64_t ballot_(bool p) { return p ? 1u : 0u; }
-GEO_HD bool in_ballot_(uint64_t m) { return m != 0; }
-#define GEO_RARE() ((void)0)
-#endif
 
 template <int G, int KIND>
 GEO_HD void group_steps_(float u, float b, float h, float hh, float hh2, float hhh, float h6, float h2_6,
@@ -795,6 +804,15 @@ GEO_HD void dp5_step(float U, float V, float h, float hh, float* NU, float* NV, 
 //   |SE| h^2 > tolU           reject, h /= 2
 //   |SE| h^2 < tolU/64        accept, then h = min(2h, hmax)  (5th order: x32)
 //   otherwise                 accept, keep h
+//
+// The loop is wave-uniform: every lane that entered it attempts a step per
+// iteration, with no per-lane exit and no exec-mask bookkeeping; the lanes
+// still integrating are the scalar mask `live`.  A lane that stops (an
+// accepted step's stop test) records its step's start (U, V, h, ang) and end
+// (NU, NV) in a rarely taken block, leaves `live`, and keeps stepping
+// harmlessly (its registers are no longer read).  The loop ends when `live`
+// is empty or the budget is spent.  Round 2's per-lane `break` cost 26 SALU
+// and ~10 VALU of mask and state bookkeeping per attempt.
 template <int KIND>
 GEO_HD float geodesic_angle_adaptive(const PixelConsts& k, float st, float ct, float rct, uint32_t* steps) {
     *steps = 0;
@@ -803,48 +821,64 @@ GEO_HD float geodesic_angle_adaptive(const PixelConsts& k, float st, float ct, f
     const StopTest<KIND> stop_at(k);
     const uint32_t ms = k.max_steps;
     float h = k.step, ang = 0.0f;
-    float NU = U, NV = V;
-    bool stopped = false;
+    // the stopping step: start (sU, sV, sh, sang) and end (sNU, sNV)
+    float sU, sV, sh, sang, sNU, sNV;
+    GEO_UNSET(sU);
+    GEO_UNSET(sV);
+    GEO_UNSET(sh);
+    GEO_UNSET(sang);
+    GEO_UNSET(sNU);
+    GEO_UNSET(sNV);
+    // attempts up to and including the lane's stop; 0: no stop (the budget)
     uint32_t it = 0;
-    // One exit per attempt (the stop of an accepted step); accept/reject is
-    // branch-free selects, so the wave runs one straight-line attempt per
-    // iteration.  On the stop, (U, V, h) still hold the step's start and size.
-    while (it < ms) {
-        ++it;
-        float SE;
+    uint64_t live = ballot_(true);
+    // one exit edge (an empty `live` ends the count instead of a break: hipcc
+    // turns a second exit into lane-mask flags at the latch)
+    for (uint32_t n = 1; n <= ms; ++n) {
+        float NU, NV, SE;
         const float hh = h * h;
         dp5_step<KIND>(U, V, h, hh, &NU, &NV, &SE);
         const float err = __builtin_fabsf(SE) * hh;
         const bool acc = !(err > k.tolU);
-        if (acc & stop_at.exact(NU, NV)) {  // `&`: both flags as lane masks, no branch between them
-            stopped = true;
-            break;
+        const uint64_t hit = ballot_(acc) & stop_at.exact_mask(NU, NV) & live;
+        if (hit != 0) {
+            if (in_ballot_(hit)) {
+                GEO_RARE();
+                sU = U;
+                sV = V;
+                sh = h;
+                sang = ang;
+                sNU = NU;
+                sNV = NV;
+                it = n;
+            }
+            live &= ~hit;
+            n = live == 0 ? ms : n;
         }
-        // min(2h, hmax) as a growth test: h is step/2^j or step*2^j <= hmax with
-        // hmax = 16 step, so h < hmax implies 2h <= hmax (same bits, 2 fewer VALU)
         // the new step as h times 2, 1 or 1/2 (exact: the same bits as h + h,
-        // h and h * 0.5), one multiply after two selects of the factor
+        // h and h * 0.5), one multiply after two selects of the factor; the
+        // cap as a growth test (h = step 2^j, so h < hmax implies 2h <= hmax)
         const float grow = (err < k.tolG && h < k.hmax) ? 2.0f : 1.0f;
         U = acc ? NU : U;
         V = acc ? NV : V;
         ang = acc ? ang + h : ang;
         h = h * (acc ? grow : 0.5f);
     }
-    *steps = it;
-    if (!stopped || (NU > k.SU) == (U > k.SU)) return kNoValue;
+    *steps = it != 0 ? it : ms;
+    if (it == 0 || (sNU > k.SU) == (sU > k.SU)) return kNoValue;
     // Newton on the step length from the steeper end (:150-182)
     float ns, wu, wv;
-    if (__builtin_fabsf(V) > __builtin_fabsf(NV)) {
-        ns = 0.0f; wu = U; wv = V;
+    if (__builtin_fabsf(sV) > __builtin_fabsf(sNV)) {
+        ns = 0.0f; wu = sU; wv = sV;
     } else {
-        ns = h; wu = NU; wv = NV;
+        ns = sh; wu = sNU; wv = sNV;
     }
     for (int n = 0; n < kNewtonIters; ++n) {
         ns = ns - divf_(wu - k.SU, wv);
         float se;
-        dp5_step<KIND>(U, V, ns, ns * ns, &wu, &wv, &se);
+        dp5_step<KIND>(sU, sV, ns, ns * ns, &wu, &wv, &se);
     }
-    return ang + ns;
+    return sang + ns;
 }
 
 // 3x3 part of a column-major mat4 times v (w = 0).

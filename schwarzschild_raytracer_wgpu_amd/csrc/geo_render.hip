@@ -15,6 +15,7 @@
 // ray fan (fan mode) is read from its cache-resident device copy; per-lane
 // ray state lives in VGPRs.  The hot loop
 // is pure FP32 VALU — no MFMA, no LDS, no memory traffic.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -577,8 +578,12 @@ static int wait_fan(geo_ctx* c, int b) {
     return GEO_OK;
 }
 
-// Records the context's latest work on stream s (geo_ctx::render_done).
-static int note_render(geo_ctx* c, hipStream_t s) {
+// The event that tracks the context's work on stream s (geo_ctx::render_done):
+// the caller's next kernel on s records it as its stop event
+// (hipExtLaunchKernelGGL), which rides on the dispatch's own completion
+// signal instead of a marker packet after it (a marker per frame cost ~1 % of
+// the event-timed 4K kernel).  Null on a HIP error.
+static hipEvent_t render_event(geo_ctx* c, hipStream_t s) {
     int i = 0;
     while (i < c->n_render_streams && c->render_stream[i] != s) ++i;
     if (i == c->n_render_streams) {
@@ -589,11 +594,11 @@ static int note_render(geo_ctx* c, hipStream_t s) {
             // records next covers the evicted stream's last render as well
             i = c->render_next;
             c->render_next = (i + 1) % geo_ctx::kRenderStreams;
-            if (hipStreamWaitEvent(s, c->render_done[i], 0) != hipSuccess) return GEO_EHIP;
+            if (hipStreamWaitEvent(s, c->render_done[i], 0) != hipSuccess) return nullptr;
         }
         c->render_stream[i] = s;
     }
-    return hipEventRecord(c->render_done[i], s) == hipSuccess ? GEO_OK : GEO_EHIP;
+    return c->render_done[i];
 }
 
 void geo_ctx_destroy(geo_ctx* c) {
@@ -746,12 +751,14 @@ static uint32_t band_rows_magic(uint32_t d) {
 // with its first tile row in tile_y0.  The kernel's mapping is the same.
 constexpr uint32_t kMaxGridY = 65535;
 extern "C++" {
+// The last launch records `done` (render_event) as its stop event.
 template <int MODE, int KIND>
-static int launch_tiles(RenderArgs a, uint32_t tiles_x, uint32_t tiles_y, hipStream_t s) {
+static int launch_tiles(RenderArgs a, uint32_t tiles_x, uint32_t tiles_y, hipStream_t s, hipEvent_t done) {
     for (uint32_t y0 = 0; y0 < tiles_y; y0 += kMaxGridY) {
         a.tile_y0 = y0;
         const uint32_t ny = tiles_y - y0 < kMaxGridY ? tiles_y - y0 : kMaxGridY;
-        hipLaunchKernelGGL((geo_render_kernel<MODE, KIND>), dim3(tiles_x, ny), dim3(kBlock), 0, s, a);
+        hipExtLaunchKernelGGL((geo_render_kernel<MODE, KIND>), dim3(tiles_x, ny), dim3(kBlock), 0, s, nullptr,
+                              y0 + ny >= tiles_y ? done : nullptr, 0, a);
         if (hipGetLastError() != hipSuccess) return GEO_EHIP;
     }
     return GEO_OK;
@@ -821,28 +828,30 @@ static int render_impl(geo_ctx* c, const geo_frame* frame, const geo_scene* scen
             return GEO_EHIP;
         a.step_slots = c->step_slots + (size_t)(1 + call_set) * kSlotSetU64;
     }
+    const hipEvent_t done = render_event(c, s);
+    if (!done) return GEO_EHIP;
     int st;
     if (scene->mode == GEO_MODE_FAN) {
         // after the solve that wrote the buffer; then this render joins the
         // buffer's chain of readers (the wait is queued after the launch, so
         // it holds back only later work on s, never this render)
         if (c->fan_written_rec[fb] && hipStreamWaitEvent(s, c->fan_written[fb], 0) != hipSuccess) return GEO_EHIP;
-        st = launch_tiles<GEO_MODE_FAN, geo::kCurvedOut>(a, tiles_x, tiles_y, s);
+        st = launch_tiles<GEO_MODE_FAN, geo::kCurvedOut>(a, tiles_x, tiles_y, s, done);
         if (st) return st;
         if (c->fan_read_rec[fb] && hipStreamWaitEvent(s, c->fan_read[fb], 0) != hipSuccess) return GEO_EHIP;
         if (hipEventRecord(c->fan_read[fb], s) != hipSuccess) return GEO_EHIP;
         c->fan_read_rec[fb] = true;
     } else if (adaptive) {
         switch (geo::geodesic_kind(a.k)) {
-            case geo::kCurvedOut: st = launch_tiles<GEO_MODE_ADAPTIVE, geo::kCurvedOut>(a, tiles_x, tiles_y, s); break;
-            case geo::kCurvedIn: st = launch_tiles<GEO_MODE_ADAPTIVE, geo::kCurvedIn>(a, tiles_x, tiles_y, s); break;
-            default: st = launch_tiles<GEO_MODE_ADAPTIVE, geo::kFlat>(a, tiles_x, tiles_y, s);
+            case geo::kCurvedOut: st = launch_tiles<GEO_MODE_ADAPTIVE, geo::kCurvedOut>(a, tiles_x, tiles_y, s, done); break;
+            case geo::kCurvedIn: st = launch_tiles<GEO_MODE_ADAPTIVE, geo::kCurvedIn>(a, tiles_x, tiles_y, s, done); break;
+            default: st = launch_tiles<GEO_MODE_ADAPTIVE, geo::kFlat>(a, tiles_x, tiles_y, s, done);
         }
     } else {
         switch (geo::geodesic_kind(a.k)) {
-            case geo::kCurvedOut: st = launch_tiles<GEO_MODE_DIRECT, geo::kCurvedOut>(a, tiles_x, tiles_y, s); break;
-            case geo::kCurvedIn: st = launch_tiles<GEO_MODE_DIRECT, geo::kCurvedIn>(a, tiles_x, tiles_y, s); break;
-            default: st = launch_tiles<GEO_MODE_DIRECT, geo::kFlat>(a, tiles_x, tiles_y, s);
+            case geo::kCurvedOut: st = launch_tiles<GEO_MODE_DIRECT, geo::kCurvedOut>(a, tiles_x, tiles_y, s, done); break;
+            case geo::kCurvedIn: st = launch_tiles<GEO_MODE_DIRECT, geo::kCurvedIn>(a, tiles_x, tiles_y, s, done); break;
+            default: st = launch_tiles<GEO_MODE_DIRECT, geo::kFlat>(a, tiles_x, tiles_y, s, done);
         }
     }
     if (st) return st;
@@ -852,7 +861,7 @@ static int render_impl(geo_ctx* c, const geo_frame* frame, const geo_scene* scen
         if (hipEventRecord(c->step_set_free[call_set], s) != hipSuccess) return GEO_EHIP;
         c->step_set_rec[call_set] = true;
     }
-    return note_render(c, s);
+    return GEO_OK;
 }
 
 int geo_assemble_bands(geo_ctx* c, const uint8_t* src, size_t rank_stride, size_t frame_stride, uint32_t world,
@@ -948,10 +957,11 @@ int geo_steps_flush(geo_ctx* c, unsigned long long* steps_total, void* stream) {
     if (!c || !steps_total) return GEO_EINVAL;
     DeviceGuard g(c->device);
     if (!g.ok) return GEO_EHIP;
-    hipLaunchKernelGGL(geo_steps_finalize, dim3(1), dim3(kStepSlots), 0, (hipStream_t)stream, c->step_slots,
-                       steps_total);
-    if (hipGetLastError() != hipSuccess) return GEO_EHIP;
-    return note_render(c, (hipStream_t)stream);
+    const hipEvent_t done = render_event(c, (hipStream_t)stream);
+    if (!done) return GEO_EHIP;
+    hipExtLaunchKernelGGL(geo_steps_finalize, dim3(1), dim3(kStepSlots), 0, (hipStream_t)stream, nullptr, done, 0,
+                          c->step_slots, steps_total);
+    return hipGetLastError() == hipSuccess ? GEO_OK : GEO_EHIP;
 }
 
 int geo_render_rows(geo_ctx* c, const geo_frame* frame, const geo_scene* scene, uint32_t width,

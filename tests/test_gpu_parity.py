@@ -172,6 +172,40 @@ def test_tallest_frame_takes_several_launches(geo, torch_mod):
     assert np.array_equal(last["rgba"], full["rgba"][h - 9:])
 
 
+def test_sky_swap_waits_for_renders_on_other_streams(geo, torch_mod):
+    """geo_set_sky waits for the context's renders in flight on every stream
+    it has rendered on (per-stream events, no device-wide wait),
+    including streams evicted from the context's 8 tracked slots: renders
+    queued before the swap sample the old sky, renders after it the new one."""
+    from schwarzschild_raytracer_wgpu_amd.scenes import make_sky
+
+    torch = torch_mod
+    w, h = 1920, 1080
+    frame, scene = default_frame(w, h), default_scene(2048)
+    sky_a = make_sky("equirect", (512, 256))
+    sky_b = np.ascontiguousarray(255 - sky_a)
+    sky_b[..., 3] = 255
+    want = {}
+    for name, sky in (("a", sky_a), ("b", sky_b)):
+        ref_ctx = make_ctx(geo, sky)
+        want[name] = render(geo, torch, ref_ctx, frame, scene, w, h)["rgba"]
+        ref_ctx.close()
+    assert not np.array_equal(want["a"], want["b"])
+    dev = torch.device("cuda:0")
+    ctx = make_ctx(geo, sky_a)
+    streams = [torch.cuda.Stream() for _ in range(11)]  # > 8 tracked slots
+    before = [torch.empty(h * w * 4, dtype=torch.uint8, device=dev) for _ in streams]
+    for st, buf in zip(streams, before):
+        ctx.render_rows(frame, scene, w, h, 0, h, buf, stream=st)
+    ctx.set_sky(sky_b)  # same size: overwritten in place
+    after = torch.empty(h * w * 4, dtype=torch.uint8, device=dev)
+    ctx.render_rows(frame, scene, w, h, 0, h, after, stream=streams[0])
+    torch.cuda.synchronize()
+    for buf in before:
+        assert np.array_equal(buf.cpu().numpy().reshape(h, w, 4), want["a"])
+    assert np.array_equal(after.cpu().numpy().reshape(h, w, 4), want["b"])
+
+
 def test_render_bands_interleaved(geo, torch_mod):
     """geo_render_bands for 3 ranks x 8-row bands == the full frame's rows."""
     from schwarzschild_raytracer_wgpu_amd.dist import BandLayout

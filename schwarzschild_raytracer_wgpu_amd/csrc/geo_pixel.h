@@ -516,6 +516,21 @@ GEO_HD uint64_t group_stop_(const StopTest<KIND>& stop_at, const float (&ou)[G],
     }
 }
 
+// The lower half of kTestLow alone: the minimum of all G states below lo (a
+// NaN state is left to a later test: NaN propagates).  The pair loop's A
+// groups take this test (3 VALU instead of 4) and leave a stop above hi to
+// the B group's full test (run_groups_pp): a state above hi = HU keeps every
+// later state above it (group_stop_'s kTestLow argument), so B's last state is
+// above hi, or NaN, too.
+template <int G>
+GEO_HD uint64_t group_low_(float lo, const float (&ou)[G]) {
+    float mn = ou[0];
+    int j = 1;
+    for (; j + 2 <= G; j += 2) mn = min3_(mn, ou[j], ou[j + 1]);
+    for (; j < G; ++j) mn = min3_(mn, ou[j], ou[j]);
+    return ballot_(mn < lo);
+}
+
 // The group loop: G RK4 steps per exit test; returns the steps before the
 // stopping group (or `all` when the budget of whole groups runs out), with the
 // group's G + 1 states in su_/sb_.  A lane that stops inside a group discards
@@ -564,7 +579,8 @@ GEO_HD uint32_t run_groups_pp(const StopTest<KIND>& stop_at, uint32_t ngroups, u
     uint32_t rem = ngroups >> 1;
     while (rem != 0) {
         if (in_ballot_(live)) group_steps_<G, KIND>(xu, xb, h, hh, hh2, hhh, h6, h2_6, au, ab);
-        uint64_t hit = group_stop_<G, KIND, TEST>(stop_at, au, ab) & live;
+        uint64_t hit = (TEST == kTestLow ? group_low_<G>(stop_at.lo, au) : group_stop_<G, KIND, TEST>(stop_at, au, ab)) &
+                       live;
         --rem;
         if (hit != 0) {
             if (in_ballot_(hit)) {
@@ -598,7 +614,24 @@ GEO_HD uint32_t run_groups_pp(const StopTest<KIND>& stop_at, uint32_t ngroups, u
         // `live` empties only where lanes stop, so its test sits in that
         // branch: a pair without stops ends in the counter's compare alone
         if (hit != 0) {
-            if (in_ballot_(hit)) {
+            uint64_t in_a = 0;
+            if constexpr (TEST == kTestLow) {
+                // A stops above hi (or at a NaN), left to this test: a_G is
+                // then above hi or NaN.  The A group's start state X is B's
+                // end now; the replay (geodesic_finish) reads it only as the
+                // state before a first stop at a_1, where any value above SU
+                // gives the same result (no crossing; a NaN a_1 gives NaN
+                // either way), so hi stands in for it.
+                in_a = hit & ~ballot_(au[G - 1] <= stop_at.hi);
+                if (in_a != 0) {
+                    if (in_ballot_(in_a)) {
+                        GEO_RARE();
+                        it = (q - 2u) * (uint32_t)G;
+                        xu = stop_at.hi;
+                    }
+                }
+            }
+            if (in_ballot_(hit & ~in_a)) {
                 GEO_RARE();
                 it = (q - 1u) * (uint32_t)G;
             }

@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define GEO_ABI_VERSION 2
+#define GEO_ABI_VERSION 3
 
 typedef enum geo_status {
     GEO_OK = 0,
@@ -72,6 +72,13 @@ typedef enum geo_status {
                                    pixels untouched: the 2nd, 3rd... sphere of a frame
                                    (lib.rs:67-89).  Without it a sphere is drawn over the
                                    cleared target (0,0,0,1). */
+#define GEO_FLAG_MIPS 4u        /* sample the sky through its 4-level mip chain, trilinear,
+                                   with the level of detail from the UV differences across
+                                   each 2x2 pixel quad, as textureSample does
+                                   (basic_sphere_buffer.rs:31-36, shader.wgsl:101; the
+                                   level-0 bilinear sample otherwise).  Quads are frame-
+                                   aligned, so row0 must be even (GEO_EINVAL otherwise);
+                                   band layouts keep bands 8-row aligned. */
 
 /* Observer motion states, ObserverState (SR/simulation/observer.rs:12-16). */
 #define GEO_OBSERVER_UNMOVING 0

@@ -83,6 +83,11 @@ def _load() -> ctypes.CDLL:
         "geo_oracle_asinf": (ctypes.c_float, [ctypes.c_float]),
         "geo_oracle_atan2f": (ctypes.c_float, [ctypes.c_float, ctypes.c_float]),
         "geo_oracle_sincosf": (None, [ctypes.c_float, vp, vp]),
+        "geo_oracle_mip_chain_texels": (ctypes.c_uint64, [u32, u32]),
+        "geo_oracle_mip_chain": (None, [vp, u32, u32, vp]),
+        "geo_oracle_lod_q8_n": (None, [vp, u32, vp]),
+        "geo_oracle_render_mips_f32": (i, [vp, vp, vp, u32, vp, u32, u32, u32, u32, u32, u32, i, vp, vp, vp, vp,
+                                           vp]),
     }
     for n, (r, a) in sig.items():
         fn = getattr(lib, n)
@@ -197,6 +202,42 @@ def render_f32(frame, scene, sky, width, height, row0=0, nrows=None, row_step=1,
                                    threads, _np(rgba), _np(mask), _np(uv), _np(steps), _addr(total))
     if rc != 0:
         raise ValueError(f"geo_oracle_render_f32: {rc}")
+    return dict(rgba=rgba, mask=mask, uv=uv, steps=steps, steps_total=total.value)
+
+
+def mip_chain(sky) -> list:
+    """The GEO_FLAG_MIPS mip chain of an (h, w, 4) RGBA8 texture: 4 levels
+    (geo_pixel.h mip_down, box filter), each an (h_l, w_l, 4) array."""
+    sky_a = np.ascontiguousarray(sky, dtype=np.uint8)
+    h, w = sky_a.shape[:2]
+    out = np.empty(int(lib.geo_oracle_mip_chain_texels(w, h)), np.uint32)
+    lib.geo_oracle_mip_chain(_np(sky_a), w, h, _np(out))
+    levels, o = [], 0
+    for lvl in range(4):
+        lw, lh = max(1, w >> lvl), max(1, h >> lvl)
+        levels.append(out[o:o + lw * lh].view(np.uint8).reshape(lh, lw, 4))
+        o += lw * lh
+    return levels
+
+
+def render_mips_f32(frame, scene, sky, width, height, row0=0, nrows=None, fan=None, threads=8, target=None):
+    """The GEO_FLAG_MIPS mirror: rows [row0, row0 + nrows) (row0 even) sampled
+    trilinearly through the sky's mip chain; target as in render_f32."""
+    nrows = height - row0 if nrows is None else nrows
+    fr, sc = as_frame(frame), as_scene(scene)
+    sky_a = np.ascontiguousarray(sky, dtype=np.uint8)
+    fan_a = None if fan is None else np.ascontiguousarray(fan, dtype=np.float32)
+    rgba = np.zeros((nrows, width, 4), np.uint8) if target is None else np.array(target, np.uint8).reshape(
+        nrows, width, 4)
+    mask = np.empty((nrows, width), np.uint8)
+    uv = np.empty((nrows, width, 2), np.float32)
+    steps = np.empty((nrows, width), np.uint32)
+    total = ctypes.c_uint64()
+    rc = lib.geo_oracle_render_mips_f32(_addr(fr), _addr(sc), _np(fan_a), 0 if fan_a is None else fan_a.size,
+                                        _np(sky_a), sky_a.shape[1], sky_a.shape[0], width, height, row0, nrows,
+                                        threads, _np(rgba), _np(mask), _np(uv), _np(steps), _addr(total))
+    if rc != 0:
+        raise ValueError(f"geo_oracle_render_mips_f32: {rc}")
     return dict(rgba=rgba, mask=mask, uv=uv, steps=steps, steps_total=total.value)
 
 

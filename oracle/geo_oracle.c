@@ -584,6 +584,50 @@ static cam_f32 camera_f32(const geo_frame* f, uint32_t width, uint32_t height) {
     return cc;
 }
 
+/* bilinear sample of one sw x sh level, U wraps, V clamps, 8-bit sub-texel
+ * weights; per channel: horizontal lerp truncated to 8 bits, vertical lerp
+ * rounded.  Texel coordinates in 1/256 texel units: n = floor(256 (U sw -
+ * 1/2)); texel floor(n / 256), 8-bit weight n mod 256. */
+static uint32_t bilinear_level(const uint32_t* sky, uint32_t sw, uint32_t sh, float U, float V) {
+    int nx = (int)floorf(fmaf(U, (float)sw * 256.0f, -128.0f));
+    int ny = (int)floorf(fmaf(V, (float)sh * 256.0f, -128.0f));
+    uint32_t wx = (uint32_t)nx & 255u;
+    uint32_t wy = (uint32_t)ny & 255u;
+    int ix0 = nx >> 8, iy0 = ny >> 8;
+    int w = (int)sw, h = (int)sh;
+    if (ix0 < 0) ix0 += w;
+    if (ix0 >= w) ix0 -= w;
+    int ix1 = (ix0 + 1 == w) ? 0 : ix0 + 1;
+    int iy1 = iy0 + 1;
+    iy0 = iy0 < 0 ? 0 : (iy0 > h - 1 ? h - 1 : iy0);
+    iy1 = iy1 < 0 ? 0 : (iy1 > h - 1 ? h - 1 : iy1);
+    uint32_t t[4] = {sky[(uint32_t)iy0 * sw + (uint32_t)ix0], sky[(uint32_t)iy0 * sw + (uint32_t)ix1],
+                     sky[(uint32_t)iy1 * sw + (uint32_t)ix0], sky[(uint32_t)iy1 * sw + (uint32_t)ix1]};
+    uint32_t c = 0;
+    for (int ch = 0; ch < 4; ++ch) {
+        uint32_t v00 = (t[0] >> (8 * ch)) & 255u, v10 = (t[1] >> (8 * ch)) & 255u;
+        uint32_t v01 = (t[2] >> (8 * ch)) & 255u, v11 = (t[3] >> (8 * ch)) & 255u;
+        uint32_t top = (v00 * (256u - wx) + v10 * wx) >> 8;
+        uint32_t bot = (v01 * (256u - wx) + v11 * wx) >> 8;
+        c |= ((top * (256u - wy) + bot * wy + 128u) >> 8) << (8 * ch);
+    }
+    return c;
+}
+
+/* BlendState::ALPHA_BLENDING (pipeline.rs:49) of the sample s over the target
+ * d, 8-bit fixed point: rgb = round((s a + d (255 - a))/255), alpha =
+ * round((255 a + d_a (255 - a))/255); without GEO_FLAG_COMPOSITE d = the
+ * clear colour (0,0,0,255). */
+static uint32_t blend_over(uint32_t s, uint32_t dst) {
+    uint32_t a = s >> 24, out = 0;
+    for (int ch = 0; ch < 4; ++ch) {
+        uint32_t sv = ch < 3 ? (s >> (8 * ch)) & 255u : 255u;
+        uint32_t p = sv * a + ((dst >> (8 * ch)) & 255u) * (255u - a) + 128u;
+        out |= ((p + (p >> 8)) >> 8) << (8 * ch);
+    }
+    return out;
+}
+
 static void pixel_f32(const geo_frame* f, const cam_f32* cam, const fconsts* k, int mode, const float* fan, uint32_t n_fan,
                       const uint32_t* sky, uint32_t sw, uint32_t sh, int opaque, int composite, uint32_t width,
                       uint32_t height, uint32_t px, uint32_t py, uint32_t* rgba, uint8_t* bh_out, float* uv,
@@ -652,46 +696,8 @@ static void pixel_f32(const geo_frame* f, const cam_f32* cam, const fconsts* k, 
         if (!composite) *rgba = 0xFF000000u; /* composite: a discarded fragment keeps the target */
         return;
     }
-    /* bilinear LOD-0, U wraps, V clamps, 8-bit sub-texel weights; per
-     * channel: horizontal lerp truncated to 8 bits, vertical lerp rounded;
-     * then the alpha blend over (0,0,0,1): round(c*a/255), alpha 255. */
-    /* texel coordinates in 1/256 texel units: n = floor(256 (U sw - 1/2));
-     * texel floor(n / 256), 8-bit weight n mod 256 */
-    int nx = (int)floorf(fmaf(U, (float)sw * 256.0f, -128.0f));
-    int ny = (int)floorf(fmaf(V, (float)sh * 256.0f, -128.0f));
-    uint32_t wx = (uint32_t)nx & 255u;
-    uint32_t wy = (uint32_t)ny & 255u;
-    int ix0 = nx >> 8, iy0 = ny >> 8;
-    int w = (int)sw, h = (int)sh;
-    if (ix0 < 0) ix0 += w;
-    if (ix0 >= w) ix0 -= w;
-    int ix1 = (ix0 + 1 == w) ? 0 : ix0 + 1;
-    int iy1 = iy0 + 1;
-    iy0 = iy0 < 0 ? 0 : (iy0 > h - 1 ? h - 1 : iy0);
-    iy1 = iy1 < 0 ? 0 : (iy1 > h - 1 ? h - 1 : iy1);
-    uint32_t t[4] = {sky[(uint32_t)iy0 * sw + (uint32_t)ix0], sky[(uint32_t)iy0 * sw + (uint32_t)ix1],
-                     sky[(uint32_t)iy1 * sw + (uint32_t)ix0], sky[(uint32_t)iy1 * sw + (uint32_t)ix1]};
-    uint32_t c[4];
-    for (int ch = 0; ch < 4; ++ch) {
-        uint32_t v00 = (t[0] >> (8 * ch)) & 255u, v10 = (t[1] >> (8 * ch)) & 255u;
-        uint32_t v01 = (t[2] >> (8 * ch)) & 255u, v11 = (t[3] >> (8 * ch)) & 255u;
-        uint32_t top = (v00 * (256u - wx) + v10 * wx) >> 8;
-        uint32_t bot = (v01 * (256u - wx) + v11 * wx) >> 8;
-        c[ch] = (top * (256u - wy) + bot * wy + 128u) >> 8;
-    }
-    /* BlendState::ALPHA_BLENDING (pipeline.rs:49) over the target d, 8-bit
-     * fixed point: rgb = round((s a + d (255 - a))/255), alpha = round((255 a
-     * + d_a (255 - a))/255); without GEO_FLAG_COMPOSITE d = the clear colour
-     * (0,0,0,255). */
-    uint32_t dst = composite ? *rgba : 0xFF000000u;
-    uint32_t a = c[3], out[4];
-    for (int ch = 0; ch < 4; ++ch) {
-        uint32_t sv = ch < 3 ? c[ch] : 255u;
-        uint32_t p = sv * a + ((dst >> (8 * ch)) & 255u) * (255u - a) + 128u;
-        out[ch] = (p + (p >> 8)) >> 8;
-    }
+    *rgba = blend_over(bilinear_level(sky, sw, sh, U, V), composite ? *rgba : 0xFF000000u);
     (void)opaque; /* all-opaque skies take the same formula (a = 255: out = s) */
-    *rgba = out[0] | (out[1] << 8) | (out[2] << 16) | (out[3] << 24);
 }
 
 typedef struct {
@@ -832,6 +838,209 @@ int geo_oracle_render_f32(const geo_frame* f, const geo_scene* s, const float* f
     j.uv = uv;
     j.steps = steps;
     return run_jobs(&j, threads, job_f32, steps_total);
+}
+
+/* ---- GEO_FLAG_MIPS: the specification of geo_pixel.h restated ---------
+ * (DESIGN.md §3): a 4-level box-filtered mip chain (basic_sphere_buffer.rs:
+ * 31-36), the level of detail from the UV differences across each frame-
+ * aligned 2 x 2 pixel quad, trilinear between two bilinear level samples
+ * (textureSample, shader.wgsl:101). */
+#define O_MIP_LEVELS 4
+
+static uint32_t mipdim(uint32_t d, int l) {
+    uint32_t r = d >> l;
+    return r ? r : 1u;
+}
+
+uint64_t geo_oracle_mip_chain_texels(uint32_t w, uint32_t h) {
+    uint64_t n = 0;
+    for (int l = 0; l < O_MIP_LEVELS; ++l) n += (uint64_t)mipdim(w, l) * mipdim(h, l);
+    return n;
+}
+
+/* out: the levels one after another, level 0 = the texture; texel (x, y) of
+ * level l+1 = (a + b + c + d + 2) >> 2 per channel over (2x..2x+1, 2y..2y+1)
+ * of level l, indices clamped to level l */
+void geo_oracle_mip_chain(const uint8_t* rgba8, uint32_t w, uint32_t h, uint32_t* out) {
+    memcpy(out, rgba8, (size_t)w * h * 4);
+    const uint32_t* src = out;
+    uint32_t sw = w, sh = h;
+    uint32_t* dst = out + (size_t)w * h;
+    for (int l = 1; l < O_MIP_LEVELS; ++l) {
+        uint32_t dw = mipdim(w, l), dh = mipdim(h, l);
+        for (uint32_t y = 0; y < dh; ++y)
+            for (uint32_t x = 0; x < dw; ++x) {
+                uint32_t xs[2] = {2 * x < sw ? 2 * x : sw - 1, 2 * x + 1 < sw ? 2 * x + 1 : sw - 1};
+                uint32_t ys[2] = {2 * y < sh ? 2 * y : sh - 1, 2 * y + 1 < sh ? 2 * y + 1 : sh - 1};
+                uint32_t o = 0;
+                for (int ch = 0; ch < 4; ++ch) {
+                    uint32_t sum = 2;
+                    for (int j = 0; j < 2; ++j)
+                        for (int i = 0; i < 2; ++i) sum += (src[(size_t)ys[j] * sw + xs[i]] >> (8 * ch)) & 255u;
+                    o |= (sum >> 2) << (8 * ch);
+                }
+                dst[(size_t)y * dw + x] = o;
+            }
+        src = dst;
+        dst += (size_t)dw * dh;
+        sw = dw;
+        sh = dh;
+    }
+}
+
+/* 256 lambda, lambda = log2(rho2)/2 clamped to [0, 3]; log2(1 + t) by the
+ * fixed polynomial t (c1 + t (c2 + t (c3 + t c4))) */
+static uint32_t lod_q8(float rho2) {
+    if (!(rho2 > 1.0f)) return 0u;
+    if (!(rho2 < 64.0f)) return 768u;
+    uint32_t b;
+    memcpy(&b, &rho2, 4);
+    float e = (float)((int32_t)(b >> 23) - 127);
+    uint32_t mb = (b & 0x007FFFFFu) | 0x3F800000u;
+    float m;
+    memcpy(&m, &mb, 4);
+    float t = m - 1.0f;
+    float p = t * fmaf(t, fmaf(t, fmaf(t, -0x1.59455ap-4f, 0x1.4b69f0p-2f), -0x1.5b2e8ap-1f), 0x1.7044aep+0f);
+    float l2 = e + p;
+    int32_t q = (int32_t)floorf(l2 * 128.0f);
+    return q < 0 ? 0u : ((uint32_t)q < 768u ? (uint32_t)q : 768u);
+}
+
+void geo_oracle_lod_q8_n(const float* rho2, uint32_t n, uint32_t* out) {
+    for (uint32_t i = 0; i < n; ++i) out[i] = lod_q8(rho2[i]);
+}
+
+/* the quad footprint in level-0 texels^2: max over the x and y differences */
+static float mip_rho2(float dux, float dvx, float duy, float dvy, float w, float h) {
+    float ax = dux * w, bx = dvx * h, ay = duy * w, by = dvy * h;
+    float rx = fmaf(bx, bx, ax * ax), ry = fmaf(by, by, ay * ay);
+    return rx > ry ? rx : ry;
+}
+
+typedef struct {
+    const geo_frame* f;
+    const cam_f32* cam;
+    const fconsts* k;
+    int mode;
+    const float* fan;
+    uint32_t n_fan;
+    const uint32_t* sky;
+    uint32_t sw, sh, width, height, r_lo, gw, gh;
+    int threads, tid;
+    float* uv;
+    uint8_t* bh;
+    uint32_t* steps;
+} grid_job;
+
+/* UV, black-hole flag and steps of every pixel of the quad-aligned grid
+ * (columns 0..gw-1, rows r_lo..r_lo+gh-1), the quads' helpers outside the
+ * frame included (the camera of the width x height frame, extrapolated) */
+static void* job_grid(void* arg) {
+    grid_job* g = (grid_job*)arg;
+    for (uint32_t r = (uint32_t)g->tid; r < g->gh; r += (uint32_t)g->threads)
+        for (uint32_t x = 0; x < g->gw; ++x) {
+            size_t o = (size_t)r * g->gw + x;
+            uint32_t rgba = 0;
+            pixel_f32(g->f, g->cam, g->k, g->mode, g->fan, g->n_fan, g->sky, g->sw, g->sh, 1, 0, g->width, g->height,
+                      x, g->r_lo + r, &rgba, &g->bh[o], &g->uv[2 * o], &g->steps[o]);
+        }
+    return NULL;
+}
+
+int geo_oracle_render_mips_f32(const geo_frame* f, const geo_scene* s, const float* fan, uint32_t n_fan,
+                               const uint8_t* sky, uint32_t sky_w, uint32_t sky_h, uint32_t width, uint32_t height,
+                               uint32_t row0, uint32_t nrows, int threads, uint8_t* rgba, uint8_t* mask, float* uv,
+                               uint32_t* steps, uint64_t* steps_total) {
+    if (!f || !s || !sky || !rgba || width == 0 || height == 0 || nrows == 0 || (row0 & 1u)) return -1;
+    if ((uint64_t)row0 + nrows > height) return -1;
+    if (s->mode == GEO_MODE_FAN && (!fan || n_fan < 2)) return -1;
+    if (threads < 1) threads = 1;
+    if (threads > 64) threads = 64;
+    uint32_t* chain = (uint32_t*)malloc(geo_oracle_mip_chain_texels(sky_w, sky_h) * 4);
+    uint32_t gw = width + (width & 1u), gh = nrows + (nrows & 1u);
+    float* guv = (float*)malloc((size_t)gw * gh * 2 * sizeof(float));
+    uint8_t* gbh = (uint8_t*)malloc((size_t)gw * gh);
+    uint32_t* gst = (uint32_t*)malloc((size_t)gw * gh * 4);
+    grid_job* jobs = (grid_job*)calloc((size_t)threads, sizeof(grid_job));
+    pthread_t* th = (pthread_t*)calloc((size_t)threads, sizeof(pthread_t));
+    if (!chain || !guv || !gbh || !gst || !jobs || !th) {
+        free(chain); free(guv); free(gbh); free(gst); free(jobs); free(th);
+        return -3;
+    }
+    geo_oracle_mip_chain(sky, sky_w, sky_h, chain);
+    int opaque = 1;
+    for (size_t i = 0; i < (size_t)sky_w * sky_h; ++i)
+        if (sky[4 * i + 3] != 255u) {
+            opaque = 0;
+            break;
+        }
+    fconsts k = make_fconsts(s);
+    cam_f32 cam = camera_f32(f, width, height);
+    for (int t = 0; t < threads; ++t) {
+        grid_job g = {f, &cam, &k, (int)s->mode, fan, n_fan, chain, sky_w, sky_h, width, height, row0, gw, gh,
+                      threads, t, guv, gbh, gst};
+        jobs[t] = g;
+        if (t > 0 && pthread_create(&th[t], NULL, job_grid, &jobs[t]) != 0) jobs[t].tid = -1;
+    }
+    job_grid(&jobs[0]);
+    for (int t = 1; t < threads; ++t) {
+        if (jobs[t].tid < 0) {
+            jobs[t].tid = t;
+            job_grid(&jobs[t]);
+        } else {
+            pthread_join(th[t], NULL);
+        }
+    }
+    const uint32_t* lvl[O_MIP_LEVELS];
+    uint32_t lw[O_MIP_LEVELS], lh[O_MIP_LEVELS];
+    const uint32_t* p = chain;
+    for (int l = 0; l < O_MIP_LEVELS; ++l) {
+        lvl[l] = p;
+        lw[l] = mipdim(sky_w, l);
+        lh[l] = mipdim(sky_h, l);
+        p += (size_t)lw[l] * lh[l];
+    }
+    int composite = (s->flags & GEO_FLAG_COMPOSITE) != 0;
+    uint64_t total = 0;
+    for (uint32_t r = 0; r < nrows; ++r)
+        for (uint32_t x = 0; x < width; ++x) {
+            size_t o = (size_t)r * gw + x, oo = (size_t)r * width + x;
+            size_t ox = (size_t)r * gw + (x ^ 1u), oy = (size_t)(r ^ 1u) * gw + x;
+            float U = guv[2 * o], V = guv[2 * o + 1];
+            /* each row's and each column's own difference, the higher-index pixel minus the lower */
+            float dux = (x & 1u) ? U - guv[2 * ox] : guv[2 * ox] - U;
+            float dvx = (x & 1u) ? V - guv[2 * ox + 1] : guv[2 * ox + 1] - V;
+            float duy = (r & 1u) ? U - guv[2 * oy] : guv[2 * oy] - U;
+            float dvy = (r & 1u) ? V - guv[2 * oy + 1] : guv[2 * oy + 1] - V;
+            uint32_t q = lod_q8(mip_rho2(dux, dvx, duy, dvy, (float)sky_w, (float)sky_h));
+            uint32_t l0 = q >> 8, wf = q & 255u, l1 = l0 + 1 < O_MIP_LEVELS ? l0 + 1 : l0;
+            uint32_t s0 = bilinear_level(lvl[l0], lw[l0], lh[l0], U, V);
+            uint32_t s1 = bilinear_level(lvl[l1], lw[l1], lh[l1], U, V);
+            uint32_t sm = 0;
+            for (int ch = 0; ch < 4; ++ch) {
+                uint32_t a0 = (s0 >> (8 * ch)) & 255u, a1 = (s1 >> (8 * ch)) & 255u;
+                sm |= ((a0 * (256u - wf) + a1 * wf + 128u) >> 8) << (8 * ch);
+            }
+            uint32_t dst;
+            memcpy(&dst, rgba + 4 * oo, 4);
+            uint32_t out;
+            if (gbh[o])
+                out = composite ? dst : 0xFF000000u;
+            else
+                out = blend_over(sm, composite ? dst : 0xFF000000u);
+            (void)opaque;
+            memcpy(rgba + 4 * oo, &out, 4);
+            if (mask) mask[oo] = gbh[o];
+            if (uv) {
+                uv[2 * oo] = U;
+                uv[2 * oo + 1] = V;
+            }
+            if (steps) steps[oo] = gst[o];
+            total += gst[o];
+        }
+    if (steps_total) *steps_total = total;
+    free(chain); free(guv); free(gbh); free(gst); free(jobs); free(th);
+    return 0;
 }
 
 int geo_oracle_render_f64(const geo_frame* f, const geo_scene* s, const float* fan, uint32_t n_fan,

@@ -75,6 +75,18 @@ int geo_oracle_render_f32(const geo_frame* f, const geo_scene* s, const float* f
                           int threads, uint8_t* rgba, uint8_t* mask, float* uv, uint32_t* steps,
                           uint64_t* steps_total);
 
+/* GEO_FLAG_MIPS mirror (geo_pixel.h): the 4-level box-filtered mip chain
+ * (levels one after another, geo_oracle_mip_chain_texels(w, h) texels), and
+ * rows [row0, row0 + nrows) (row0 even) sampled trilinearly with the level of
+ * detail from each frame-aligned 2 x 2 quad's UV differences. */
+uint64_t geo_oracle_mip_chain_texels(uint32_t w, uint32_t h);
+void geo_oracle_mip_chain(const uint8_t* rgba8, uint32_t w, uint32_t h, uint32_t* out);
+void geo_oracle_lod_q8_n(const float* rho2, uint32_t n, uint32_t* out); /* 256 lambda per footprint */
+int geo_oracle_render_mips_f32(const geo_frame* f, const geo_scene* s, const float* fan, uint32_t n_fan,
+                               const uint8_t* sky, uint32_t sky_w, uint32_t sky_h, uint32_t width, uint32_t height,
+                               uint32_t row0, uint32_t nrows, int threads, uint8_t* rgba, uint8_t* mask, float* uv,
+                               uint32_t* steps, uint64_t* steps_total);
+
 /* Traveled angle of one ray in the f32 kernel order (direct or adaptive mode
  * by s->mode) for (sin theta, cos theta) of the central-frame direction. */
 float geo_oracle_geodesic_f32(const geo_scene* s, float st, float ct, uint32_t* steps);

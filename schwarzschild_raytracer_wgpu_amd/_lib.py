@@ -25,6 +25,7 @@ GEO_ADAPTIVE_DEFAULT_TOL = 1e-6
 GEO_ADAPTIVE_MAX_GROWTH = 16
 GEO_FLAG_DEFER_STEPS = 1
 GEO_FLAG_COMPOSITE = 2
+GEO_FLAG_MIPS = 4
 
 GEO_RAYS_NEAR = 1
 GEO_RAYS_FAR = 2

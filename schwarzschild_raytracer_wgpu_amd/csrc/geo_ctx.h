@@ -9,9 +9,16 @@
 struct geo_ctx {
     int device;
     int num_cus;
+    // The sky's mip chain (geo::kSkyMipLevels levels, geo::mip_down), each
+    // level padded (geo::pad_sky) and stored one after another in `sky`:
+    // level l at byte sky_lvl_off[l], (sky_lvl_w[l] + 2) x (sky_lvl_h[l] + 2)
+    // texels; level 0 first, so a level-0 render reads `sky` as before.
     uint32_t* sky;
     uint32_t sky_w, sky_h;
     bool sky_opaque;
+    static constexpr int kSkyLevels = 4;
+    uint32_t sky_lvl_w[kSkyLevels], sky_lvl_h[kSkyLevels], sky_lvl_off[kSkyLevels];
+    uint32_t sky_total_bytes;
     // Ray fan, double-buffered so that a frame's fan can be solved on a side
     // stream while the previous frame's fan-mode draws still read the other
     // buffer.  fan[fan_cur] is the context's fan (fan_cur < 0: none).  Each

@@ -1184,16 +1184,107 @@ GEO_HD uint32_t composite_(uint32_t s, uint32_t d) {
     return r | (g << 8) | (b << 16) | (al << 24);
 }
 
+// ---- GEO_FLAG_MIPS: the reference's mip-mapped sky (textureSample) ----
+//
+// The reference samples a 4-level mip chain (Texture::new_with_mipmaps(...,
+// 4), basic_sphere_buffer.rs:31-36) with implicit derivatives (textureSample,
+// shader.wgsl:101).  Its mip generator and sampler live in the absent
+// wgpu_renderer submodule, so this specification fixes them:
+//   * level l is max(1, w >> l) x max(1, h >> l); texel (x, y) of level l+1 =
+//     the rounded mean (a + b + c + d + 2) >> 2 per channel of the 2 x 2 block
+//     (2x..2x+1, 2y..2y+1) of level l, indices clamped to level l (box filter);
+//   * the footprint from the UV differences across the pixel's 2 x 2 quad
+//     (frame-aligned: x pairs 2i, 2i+1; y pairs 2j, 2j+1), each row's and
+//     each column's own difference (WGSL leaves coarse or fine to the
+//     implementation), U unwrapped as textureSample sees it (the seam takes the
+//     coarsest level, as in the reference);
+//   * rho2 = max((dU/dx W)^2 + (dV/dx H)^2, (dU/dy W)^2 + (dV/dy H)^2) in
+//     level-0 texels, lambda = log2(rho2)/2 clamped to [0, 3] and taken in
+//     1/256 steps (lod_q8); trilinear: bilinear samples of levels floor(lambda)
+//     and floor(lambda) + 1 (U wraps, V clamps, as level 0), blended with the
+//     8-bit weight frac(lambda) like the vertical bilinear lerp.
+constexpr int kSkyMipLevels = 4;
+
+GEO_HD uint32_t mip_dim(uint32_t d, int l) {
+    const uint32_t r = d >> l;
+    return r ? r : 1u;
+}
+
+// Level l + 1 of a w x h level (row-major RGBA8 texels as u32): the rounded
+// 2 x 2 box mean, block indices clamped to the level.
+GEO_HD void mip_down(const uint32_t* src, uint32_t w, uint32_t h, uint32_t* dst) {
+    const uint32_t w2 = mip_dim(w, 1), h2 = mip_dim(h, 1);
+    for (uint32_t y = 0; y < h2; ++y) {
+        const uint32_t y0 = 2u * y < h ? 2u * y : h - 1u, y1 = 2u * y + 1u < h ? 2u * y + 1u : h - 1u;
+        for (uint32_t x = 0; x < w2; ++x) {
+            const uint32_t x0 = 2u * x < w ? 2u * x : w - 1u, x1 = 2u * x + 1u < w ? 2u * x + 1u : w - 1u;
+            const uint32_t t00 = src[(size_t)y0 * w + x0], t10 = src[(size_t)y0 * w + x1];
+            const uint32_t t01 = src[(size_t)y1 * w + x0], t11 = src[(size_t)y1 * w + x1];
+            uint32_t o = 0;
+            for (int c = 0; c < 4; ++c) {
+                const uint32_t sh = 8u * (uint32_t)c;
+                const uint32_t sum = ((t00 >> sh) & 255u) + ((t10 >> sh) & 255u) + ((t01 >> sh) & 255u) +
+                                     ((t11 >> sh) & 255u) + 2u;
+                o |= (sum >> 2) << sh;
+            }
+            dst[(size_t)y * w2 + x] = o;
+        }
+    }
+}
+
+// log2(1 + t), t in [0, 1): fixed polynomial, max error 1.9e-4 (far below
+// the 1/512 resolution of lod_q8's lambda).
+GEO_HD float log2_1p_(float t) {
+    return t * fmaf_(t, fmaf_(t, fmaf_(t, -0x1.59455ap-4f, 0x1.4b69f0p-2f), -0x1.5b2e8ap-1f), 0x1.7044aep+0f);
+}
+
+// 256 lambda, lambda = log2(rho2)/2 clamped to [0, kSkyMipLevels - 1]:
+// rho2 <= 1 (magnification) or NaN gives 0, rho2 >= 2^6 gives 768.
+GEO_HD uint32_t lod_q8(float rho2) {
+    if (!(rho2 > 1.0f)) return 0u;
+    if (!(rho2 < 64.0f)) return 256u * (uint32_t)(kSkyMipLevels - 1);
+    uint32_t b;
+    __builtin_memcpy(&b, &rho2, 4);
+    const float e = (float)((int32_t)(b >> 23) - 127);  // 0..5
+    const uint32_t mb = (b & 0x007FFFFFu) | 0x3F800000u;
+    float m;
+    __builtin_memcpy(&m, &mb, 4);
+    const float l2 = e + log2_1p_(m - 1.0f);  // log2(rho2) in [0, 6]
+    const int32_t q = floor_i32_(l2 * 128.0f);
+    const uint32_t qmax = 256u * (uint32_t)(kSkyMipLevels - 1);
+    return q < 0 ? 0u : ((uint32_t)q < qmax ? (uint32_t)q : qmax);
+}
+
+// The squared footprint in level-0 texels from the quad differences.
+GEO_HD float mip_rho2(float dux, float dvx, float duy, float dvy, float w, float h) {
+    const float ax = dux * w, bx = dvx * h, ay = duy * w, by = dvy * h;
+    const float rx = fmaf_(bx, bx, ax * ax), ry = fmaf_(by, by, ay * ay);
+    return rx > ry ? rx : ry;
+}
+
+// The trilinear blend of two level samples with the 8-bit weight f (packed
+// channel pairs, as the vertical bilinear lerp).
+GEO_HD uint32_t mip_blend(uint32_t s0, uint32_t s1, uint32_t f) {
+    const uint32_t i = 256u - f;
+    const uint32_t rb = ga_perm_(lerp2_(rb_(s0), rb_(s1), i, f) + 0x00800080u);
+    const uint32_t ga = ga_perm_(lerp2_(ga_perm_(s0), ga_perm_(s1), i, f) + 0x00800080u);
+    return rb | (ga << 8);
+}
+
+// The blend of a sample over the cleared target (sample_sky_qf's epilogue).
+GEO_HD uint32_t over_clear(uint32_t s, bool opaque) {
+    if (opaque) return s | 0xFF000000u;
+    const uint32_t a = s >> 24;
+    return blend255_(s & 0xFFu, a) | (blend255_((s >> 8) & 0xFFu, a) << 8) | (blend255_((s >> 16) & 0xFFu, a) << 16) |
+           0xFF000000u;
+}
+
 // A sample over the cleared target (0,0,0,1) (renderer.rs:233-238): rgb*a/255,
 // alpha 1.  `opaque` (every texel alpha 255, checked on upload) skips the
 // blend, which is exact there.
 template <typename Quad>
 GEO_HD uint32_t sample_sky_qf(const Quad& quad, float tw256, float th256, bool opaque, float U, float V) {
-    const uint32_t s = sample_sky_quad_f(quad, tw256, th256, U, V);
-    if (opaque) return s | 0xFF000000u;
-    const uint32_t a = s >> 24;
-    return blend255_(s & 0xFFu, a) | (blend255_((s >> 8) & 0xFFu, a) << 8) |
-           (blend255_((s >> 16) & 0xFFu, a) << 16) | 0xFF000000u;
+    return over_clear(sample_sky_quad_f(quad, tw256, th256, U, V), opaque);
 }
 template <typename Quad>
 GEO_HD uint32_t sample_sky_q(const Quad& quad, uint32_t tw, uint32_t th, bool opaque, float U, float V) {

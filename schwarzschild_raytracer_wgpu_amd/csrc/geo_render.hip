@@ -76,6 +76,12 @@ struct RenderArgs {
     uint32_t sky_w, sky_h;
     float sky_w256, sky_h256;  // sky_w * 256, sky_h * 256 (exact; geo::sample_sky_quad_f)
     uint32_t sky_pitch_b, sky_bytes;
+    // GEO_FLAG_MIPS: level l's byte offset, pitch and sizes * 256; level 0's
+    // size for the footprint; the whole chain's bytes
+    uint32_t mip_off[geo::kSkyMipLevels], mip_pitch[geo::kSkyMipLevels];
+    float mip_w256[geo::kSkyMipLevels], mip_h256[geo::kSkyMipLevels];
+    float sky_wf, sky_hf;
+    uint32_t sky_total_bytes;
     const float* fan;
     uint32_t n_fan;
     uint32_t* out_rgba;
@@ -119,6 +125,51 @@ struct PaddedSkyQuad {
     }
 };
 
+// The texel quad of one mip level of the padded chain (geo_ctx::sky): like
+// PaddedSkyQuad at a per-lane level, so base and pitch are vector values.
+struct LevelQuad {
+    __amdgpu_buffer_rsrc_t rsrc;
+    uint32_t base, pitch_b;
+    __device__ __forceinline__ void operator()(int ix0, int iy0, uint32_t (&t)[4]) const {
+        const uint32_t off = base + __umul24((uint32_t)(iy0 + 1), pitch_b) + ((uint32_t)(ix0 + 1) << 2);
+        t[0] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rsrc, off, 0, 0);
+        t[1] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rsrc, off + 4u, 0, 0);
+        t[2] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rsrc, off + pitch_b, 0, 0);
+        t[3] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rsrc, off + pitch_b + 4u, 0, 0);
+    }
+};
+
+template <typename T>
+__device__ __forceinline__ T level_sel(const T (&v)[geo::kSkyMipLevels], uint32_t l) {
+    static_assert(geo::kSkyMipLevels == 4, "four levels");
+    return l == 0u ? v[0] : (l == 1u ? v[1] : (l == 2u ? v[2] : v[3]));
+}
+
+// The trilinear sample (GEO_FLAG_MIPS, geo_pixel.h): levels floor(lambda) and
+// the next, blended with frac(lambda) in 8 bits.
+__device__ __forceinline__ uint32_t sample_trilinear(const RenderArgs& a, float rho2, float U, float V) {
+    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(a.sky), 0,
+                                                                           (int)a.sky_total_bytes, kBufferRsrcWord3);
+    const uint32_t q = geo::lod_q8(rho2);
+    const uint32_t l0 = q >> 8, f = q & 255u;
+    const uint32_t l1 = l0 + 1u < (uint32_t)geo::kSkyMipLevels ? l0 + 1u : l0;
+    const uint32_t s0 = geo::sample_sky_quad_f(LevelQuad{rsrc, level_sel(a.mip_off, l0), level_sel(a.mip_pitch, l0)},
+                                               level_sel(a.mip_w256, l0), level_sel(a.mip_h256, l0), U, V);
+    const uint32_t s1 = geo::sample_sky_quad_f(LevelQuad{rsrc, level_sel(a.mip_off, l1), level_sel(a.mip_pitch, l1)},
+                                               level_sel(a.mip_w256, l1), level_sel(a.mip_h256, l1), U, V);
+    return geo::mip_blend(s0, s1, f);
+}
+
+// The value of v in lane ^ 1 (DPP quad_perm [1, 0, 3, 2]) and in lane ^ 16
+// (ds_swizzle, bit mode: and 0x1F, xor 0x10, within 32-lane halves): the
+// x and y partners of the pixel's 2 x 2 quad in the 16 x 4 wave.
+__device__ __forceinline__ float lane_xor1(float v) {
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float lane_xor16(float v) {
+    return __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(v), 0x401F));
+}
+
 // Epilogue of one pixel (shader.wgsl:88-105): black-hole test, sky UV,
 // bilinear sample, blend and the optional outputs at index o.
 __device__ __forceinline__ void shade_pixel(const RenderArgs& a, float c2x, float c2y, float ct, float rct,
@@ -147,7 +198,38 @@ __device__ __forceinline__ void shade_pixel(const RenderArgs& a, float c2x, floa
     if (a.out_steps) a.out_steps[o] = steps;
 }
 
+// GEO_FLAG_MIPS epilogue: the pixel's UV and its quad footprint rho2 are
+// known; the trilinear sample in place of the level-0 one.
+__device__ __forceinline__ void shade_pixel_mips(const RenderArgs& a, float lam, float U, float V, float rho2,
+                                                 uint32_t steps, size_t o) {
+    const bool bh = lam < geo::kBlackHoleLambda;
+    if (a.composite) {
+        if (!bh) {
+            const uint32_t s = sample_trilinear(a, rho2, U, V);
+            a.out_rgba[o] = a.sky_opaque ? s : geo::composite_(s, a.out_rgba[o]);
+        }
+    } else {
+        a.out_rgba[o] = bh ? geo::kBlackRGBA : geo::over_clear(sample_trilinear(a, rho2, U, V), a.sky_opaque != 0);
+    }
+    if (a.out_mask) a.out_mask[o] = bh ? 1 : 0;
+    if (a.out_uv) a.out_uv[o] = make_float2(U, V);
+    if (a.out_steps) a.out_steps[o] = steps;
+}
+
+// The pixel's traveled-angle result lambda' (pi/2 - angle) by mode.
 template <int MODE, int KIND>
+__device__ __forceinline__ float pixel_lambda(const RenderArgs& a, float st, float ct, float rct, uint32_t* steps) {
+    if constexpr (MODE == GEO_MODE_FAN) {
+        *steps = 0;
+        return geo::fan_lerp(a.fan, a.n_fan, st);
+    } else if constexpr (MODE == GEO_MODE_ADAPTIVE) {
+        return geo::kPi2 - geo::geodesic_angle_adaptive<KIND>(a.k, st, ct, rct, steps);
+    } else {
+        return geo::kPi2 - geo::geodesic_angle_v<KIND>(a.k, st, ct, rct, steps);
+    }
+}
+
+template <int MODE, int KIND, bool MIPS>
 __global__ __launch_bounds__(kBlock) void geo_render_kernel(const RenderArgs a) {
     const uint2 tile = make_uint2(blockIdx.x, a.tile_y0 + blockIdx.y);
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x) >> 6;
@@ -161,22 +243,39 @@ __global__ __launch_bounds__(kBlock) void geo_render_kernel(const RenderArgs a) 
     const uint32_t band = __umulhi(wl0, a.band_magic);
     const uint32_t py = a.row0 + band * a.band_stride + (wl0 - band * a.band_rows) + (ly - wl0);
     uint32_t steps = 0;
-    if (px < a.width && ly < a.nrows && py < a.height) {
+    const bool in_frame = px < a.width && ly < a.nrows && py < a.height;
+    if constexpr (!MIPS) {
+        if (in_frame) {
+            float c2x, c2y, c2z;
+            geo::pixel_central_dir(a.cam, a.frame.movement_to_central, a.frame.psi_factor_and_position[0], a.kt, px,
+                                   py, &c2x, &c2y, &c2z);
+            const float st = geo::central_sin(c2z);
+            const float ct = geo::central_rho(c2x, c2y);
+            const float rct = geo::rcpf_(ct);  // shared by the ray's 1/b^2 and its sky direction
+            const float lam = pixel_lambda<MODE, KIND>(a, st, ct, rct, &steps);
+            shade_pixel(a, c2x, c2y, ct, rct, lam, steps, (size_t)ly * a.width + px);
+        }
+    } else {
+        // Every lane traces its pixel, the ones outside the frame or the
+        // requested rows too (the helpers of the frame-aligned 2 x 2 quads,
+        // as a fragment shader's): the footprint needs all four UVs of a quad.
+        // Black-hole pixels keep their UV as well (textureSample runs before
+        // the discard, shader.wgsl:101-104).
         float c2x, c2y, c2z;
         geo::pixel_central_dir(a.cam, a.frame.movement_to_central, a.frame.psi_factor_and_position[0], a.kt, px, py,
                                &c2x, &c2y, &c2z);
         const float st = geo::central_sin(c2z);
         const float ct = geo::central_rho(c2x, c2y);
-        const float rct = geo::rcpf_(ct);  // shared by the ray's 1/b^2 and its sky direction
-        float lam;
-        if constexpr (MODE == GEO_MODE_FAN) {
-            lam = geo::fan_lerp(a.fan, a.n_fan, st);
-        } else if constexpr (MODE == GEO_MODE_ADAPTIVE) {
-            lam = geo::kPi2 - geo::geodesic_angle_adaptive<KIND>(a.k, st, ct, rct, &steps);
-        } else {
-            lam = geo::kPi2 - geo::geodesic_angle_v<KIND>(a.k, st, ct, rct, &steps);
-        }
-        shade_pixel(a, c2x, c2y, ct, rct, lam, steps, (size_t)ly * a.width + px);
+        const float rct = geo::rcpf_(ct);
+        const float lam = pixel_lambda<MODE, KIND>(a, st, ct, rct, &steps);
+        float U, V;
+        geo::sky_uv(a.frame.central_to_uv, c2x, c2y, ct, rct, lam, &U, &V);
+        const float ux = lane_xor1(U), vx = lane_xor1(V), uy = lane_xor16(U), vy = lane_xor16(V);
+        const float rho2 = geo::mip_rho2(U - ux, V - vx, U - uy, V - vy, a.sky_wf, a.sky_hf);
+        if (in_frame)
+            shade_pixel_mips(a, lam, U, V, rho2, steps, (size_t)ly * a.width + px);
+        else
+            steps = 0;
     }
     if constexpr (MODE != GEO_MODE_FAN) {
         if (a.step_slots) {
@@ -623,33 +722,50 @@ void geo_ctx_destroy(geo_ctx* c) {
 }
 
 int geo_set_sky(geo_ctx* c, const uint8_t* rgba8, uint32_t w, uint32_t h) {
-    // the padded copy must stay below 2^31 bytes (32-bit buffer offsets, PaddedSkyQuad)
-    if (!c || !rgba8 || w == 0 || h == 0 || w > (1u << 20) || h > (1u << 20) ||
-        ((uint64_t)w + 2u) * ((uint64_t)h + 2u) * 4u >= (1ull << 31))
-        return GEO_EINVAL;
+    static_assert(geo_ctx::kSkyLevels == geo::kSkyMipLevels, "one mip chain");
+    if (!c || !rgba8 || w == 0 || h == 0 || w > (1u << 20) || h > (1u << 20)) return GEO_EINVAL;
+    // the padded chain must stay below 2^31 bytes (32-bit buffer offsets, PaddedSkyQuad / LevelQuad)
+    uint32_t lw[geo_ctx::kSkyLevels], lh[geo_ctx::kSkyLevels], loff[geo_ctx::kSkyLevels];
+    uint64_t total = 0;
+    for (int l = 0; l < geo_ctx::kSkyLevels; ++l) {
+        lw[l] = geo::mip_dim(w, l);
+        lh[l] = geo::mip_dim(h, l);
+        loff[l] = (uint32_t)total;
+        total += ((uint64_t)lw[l] + 2u) * ((uint64_t)lh[l] + 2u) * 4u;
+        if (total >= (1ull << 31)) return GEO_EINVAL;
+    }
     DeviceGuard g(c->device);
     if (!g.ok) return GEO_EHIP;
-    const size_t bytes = (size_t)w * h * 4;
-    const size_t padded = ((size_t)w + 2u) * ((size_t)h + 2u);
-    std::vector<uint32_t> pad(padded);
-    geo::pad_sky(rgba8, w, h, pad.data());
+    // the chain on the host: level 0 = the texture, level l + 1 = the 2 x 2
+    // box mean of level l (geo::mip_down), each padded for wrap/clamp
+    std::vector<uint32_t> lvl((size_t)w * h), next;
+    std::memcpy(lvl.data(), rgba8, (size_t)w * h * 4);
+    std::vector<uint32_t> pad(total / 4u);
+    for (int l = 0; l < geo_ctx::kSkyLevels; ++l) {
+        if (l > 0) {
+            next.resize((size_t)lw[l] * lh[l]);
+            geo::mip_down(lvl.data(), lw[l - 1], lh[l - 1], next.data());
+            lvl.swap(next);
+        }
+        geo::pad_sky(reinterpret_cast<const uint8_t*>(lvl.data()), lw[l], lh[l], pad.data() + loff[l] / 4u);
+    }
     // Renders of this context still running on any of the caller's streams
     // (non-blocking ones do not order against a blocking copy) may be reading
     // the current sky: let them finish before it is overwritten or freed.  A
     // sky change is a set-up call (the reference builds its texture once,
     // basic_sphere_buffer.rs:29-36), so the wait costs nothing per frame.
     if (wait_renders(c) != GEO_OK) return GEO_EHIP;
-    if (c->sky && ((size_t)c->sky_w + 2u) * ((size_t)c->sky_h + 2u) != padded) {
+    if (c->sky && c->sky_total_bytes != (uint32_t)total) {
         (void)hipFree(c->sky);
         c->sky = nullptr;
         c->sky_w = c->sky_h = 0;
     }
-    if (!c->sky && hipMalloc(&c->sky, padded * 4u) != hipSuccess) {
+    if (!c->sky && hipMalloc(&c->sky, total) != hipSuccess) {
         c->sky = nullptr;
         c->sky_w = c->sky_h = 0;
         return GEO_ENOMEM;
     }
-    if (hipMemcpy(c->sky, pad.data(), padded * 4u, hipMemcpyHostToDevice) != hipSuccess) {
+    if (hipMemcpy(c->sky, pad.data(), total, hipMemcpyHostToDevice) != hipSuccess) {
         // the buffer's contents are unknown now: no sky (renders return GEO_ESTATE until the next upload)
         (void)hipFree(c->sky);
         c->sky = nullptr;
@@ -658,9 +774,16 @@ int geo_set_sky(geo_ctx* c, const uint8_t* rgba8, uint32_t w, uint32_t h) {
     }
     c->sky_w = w;
     c->sky_h = h;
+    c->sky_total_bytes = (uint32_t)total;
+    for (int l = 0; l < geo_ctx::kSkyLevels; ++l) {
+        c->sky_lvl_w[l] = lw[l];
+        c->sky_lvl_h[l] = lh[l];
+        c->sky_lvl_off[l] = loff[l];
+    }
     bool opaque = true;
+    const size_t bytes = (size_t)w * h * 4;
     for (size_t i = 3; i < bytes && opaque; i += 4) opaque = rgba8[i] == 255;
-    c->sky_opaque = opaque;
+    c->sky_opaque = opaque;  // the means of opaque texels are opaque: every level
     return GEO_OK;
 }
 
@@ -753,12 +876,18 @@ constexpr uint32_t kMaxGridY = 65535;
 extern "C++" {
 // The last launch records `done` (render_event) as its stop event.
 template <int MODE, int KIND>
-static int launch_tiles(RenderArgs a, uint32_t tiles_x, uint32_t tiles_y, hipStream_t s, hipEvent_t done) {
+static int launch_tiles(RenderArgs a, bool mips, uint32_t tiles_x, uint32_t tiles_y, hipStream_t s,
+                        hipEvent_t done) {
     for (uint32_t y0 = 0; y0 < tiles_y; y0 += kMaxGridY) {
         a.tile_y0 = y0;
         const uint32_t ny = tiles_y - y0 < kMaxGridY ? tiles_y - y0 : kMaxGridY;
-        hipExtLaunchKernelGGL((geo_render_kernel<MODE, KIND>), dim3(tiles_x, ny), dim3(kBlock), 0, s, nullptr,
-                              y0 + ny >= tiles_y ? done : nullptr, 0, a);
+        hipEvent_t stop = y0 + ny >= tiles_y ? done : nullptr;
+        if (mips)
+            hipExtLaunchKernelGGL((geo_render_kernel<MODE, KIND, true>), dim3(tiles_x, ny), dim3(kBlock), 0, s,
+                                  nullptr, stop, 0, a);
+        else
+            hipExtLaunchKernelGGL((geo_render_kernel<MODE, KIND, false>), dim3(tiles_x, ny), dim3(kBlock), 0, s,
+                                  nullptr, stop, 0, a);
         if (hipGetLastError() != hipSuccess) return GEO_EHIP;
     }
     return GEO_OK;
@@ -771,7 +900,10 @@ static int render_impl(geo_ctx* c, const geo_frame* frame, const geo_scene* scen
                        uint32_t* out_steps, unsigned long long* steps_total, void* stream) {
     if (scene->mode != GEO_MODE_DIRECT && scene->mode != GEO_MODE_FAN && scene->mode != GEO_MODE_ADAPTIVE)
         return GEO_EINVAL;
-    if ((scene->flags & ~(GEO_FLAG_DEFER_STEPS | GEO_FLAG_COMPOSITE)) != 0) return GEO_EINVAL;
+    if ((scene->flags & ~(GEO_FLAG_DEFER_STEPS | GEO_FLAG_COMPOSITE | GEO_FLAG_MIPS)) != 0) return GEO_EINVAL;
+    // frame-aligned 2 x 2 quads: the rows a wave covers start on even frame rows
+    const bool mips = (scene->flags & GEO_FLAG_MIPS) != 0;
+    if (mips && ((row0 | band_stride) & 1u) != 0) return GEO_EINVAL;
     const bool adaptive = scene->mode == GEO_MODE_ADAPTIVE;
     // tol: 0 (default) or a positive finite tolerance in the adaptive mode, 0 otherwise
     if (adaptive ? !(scene->tol >= 0.0f && scene->tol <= 3.0e38f) : scene->tol != 0.0f) return GEO_EINVAL;
@@ -809,6 +941,15 @@ static int render_impl(geo_ctx* c, const geo_frame* frame, const geo_scene* scen
     a.sky_h256 = (float)c->sky_h * 256.0f;
     a.sky_pitch_b = (c->sky_w + 2u) * 4u;
     a.sky_bytes = a.sky_pitch_b * (c->sky_h + 2u);
+    for (int l = 0; l < geo::kSkyMipLevels; ++l) {
+        a.mip_off[l] = c->sky_lvl_off[l];
+        a.mip_pitch[l] = (c->sky_lvl_w[l] + 2u) * 4u;
+        a.mip_w256[l] = (float)c->sky_lvl_w[l] * 256.0f;
+        a.mip_h256[l] = (float)c->sky_lvl_h[l] * 256.0f;
+    }
+    a.sky_wf = (float)c->sky_w;
+    a.sky_hf = (float)c->sky_h;
+    a.sky_total_bytes = c->sky_total_bytes;
     const int fb = c->fan_cur;
     a.fan = fb < 0 ? nullptr : c->fan[fb];
     a.n_fan = fb < 0 ? 0u : c->n_fan[fb];
@@ -836,22 +977,22 @@ static int render_impl(geo_ctx* c, const geo_frame* frame, const geo_scene* scen
         // buffer's chain of readers (the wait is queued after the launch, so
         // it holds back only later work on s, never this render)
         if (c->fan_written_rec[fb] && hipStreamWaitEvent(s, c->fan_written[fb], 0) != hipSuccess) return GEO_EHIP;
-        st = launch_tiles<GEO_MODE_FAN, geo::kCurvedOut>(a, tiles_x, tiles_y, s, done);
+        st = launch_tiles<GEO_MODE_FAN, geo::kCurvedOut>(a, mips, tiles_x, tiles_y, s, done);
         if (st) return st;
         if (c->fan_read_rec[fb] && hipStreamWaitEvent(s, c->fan_read[fb], 0) != hipSuccess) return GEO_EHIP;
         if (hipEventRecord(c->fan_read[fb], s) != hipSuccess) return GEO_EHIP;
         c->fan_read_rec[fb] = true;
     } else if (adaptive) {
         switch (geo::geodesic_kind(a.k)) {
-            case geo::kCurvedOut: st = launch_tiles<GEO_MODE_ADAPTIVE, geo::kCurvedOut>(a, tiles_x, tiles_y, s, done); break;
-            case geo::kCurvedIn: st = launch_tiles<GEO_MODE_ADAPTIVE, geo::kCurvedIn>(a, tiles_x, tiles_y, s, done); break;
-            default: st = launch_tiles<GEO_MODE_ADAPTIVE, geo::kFlat>(a, tiles_x, tiles_y, s, done);
+            case geo::kCurvedOut: st = launch_tiles<GEO_MODE_ADAPTIVE, geo::kCurvedOut>(a, mips, tiles_x, tiles_y, s, done); break;
+            case geo::kCurvedIn: st = launch_tiles<GEO_MODE_ADAPTIVE, geo::kCurvedIn>(a, mips, tiles_x, tiles_y, s, done); break;
+            default: st = launch_tiles<GEO_MODE_ADAPTIVE, geo::kFlat>(a, mips, tiles_x, tiles_y, s, done);
         }
     } else {
         switch (geo::geodesic_kind(a.k)) {
-            case geo::kCurvedOut: st = launch_tiles<GEO_MODE_DIRECT, geo::kCurvedOut>(a, tiles_x, tiles_y, s, done); break;
-            case geo::kCurvedIn: st = launch_tiles<GEO_MODE_DIRECT, geo::kCurvedIn>(a, tiles_x, tiles_y, s, done); break;
-            default: st = launch_tiles<GEO_MODE_DIRECT, geo::kFlat>(a, tiles_x, tiles_y, s, done);
+            case geo::kCurvedOut: st = launch_tiles<GEO_MODE_DIRECT, geo::kCurvedOut>(a, mips, tiles_x, tiles_y, s, done); break;
+            case geo::kCurvedIn: st = launch_tiles<GEO_MODE_DIRECT, geo::kCurvedIn>(a, mips, tiles_x, tiles_y, s, done); break;
+            default: st = launch_tiles<GEO_MODE_DIRECT, geo::kFlat>(a, mips, tiles_x, tiles_y, s, done);
         }
     }
     if (st) return st;

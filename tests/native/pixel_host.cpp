@@ -103,3 +103,19 @@ extern "C" void host_math(const float* x, uint32_t n, float* out_sin, float* out
         out_asin[i] = geo::asinf_(x[i]);
     }
 }
+
+// GEO_FLAG_MIPS pieces of the header on the host: the mip chain (levels one
+// after another) and the level of detail, for comparisons with the oracle.
+extern "C" void host_mip_chain(const uint8_t* rgba8, uint32_t w, uint32_t h, uint32_t* out) {
+    std::memcpy(out, rgba8, (size_t)w * h * 4);
+    uint32_t* src = out;
+    for (int l = 1; l < geo::kSkyMipLevels; ++l) {
+        uint32_t* dst = src + (size_t)geo::mip_dim(w, l - 1) * geo::mip_dim(h, l - 1);
+        geo::mip_down(src, geo::mip_dim(w, l - 1), geo::mip_dim(h, l - 1), dst);
+        src = dst;
+    }
+}
+
+extern "C" void host_lod_q8(const float* rho2, uint32_t n, uint32_t* out) {
+    for (uint32_t i = 0; i < n; ++i) out[i] = geo::lod_q8(rho2[i]);
+}

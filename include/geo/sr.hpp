@@ -288,16 +288,21 @@ class BasicSphereBuffer : public SchwarzschildSphereShaderDraw {
 
     // BasicSphereBuffer::new (:21-60): the sphere's texture (group 2) and its
     // ray tracer; mode GEO_MODE_DIRECT integrates every pixel's own geodesic,
-    // GEO_MODE_FAN lerps the reference's 400-node fan (shader.wgsl:77-84)
+    // GEO_MODE_FAN lerps the reference's 400-node fan (shader.wgsl:77-84).
+    // mipmaps: sample the texture's 4-level mip chain trilinearly as the
+    // reference's textureSample does (Texture::new_with_mipmaps(..., 4),
+    // GEO_FLAG_MIPS); off, the level-0 bilinear sample the benchmark measures.
     BasicSphereBuffer(int device, double sphere_radius, double schwarz_radius, const Image& texture_image,
-                      uint32_t mode = GEO_MODE_DIRECT, uint32_t max_iter = MAX_ITER, double step = STEP)
+                      uint32_t mode = GEO_MODE_DIRECT, uint32_t max_iter = MAX_ITER, double step = STEP,
+                      bool mipmaps = false)
         : ctx_(std::make_shared<Context>(device)),
           ray_tracer_(sphere_radius, schwarz_radius, max_iter, step, NR_NODES_HALF, ctx_),
           sphere_radius_(sphere_radius),
           schwarz_radius_(schwarz_radius),
           max_iter_(max_iter),
           step_(step),
-          mode_(mode) {
+          mode_(mode),
+          mipmaps_(mipmaps) {
         check(geo_set_sky(ctx_->get(), texture_image.rgba.data(), texture_image.width, texture_image.height),
               "geo_set_sky");
     }
@@ -321,7 +326,7 @@ class BasicSphereBuffer : public SchwarzschildSphereShaderDraw {
         s.step = (float)step_;
         s.max_steps = max_iter_;
         s.mode = mode_;
-        s.flags = pass.cleared ? 0u : GEO_FLAG_COMPOSITE;
+        s.flags = (pass.cleared ? 0u : GEO_FLAG_COMPOSITE) | (mipmaps_ ? GEO_FLAG_MIPS : 0u);
         s.tol = 0.0f;
         check(geo_render_rows(ctx_->get(), &pass.uniform, &s, pass.width, pass.height, 0, pass.height, pass.target,
                               nullptr, nullptr, nullptr, nullptr, pass.stream),
@@ -337,6 +342,7 @@ class BasicSphereBuffer : public SchwarzschildSphereShaderDraw {
     uint32_t max_iter_;
     double step_;
     uint32_t mode_;
+    bool mipmaps_;
     double radial_position_ = 0.0;
 };
 

@@ -302,9 +302,14 @@ class BasicSphereBuffer:
     STEP = math.pi / 100.0
 
     def __init__(self, ctx: Context | int, sphere_radius: float, schwarz_radius: float, texture_rgba: np.ndarray,
-                 max_iter: int = MAX_ITER, step: float = STEP, mode: int = _lib.GEO_MODE_DIRECT):
+                 max_iter: int = MAX_ITER, step: float = STEP, mode: int = _lib.GEO_MODE_DIRECT,
+                 mipmaps: bool = False):
+        """mipmaps: sample the texture's 4-level mip chain trilinearly, as the
+        reference's textureSample does (Texture::new_with_mipmaps(..., 4),
+        GEO_FLAG_MIPS); off, the level-0 bilinear sample the benchmark measures."""
         ctx = Context(ctx) if isinstance(ctx, int) else ctx
         self.ctx = ctx
+        self.mipmaps = mipmaps
         self.sphere_radius = sphere_radius
         self.schwarz_radius = schwarz_radius
         self.max_iter = max_iter
@@ -328,7 +333,7 @@ class BasicSphereBuffer:
         if self.radial_position is None:
             raise RuntimeError("update_ray_fan must be called before draw")
         return make_scene(self.schwarz_radius, self.sphere_radius, self.radial_position, self.step, self.max_iter,
-                          self.mode)
+                          self.mode, flags=_lib.GEO_FLAG_MIPS if self.mipmaps else 0)
 
     def draw(self, frame: GeoFrame, target: RenderTarget, row0: int = 0, nrows: int | None = None,
              stream=None, composite: bool = False) -> None:

@@ -160,3 +160,20 @@ def test_mips_row_blocks_and_bands_compose(geo, torch_mod):
 
     with pytest.raises(GeoError):
         render(geo, torch_mod, ctx, frame, scene, w, h, 1, 10)
+
+
+def test_basic_sphere_buffer_mipmaps(geo, torch_mod):
+    """BasicSphereBuffer(..., mipmaps=True) draws the GEO_FLAG_MIPS frame (the
+    reference's sampler) through the host mirror."""
+    sky = sky_of("equirect", (512, 256))
+    w, h = 128, 72
+    frame = default_frame(w, h)
+    r = float(np.sqrt(2.5 ** 2 + 0.1 ** 2))
+    sphere = geo.BasicSphereBuffer(0, 50.0, 1.0, sky, mipmaps=True)
+    sphere.update_ray_fan(r)
+    rgba = torch_mod.empty(h * w * 4, dtype=torch_mod.uint8, device=torch_mod.device("cuda:0"))
+    sphere.draw(frame, geo.RenderTarget(w, h, rgba))
+    torch_mod.cuda.synchronize()
+    ref = O.render_mips_f32(frame, sphere.scene(), sky, w, h, threads=8)
+    assert np.array_equal(rgba.cpu().numpy().reshape(h, w, 4), ref["rgba"])
+    assert sphere.scene().max_steps == 1000 and sphere.scene().flags == geo._lib.GEO_FLAG_MIPS

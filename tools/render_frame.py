@@ -33,6 +33,7 @@ def main():
     p.add_argument("--frames", type=int, default=1, help="frames of motion before the saved one (dt = 1/60 s)")
     p.add_argument("--orbit", type=float, default=0.0, help="start an orbit with this rotation (observer.rs:162)")
     p.add_argument("--no-disk", action="store_true")
+    p.add_argument("--mipmaps", action="store_true", help="trilinear mip-mapped textures, as the reference samples them")
     args = p.parse_args()
 
     import torch
@@ -47,11 +48,11 @@ def main():
     if args.orbit:
         obs.start_orbit(args.orbit)
     sky = imageio.load_texture(args.sky) if args.sky else make_sky("equirect", (4096, 2048))
-    spheres = [g.BasicSphereBuffer(0, 50.0, 1.0, sky)]
+    spheres = [g.BasicSphereBuffer(0, 50.0, 1.0, sky, mipmaps=args.mipmaps)]
     if args.planet:
-        spheres.append(g.BasicSphereBuffer(0, 1.1, 1.0, imageio.load_texture(args.planet)))
+        spheres.append(g.BasicSphereBuffer(0, 1.1, 1.0, imageio.load_texture(args.planet), mipmaps=args.mipmaps))
     if args.clouds:
-        spheres.append(g.BasicSphereBuffer(0, 1.2, 1.0, imageio.load_texture(args.clouds)))
+        spheres.append(g.BasicSphereBuffer(0, 1.2, 1.0, imageio.load_texture(args.clouds), mipmaps=args.mipmaps))
     disk = None if args.no_disk else g.PointCloud.new_accretion_disk(spheres[0].ctx, 1.0, obs.get_position(), True)
     tgt = g.RenderTarget(w, h, torch.empty(w * h * 4, dtype=torch.uint8, device="cuda:0"))
     renderer = g.Renderer(obs)

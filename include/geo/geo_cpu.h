@@ -10,6 +10,8 @@
  * a separate library: libgeo.so and the Python package never load it, so the
  * product has no CPU fallback (geo_ctx_create fails without a HIP device).
  * Output equals geo_render_rows' bit for bit (tests/test_cpu_baseline.py).
+ * It samples the sky's level 0 (the measured path): GEO_FLAG_MIPS is refused
+ * with GEO_EINVAL.
  */
 #ifndef GEO_GEO_CPU_H
 #define GEO_GEO_CPU_H

@@ -7,7 +7,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 LIB=schwarzschild_raytracer_wgpu_amd/libgeo.so
 cp "$LIB" gpurun_out/.libgeo_orig.so
-for rep in 1 2; do
+for rep in $(seq 1 ${REPS:-2}); do
   for v in "$@"; do
     cp "$v" "$LIB"
     timeout -k 10 300 python ${BENCH:-bench.py} ${BENCH_ARGS:---no-cpu-baseline --steps 400} > gpurun_out/ab.json 2> gpurun_out/ab.err

@@ -78,6 +78,9 @@ def parse():
                    help="CPU baseline sample: every k-th row (default 1 up to 4K, 4 above)")
     p.add_argument("--mode", default=None, choices=["direct", "fan", "adaptive"],
                    help="default: the config's mode (cfg1-4 direct, cfg5_8k_adaptive adaptive)")
+    p.add_argument("--mips", action="store_true",
+                   help="sample the sky through its mip chain (GEO_FLAG_MIPS, the reference's textureSample); "
+                        "the metric's line is the level-0 path")
     p.add_argument("--no-frame-check", action="store_true",
                    help="skip rank 0's check, after the timed region, that every frame of the timed run's last "
                         "batch (the frames as assembled for present) equals a single-launch render of the frame; "
@@ -124,7 +127,9 @@ def main():
     args.mode = args.mode or cfg.mode
     mode = {"direct": g.GEO_MODE_DIRECT, "fan": g.GEO_MODE_FAN, "adaptive": g.GEO_MODE_ADAPTIVE}[args.mode]
     tol = cfg.tol if mode == g.GEO_MODE_ADAPTIVE else 0.0
-    scene = g.make_scene(cfg.rs, cfg.sphere_r, obs.get_radial_position(), cfg.step, cfg.max_steps, mode, tol=tol)
+    sampler_flags = g._lib.GEO_FLAG_MIPS if args.mips else 0
+    scene = g.make_scene(cfg.rs, cfg.sphere_r, obs.get_radial_position(), cfg.step, cfg.max_steps, mode,
+                         flags=sampler_flags, tol=tol)
     sky = make_sky(cfg.sky, cfg.sky_size)
     ctx = g.Context(local)
     ctx.set_sky(sky)
@@ -211,7 +216,7 @@ def main():
     from schwarzschild_raytracer_wgpu_amd.timing import HipEvent
 
     scene_defer = g.make_scene(cfg.rs, cfg.sphere_r, obs.get_radial_position(), cfg.step, cfg.max_steps, mode,
-                               flags=g._lib.GEO_FLAG_DEFER_STEPS, tol=tol)
+                               flags=g._lib.GEO_FLAG_DEFER_STEPS | sampler_flags, tol=tol)
     # per-launch kernel time: event pairs inside the timed region with one
     # render stream; with two (N > 1) launches overlap by design, so the
     # launch duration is measured on isolated launches after the timed region
@@ -357,7 +362,7 @@ def main():
     # wall time (no events; includes launch gaps)
     achieved_tflops = flops_per_launch / (kernel_ms_avg * 1e-3) / 1e12
     wall_tflops = flops_per_launch / (compute_max / args.steps) / 1e12
-    pmc_file, pmc = pmc_profile(args.config, args.mode, world)
+    pmc_file, pmc = pmc_profile(args.config, args.mode, world) if not args.mips else (None, {})
     if mode == g.GEO_MODE_ADAPTIVE:
         metric = (f"geodesic-step-attempts·pixels/sec at {W}x{H}, adaptive RK5(4) tol {cfg.tol:g} "
                   f"(whole job; /GPU = value/n_gpus)")
@@ -384,7 +389,7 @@ def main():
         "config": {
             "workload": f"{cfg.name}: {W}x{H}, rs={cfg.rs}, sphere_r={cfg.sphere_r}, observer {cfg.position} "
                         f"FrozenFall E={cfg.energy}, camera {tuple(round(c, 4) for c in cfg.camera)}, fov pi/2, "
-                        f"{stepping}, mode {args.mode}",
+                        f"{stepping}, mode {args.mode}, sky {'mip-mapped trilinear' if args.mips else 'level-0 bilinear'}",
             "width": W, "height": H, "max_steps": cfg.max_steps,
             "parallelism": f"rowbands{world}" if world > 1 else "single",
             "band_rows": args.band_rows,
@@ -434,7 +439,7 @@ def main():
             "pmc_profile": pmc_file,
         },
     }
-    if world == 1 and not args.no_cpu_baseline and mode != g.GEO_MODE_FAN:
+    if world == 1 and not args.no_cpu_baseline and mode != g.GEO_MODE_FAN and not args.mips:
         out["cpu_baseline"] = cpu_baseline(frame, scene, sky, W, H, args)
         out["reference_equivalent"] = reference_fan_cost(ctx, cfg, obs.get_radial_position())
     out["frame_check"] = frame_check

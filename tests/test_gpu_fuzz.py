@@ -93,3 +93,33 @@ def test_gpu_fuzz_fan_mode_bitexact(geo, torch_mod):  # noqa: F811
             bad.append(desc)
     print(f"fuzz fan: {n} scenes at {W}x{H}, {len(bad)} differ")
     assert not bad, f"{len(bad)} of {n} scenes differ: {bad[:5]}"
+
+
+def test_gpu_fuzz_mips_bitexact(geo, torch_mod):  # noqa: F811
+    """GEO_FLAG_MIPS on the fuzz scenes (ragged 65 x 37 frames: helper lanes
+    on the right and bottom quads) with random sky sizes down to 1 x 1: the
+    oracle's mip restatement, bit for bit."""
+    from schwarzschild_raytracer_wgpu_amd import _lib
+
+    w, h = W + 1, H + 1
+    n = int(os.environ.get("GEO_FUZZ_N", 200))
+    base = int(os.environ.get("GEO_FUZZ_BASE", 20_000))
+    bad = []
+    ctx = geo.Context(0)
+    for seed in range(base, base + n):
+        rng = np.random.default_rng(seed)
+        sw, sh = int(rng.integers(1, 300)), int(rng.integers(1, 160))
+        sky = rng.integers(0, 256, size=(sh, sw, 4), dtype=np.uint8)
+        if seed % 2:
+            sky[..., 3] = 255
+        ctx.set_sky(sky)
+        frame, scene, desc = random_scene(seed, w, h, adaptive=seed % 3 == 0)
+        scene.flags |= _lib.GEO_FLAG_MIPS
+        hip = render(geo, torch_mod, ctx, frame, scene, w, h)
+        ref = O.render_mips_f32(frame, scene, sky, w, h, threads=4)
+        same = all(np.array_equal(hip[f], ref[f]) for f in ("mask", "steps", "rgba")) and np.array_equal(
+            hip["uv"].view(np.uint32), ref["uv"].view(np.uint32)) and hip["total"] == ref["steps_total"]
+        if not same:
+            bad.append((desc, (sw, sh)))
+    print(f"fuzz mips: {n} scenes at {w}x{h}, {len(bad)} differ")
+    assert not bad, f"{len(bad)} of {n} scenes differ: {bad[:5]}"

@@ -177,3 +177,25 @@ def test_basic_sphere_buffer_mipmaps(geo, torch_mod):
     ref = O.render_mips_f32(frame, sphere.scene(), sky, w, h, threads=8)
     assert np.array_equal(rgba.cpu().numpy().reshape(h, w, 4), ref["rgba"])
     assert sphere.scene().max_steps == 1000 and sphere.scene().flags == geo._lib.GEO_FLAG_MIPS
+
+
+def test_mips_4k_config_rows(geo, torch_mod):
+    """Config 3's 4K frame with the mip-mapped sampler (its 4096 x 2048 sky):
+    row blocks across the frame equal the oracle's mip restatement."""
+    from schwarzschild_raytracer_wgpu_amd.scenes import CONFIGS, make_sky
+
+    cfg = CONFIGS["cfg3_4k"]
+    w, h = cfg.width, cfg.height
+    obs = geo.Observer(cfg.rs, cfg.fov, w, h)
+    obs.set_position(*cfg.position)
+    obs.set_camera(*cfg.camera)
+    frame = obs.calc_transformation_pipeline()
+    scene = mips(geo.make_scene(cfg.rs, cfg.sphere_r, obs.get_radial_position(), cfg.step, cfg.max_steps), geo)
+    sky = make_sky(cfg.sky, cfg.sky_size)
+    ctx = geo.Context(0)
+    ctx.set_sky(sky)
+    full = render(geo, torch_mod, ctx, frame, scene, w, h)
+    for r0 in (0, 540, 1080, 1618, 2150):
+        ref = O.render_mips_f32(frame, scene, sky, w, h, row0=r0, nrows=10, threads=16)
+        for f in ("rgba", "mask", "steps"):
+            assert np.array_equal(full[f][r0:r0 + 10], ref[f]), (f, r0)

@@ -14,7 +14,7 @@
  *   geo_observer_*             Observer::{new, calc_transformation_pipeline,
  *                              update_screen_format, move_camera, start_*}
  *                                                                SR/simulation/observer.rs:68-296
- *   geo_set_sky                Texture::new_with_mipmaps (group 2, LOD 0)
+ *   geo_set_sky                Texture::new_with_mipmaps (group 2, 4 levels)
  *                                                                SR/schwarzschild_sphere_shader/sphere_buffer/basic_sphere_buffer.rs:29-36
  *   geo_solve_ray_fan          SphereRayTracer::solve_ray_fan + BasicSphereBuffer::update_ray_fan
  *                                                                SR/simulation/sphere_ray_tracer.rs:35-56,
@@ -132,16 +132,21 @@ int geo_ctx_create(int device, geo_ctx** out);
 void geo_ctx_destroy(geo_ctx* ctx);
 
 /* Uploads an equirect RGBA8 sky (row-major, w*h*4 bytes, host memory; the
- * bytes are copied, synchronously, after every render in flight on the
- * context's device has finished, so no frame samples a half-written sky).
- * On failure the context has no sky (renders return GEO_ESTATE).  U wraps, V clamps, LOD-0 bilinear with
- * 8-bit sub-texel weights.  The device keeps a copy padded by one texel on
- * every side, which must stay below 2^31 bytes: (w + 2) * (h + 2) * 4 < 2^31,
+ * bytes are copied, synchronously, after this context's renders in flight on
+ * any stream have finished, so no frame samples a half-written sky; other
+ * contexts' work and collectives are not waited for).  On failure the
+ * context has no sky (renders return GEO_ESTATE).  U wraps, V clamps,
+ * bilinear with 8-bit sub-texel weights: level 0, or with GEO_FLAG_MIPS the
+ * 4-level mip chain built here (box filter; Texture::new_with_mipmaps(..., 4),
+ * basic_sphere_buffer.rs:31-36).  The device keeps every level padded by one
+ * texel on every side, which must stay below 2^31 bytes in all:
+ * sum over l < 4 of (max(1, w >> l) + 2) * (max(1, h >> l) + 2) * 4 < 2^31,
  * w, h <= 2^20 (GEO_EINVAL otherwise). */
 int geo_set_sky(geo_ctx* ctx, const uint8_t* rgba8, uint32_t w, uint32_t h);
 
 /* Uploads a ray fan of n >= 2 nodes (host memory, copied synchronously after
- * the device's work in flight; geo_solve_ray_fan replaces it stream-ordered):
+ * the last solve and draws of the buffer it goes to; geo_solve_ray_fan
+ * replaces it stream-ordered):
  * node i is PI/2 - traveled angle of the ray at theta_i = PI/2 - PI*i/(n-1). */
 int geo_set_fan(geo_ctx* ctx, const float* fan, uint32_t n);
 

@@ -418,11 +418,22 @@ struct StopTest {
         else
             return (*this)(NU, NUB);
     }
-    // exact() as a wave mask, each compare balloted on its own (hipcc
-    // rebuilds a compound condition through a VGPR before its ballot)
-    GEO_HDM uint64_t exact_mask(float NU, float NUB) const {
+    // exact() as a wave mask in two parts, for the adaptive loop: out_mask,
+    // a superset (kCurvedOut: NU outside [lo, hi] or NaN, one v_med3_f32 and
+    // a compare per attempt), then exact_refine, taken only when out_mask
+    // has lanes: out & exact_refine == exact, because a state outside the
+    // interval stops iff it is below lo (or NaN) or its U' exceeds vmin.
+    // hipcc rebuilds a compound condition through a VGPR before its ballot,
+    // so the compares are balloted one by one.
+    GEO_HDM uint64_t out_mask(float NU) const {
         if constexpr (KIND == kCurvedOut)
-            return ballot_(!(NU >= lo)) | (ballot_(NU > hi) & ballot_(NUB > vmin));
+            return ballot_(med3_(NU, lo, hi) != NU);
+        else
+            return ~0ull;
+    }
+    GEO_HDM uint64_t exact_refine(float NU, float NUB) const {
+        if constexpr (KIND == kCurvedOut)
+            return ballot_(!(NU >= lo)) | ballot_(NUB > vmin);
         else
             return ballot_((*this)(NU, NUB));
     }
@@ -873,7 +884,8 @@ GEO_HD float geodesic_angle_adaptive(const PixelConsts& k, float st, float ct, f
         dp5_step<KIND>(U, V, h, hh, &NU, &NV, &SE);
         const float err = __builtin_fabsf(SE) * hh;
         const bool acc = !(err > k.tolU);
-        const uint64_t hit = ballot_(acc) & stop_at.exact_mask(NU, NV) & live;
+        uint64_t hit = ballot_(acc) & stop_at.out_mask(NU) & live;
+        if (hit != 0) hit &= stop_at.exact_refine(NU, NV);
         if (hit != 0) {
             if (in_ballot_(hit)) {
                 GEO_RARE();

@@ -439,7 +439,7 @@ def main():
             "pmc_profile": pmc_file,
         },
     }
-    if world == 1 and not args.no_cpu_baseline and mode != g.GEO_MODE_FAN and not args.mips:
+    if world == 1 and not args.no_cpu_baseline and mode != g.GEO_MODE_FAN:
         out["cpu_baseline"] = cpu_baseline(frame, scene, sky, W, H, args)
         out["reference_equivalent"] = reference_fan_cost(ctx, cfg, obs.get_radial_position())
     out["frame_check"] = frame_check
@@ -624,8 +624,9 @@ def cpu_baseline(frame, scene, sky, W, H, args):
         "cores": threads,
         "kind": "port",
         "cpu_model": cpu_model(),
-        "sample": f"{what} {W}x{H} frame ({nrows * W} pixels, {steps} steps): median of 3 runs after one warm-up, "
-                  f"{threads} threads",
+        "sample": f"{what} {W}x{H} frame ({nrows * W} pixels, {steps} steps"
+                  f"{', mip-mapped: quad partner rows traced too' if args.mips and k > 1 else ''}): "
+                  f"median of 3 runs after one warm-up, {threads} threads",
         "seconds_per_run": times,
         "implementation": "geo_render_cpu (libgeo_cpu.so): geo_pixel.h compiled for the host, g++ -O2 "
                           "-ffp-contract=off -mfma -msse4.1, scalar, std::thread row blocks; output bit-identical "

@@ -10,8 +10,10 @@
  * a separate library: libgeo.so and the Python package never load it, so the
  * product has no CPU fallback (geo_ctx_create fails without a HIP device).
  * Output equals geo_render_rows' bit for bit (tests/test_cpu_baseline.py).
- * It samples the sky's level 0 (the measured path): GEO_FLAG_MIPS is refused
- * with GEO_EINVAL.
+ * GEO_FLAG_MIPS builds the same 4-level chain as geo_set_sky and takes each
+ * pixel's level of detail from its frame-aligned 2 x 2 quad, tracing the
+ * quad partners outside the frame or the requested rows as the kernel's
+ * helper lanes do; any row0 and row_step are accepted.
  */
 #ifndef GEO_GEO_CPU_H
 #define GEO_GEO_CPU_H

@@ -31,6 +31,10 @@ struct CpuJob {
     uint8_t* mask;
     float* uv;
     uint32_t* steps;
+    // GEO_FLAG_MIPS: the chain's levels (geo::mip_down of level 0)
+    bool mips;
+    const uint32_t* lvl[geo::kSkyMipLevels];
+    uint32_t lw[geo::kSkyMipLevels], lh[geo::kSkyMipLevels];
 };
 
 float geodesic(const CpuJob& j, float st, float ct, float rct, uint32_t* n) {
@@ -50,9 +54,94 @@ float geodesic(const CpuJob& j, float st, float ct, float rct, uint32_t* n) {
     }
 }
 
+// One traced pixel of a GEO_FLAG_MIPS frame: lambda', its UV (every pixel's,
+// as the kernel's lanes compute it for their quad partners) and its steps.
+struct Traced {
+    float lam, U, V;
+    uint32_t n;
+};
+
+Traced trace(const CpuJob& j, uint32_t px, uint32_t py) {
+    float c2x, c2y, c2z;
+    geo::pixel_central_dir(j.cam, j.f->movement_to_central, j.f->psi_factor_and_position[0], j.kt, px, py, &c2x, &c2y,
+                           &c2z);
+    const float st = geo::central_sin(c2z);
+    const float ct = geo::central_rho(c2x, c2y);
+    const float rct = geo::rcpf_(ct);
+    Traced t;
+    t.n = 0;
+    t.lam = geodesic(j, st, ct, rct, &t.n);
+    geo::sky_uv(j.f->central_to_uv, c2x, c2y, ct, rct, t.lam, &t.U, &t.V);
+    return t;
+}
+
+// The kernel's sample_trilinear (geo_render.hip) on the host chain: levels
+// floor(lambda) and the next, blended with frac(lambda) in 8 bits.
+uint32_t sample_trilinear(const CpuJob& j, float rho2, float U, float V) {
+    const uint32_t q = geo::lod_q8(rho2);
+    const uint32_t l0 = q >> 8, f = q & 255u;
+    const uint32_t l1 = l0 + 1u < (uint32_t)geo::kSkyMipLevels ? l0 + 1u : l0;
+    auto fetch0 = [p = j.lvl[l0]](uint32_t i) { return p[i]; };
+    auto fetch1 = [p = j.lvl[l1]](uint32_t i) { return p[i]; };
+    const uint32_t s0 = geo::sample_sky_raw(fetch0, j.lw[l0], j.lh[l0], U, V);
+    const uint32_t s1 = geo::sample_sky_raw(fetch1, j.lw[l1], j.lh[l1], U, V);
+    return geo::mip_blend(s0, s1, f);
+}
+
+// GEO_FLAG_MIPS rows: each pixel's level of detail comes from its
+// frame-aligned 2 x 2 quad (partners x ^ 1 and y ^ 1, traced even where they
+// lie outside the frame or the requested rows, like the kernel's helper
+// lanes); rows tid, tid + nthreads, ... as run_rows.
+unsigned long long run_rows_mips(const CpuJob& j, unsigned tid, unsigned nthreads) {
+    unsigned long long total = 0;
+    const bool composite = (j.s->flags & GEO_FLAG_COMPOSITE) != 0;
+    const uint32_t gw = j.width + (j.width & 1u);
+    std::vector<Traced> rows[2] = {std::vector<Traced>(gw), std::vector<Traced>(gw)};
+    int64_t have[2] = {-1, -1};  // the frame row each buffer holds
+    auto row_of = [&](uint32_t py) -> const std::vector<Traced>& {
+        for (int b = 0; b < 2; ++b)
+            if (have[b] == (int64_t)py) return rows[b];
+        const int b = have[0] == (int64_t)(py ^ 1u) ? 1 : 0;  // keep the partner row
+        for (uint32_t x = 0; x < gw; ++x) rows[b][x] = trace(j, x, py);
+        have[b] = py;
+        return rows[b];
+    };
+    for (uint32_t ly = tid; ly < j.nrows; ly += nthreads) {
+        const uint32_t py = j.row0 + ly * j.row_step;
+        (void)row_of(py);
+        const std::vector<Traced>& ry = row_of(py ^ 1u);  // never evicts row py
+        const std::vector<Traced>& rr = have[0] == (int64_t)py ? rows[0] : rows[1];
+        for (uint32_t px = 0; px < j.width; ++px) {
+            const Traced& t = rr[px];
+            const Traced& tx = rr[px ^ 1u];
+            const Traced& ty = ry[px];
+            const float rho2 = geo::mip_rho2(t.U - tx.U, t.V - tx.V, t.U - ty.U, t.V - ty.V, (float)j.sw, (float)j.sh);
+            const bool bh = t.lam < geo::kBlackHoleLambda;
+            const size_t o = (size_t)ly * j.width + px;
+            if (composite) {
+                if (!bh) {
+                    const uint32_t sm = sample_trilinear(j, rho2, t.U, t.V);
+                    j.rgba[o] = j.opaque ? sm : geo::composite_(sm, j.rgba[o]);
+                }
+            } else {
+                j.rgba[o] = bh ? geo::kBlackRGBA : geo::over_clear(sample_trilinear(j, rho2, t.U, t.V), j.opaque);
+            }
+            if (j.mask) j.mask[o] = bh ? 1 : 0;
+            if (j.uv) {
+                j.uv[2 * o] = t.U;
+                j.uv[2 * o + 1] = t.V;
+            }
+            if (j.steps) j.steps[o] = t.n;
+            total += t.n;
+        }
+    }
+    return total;
+}
+
 // rows tid, tid + nthreads, ... of the job (interleaved: the frame's cost is
 // centre-heavy); returns the thread's executed RK4 steps
 unsigned long long run_rows(const CpuJob& j, unsigned tid, unsigned nthreads) {
+    if (j.mips) return run_rows_mips(j, tid, nthreads);
     unsigned long long total = 0;
     const float psi_k = j.f->psi_factor_and_position[0];
     const bool composite = (j.s->flags & GEO_FLAG_COMPOSITE) != 0;
@@ -108,7 +197,7 @@ extern "C" int geo_render_cpu(const geo_frame* frame, const geo_scene* scene, co
     if ((uint64_t)row0 + (uint64_t)(nrows - 1) * row_step >= height) return GEO_EINVAL;
     if (scene->mode != GEO_MODE_DIRECT && scene->mode != GEO_MODE_FAN && scene->mode != GEO_MODE_ADAPTIVE)
         return GEO_EINVAL;
-    if ((scene->flags & ~(GEO_FLAG_DEFER_STEPS | GEO_FLAG_COMPOSITE)) != 0) return GEO_EINVAL;
+    if ((scene->flags & ~(GEO_FLAG_DEFER_STEPS | GEO_FLAG_COMPOSITE | GEO_FLAG_MIPS)) != 0) return GEO_EINVAL;
     if (scene->mode == GEO_MODE_FAN && (!fan || n_fan < 2)) return GEO_EINVAL;
     if (scene->mode != GEO_MODE_FAN &&
         (!(scene->step > 0.0f) || !(scene->r_obs > 0.0f) || !(scene->sphere_r > 0.0f) || !(scene->rs >= 0.0f)))
@@ -140,6 +229,22 @@ extern "C" int geo_render_cpu(const geo_frame* frame, const geo_scene* scene, co
     j.mask = out_mask;
     j.uv = out_uv;
     j.steps = out_steps;
+    // GEO_FLAG_MIPS: the chain geo_set_sky builds (geo::mip_down, level by level)
+    j.mips = (scene->flags & GEO_FLAG_MIPS) != 0;
+    std::vector<uint32_t> chain[geo::kSkyMipLevels];
+    for (int l = 0; l < geo::kSkyMipLevels; ++l) {
+        j.lw[l] = geo::mip_dim(sky_w, l);
+        j.lh[l] = geo::mip_dim(sky_h, l);
+        if (l == 0) {
+            j.lvl[0] = sky.data();
+        } else if (j.mips) {
+            chain[l].resize((size_t)j.lw[l] * j.lh[l]);
+            geo::mip_down(j.lvl[l - 1], j.lw[l - 1], j.lh[l - 1], chain[l].data());
+            j.lvl[l] = chain[l].data();
+        } else {
+            j.lvl[l] = nullptr;
+        }
+    }
     unsigned n = threads > 0 ? (unsigned)threads : std::thread::hardware_concurrency();
     if (n == 0) n = 1;
     if (n > nrows) n = nrows;

@@ -146,15 +146,25 @@ __device__ __forceinline__ T level_sel(const T (&v)[geo::kSkyMipLevels], uint32_
 }
 
 // The trilinear sample (GEO_FLAG_MIPS, geo_pixel.h): levels floor(lambda) and
-// the next, blended with frac(lambda) in 8 bits.
+// the next, blended with frac(lambda) in 8 bits.  A zero weight returns
+// level floor(lambda) alone: mip_blend(s0, s1, 0) == s0 bit for bit (each
+// channel (256 s0 + 128) >> 8), so the second level is fetched only under the
+// lanes that blend.  A wave magnified everywhere (rho2 <= 1, so lambda = 0,
+// on every active lane: most of a 4K frame of a 4096 x 2048 sky) skips the
+// level of detail and samples level 0 with its base and pitch as scalars, as
+// the level-0 path does.
 __device__ __forceinline__ uint32_t sample_trilinear(const RenderArgs& a, float rho2, float U, float V) {
     const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(a.sky), 0,
                                                                            (int)a.sky_total_bytes, kBufferRsrcWord3);
+    if (geo::ballot_(rho2 > 1.0f) == 0)  // lod_q8 is 0 unless rho2 > 1
+        return geo::sample_sky_quad_f(LevelQuad{rsrc, a.mip_off[0], a.mip_pitch[0]}, a.mip_w256[0], a.mip_h256[0], U,
+                                      V);
     const uint32_t q = geo::lod_q8(rho2);
     const uint32_t l0 = q >> 8, f = q & 255u;
-    const uint32_t l1 = l0 + 1u < (uint32_t)geo::kSkyMipLevels ? l0 + 1u : l0;
     const uint32_t s0 = geo::sample_sky_quad_f(LevelQuad{rsrc, level_sel(a.mip_off, l0), level_sel(a.mip_pitch, l0)},
                                                level_sel(a.mip_w256, l0), level_sel(a.mip_h256, l0), U, V);
+    if (f == 0u) return s0;
+    const uint32_t l1 = l0 + 1u < (uint32_t)geo::kSkyMipLevels ? l0 + 1u : l0;
     const uint32_t s1 = geo::sample_sky_quad_f(LevelQuad{rsrc, level_sel(a.mip_off, l1), level_sel(a.mip_pitch, l1)},
                                                level_sel(a.mip_w256, l1), level_sel(a.mip_h256, l1), U, V);
     return geo::mip_blend(s0, s1, f);
@@ -268,10 +278,16 @@ __global__ __launch_bounds__(kBlock) void geo_render_kernel(const RenderArgs a) 
         const float ct = geo::central_rho(c2x, c2y);
         const float rct = geo::rcpf_(ct);
         const float lam = pixel_lambda<MODE, KIND>(a, st, ct, rct, &steps);
-        float U, V;
-        geo::sky_uv(a.frame.central_to_uv, c2x, c2y, ct, rct, lam, &U, &V);
-        const float ux = lane_xor1(U), vx = lane_xor1(V), uy = lane_xor16(U), vy = lane_xor16(V);
-        const float rho2 = geo::mip_rho2(U - ux, V - vx, U - uy, V - vy, a.sky_wf, a.sky_hf);
+        // A pixel's UV is read by its own sample and by its quad partners'
+        // footprints, all in this wave: a wave wholly inside the shadow reads
+        // none (unless the caller asks for UV) and skips the UV and the
+        // footprint (a wave-uniform branch)
+        float U = 0.0f, V = 0.0f, rho2 = 0.0f;
+        if (geo::ballot_(!(lam < geo::kBlackHoleLambda)) != 0 || a.out_uv) {
+            geo::sky_uv(a.frame.central_to_uv, c2x, c2y, ct, rct, lam, &U, &V);
+            const float ux = lane_xor1(U), vx = lane_xor1(V), uy = lane_xor16(U), vy = lane_xor16(V);
+            rho2 = geo::mip_rho2(U - ux, V - vx, U - uy, V - vy, a.sky_wf, a.sky_hf);
+        }
         if (in_frame)
             shade_pixel_mips(a, lam, U, V, rho2, steps, (size_t)ly * a.width + px);
         else

@@ -13,8 +13,8 @@ import pytest
 import oracle as O
 from helpers import default_frame, default_scene
 from schwarzschild_raytracer_wgpu_amd import make_scene
-from schwarzschild_raytracer_wgpu_amd._lib import (GEO_EINVAL, GEO_FLAG_COMPOSITE, GEO_MODE_ADAPTIVE, GEO_MODE_FAN,
-                                                   GEO_OK)
+from schwarzschild_raytracer_wgpu_amd._lib import (GEO_EINVAL, GEO_FLAG_COMPOSITE, GEO_FLAG_MIPS, GEO_MODE_ADAPTIVE,
+                                                   GEO_MODE_FAN, GEO_OK)
 from schwarzschild_raytracer_wgpu_amd.scenes import make_sky
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -111,3 +111,39 @@ def test_cpu_baseline_rejects(cpu):
     assert render_cpu(cpu, frame, fs, sky, w, h)[0] == GEO_EINVAL  # fan mode without a fan
     neg = default_scene(64, step=-0.1)
     assert render_cpu(cpu, frame, neg, sky, w, h)[0] == GEO_EINVAL
+
+
+def test_cpu_baseline_mips(cpu):
+    """GEO_FLAG_MIPS: the CPU library equals the oracle's trilinear mirror
+    (render_mips_f32) on ragged frames (quad partners past the right and
+    bottom edges), in direct, adaptive and fan mode and composited over a
+    target; sampled rows (any row0, any row_step) equal the same rows of the
+    full frame, their quad partners traced as helpers."""
+    sky = np.random.default_rng(11).integers(0, 256, size=(48, 96, 4), dtype=np.uint8)  # translucent texels
+    for (w, h) in ((66, 38), (65, 37)):
+        frame = default_frame(w, h)
+        scene = default_scene(2048)
+        scene.flags |= GEO_FLAG_MIPS
+        rc, a = render_cpu(cpu, frame, scene, sky, w, h, threads=3)
+        ref = O.render_mips_f32(frame, scene, sky, w, h, threads=4)
+        assert rc == GEO_OK and same(a, ref) and a["total"] == ref["steps_total"], (w, h)
+        for r0, n, rs in ((1, 12, 3), (4, 9, 4), (h - 1, 1, 1)):
+            rc, b = render_cpu(cpu, frame, scene, sky, w, h, row0=r0, nrows=n, row_step=rs, threads=2)
+            rows = [r0 + i * rs for i in range(n)]
+            sub = {f: a[f][rows] for f in ("rgba", "mask", "uv", "steps")}
+            assert rc == GEO_OK and same(b, sub), (w, h, r0, rs)
+    w, h = 66, 38
+    frame = default_frame(w, h, pos=(1.2, 0.5, 0.0), camera=(math.pi + 0.6, 0.3))
+    sa = make_scene(1.0, 50.0, 1.3, math.pi / 100, 2048, GEO_MODE_ADAPTIVE, flags=GEO_FLAG_MIPS)
+    rc, a = render_cpu(cpu, frame, sa, sky, w, h, threads=4)
+    assert rc == GEO_OK and same(a, O.render_mips_f32(frame, sa, sky, w, h, threads=4))
+    frame = default_frame(w, h)
+    r = math.sqrt(2.5 ** 2 + 0.1 ** 2)
+    fan = O.solve_ray_fan(50.0, 1.0, 1000, math.pi / 100, 400, r)
+    sf = make_scene(1.0, 50.0, r, math.pi / 100, 1000, GEO_MODE_FAN, flags=GEO_FLAG_MIPS)
+    rc, a = render_cpu(cpu, frame, sf, sky, w, h, fan=fan)
+    assert rc == GEO_OK and same(a, O.render_mips_f32(frame, sf, sky, w, h, fan=fan, threads=4))
+    tgt = np.random.default_rng(12).integers(0, 256, size=(h, w, 4), dtype=np.uint8)
+    sc = make_scene(1.0, 50.0, r, math.pi / 100, 2048, flags=GEO_FLAG_COMPOSITE | GEO_FLAG_MIPS)
+    rc, a = render_cpu(cpu, frame, sc, sky, w, h, target=tgt)
+    assert rc == GEO_OK and same(a, O.render_mips_f32(frame, sc, sky, w, h, threads=4, target=tgt))

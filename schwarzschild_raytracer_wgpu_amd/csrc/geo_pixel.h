@@ -1016,7 +1016,11 @@ GEO_HD int32_t floor_i32_(float x) {
 // one fma correction (exhaustively equal to a / pi over fan_lerp's domain,
 // tests/native/divpi_exhaustive.hip), the index by v_cvt_flr_i32_f32 and the
 // weight by v_fract_f32 (t - floor(t), exact for t >= 0).
-GEO_HD float fan_lerp(const float* fan, uint32_t n, float st) {
+struct FanPos {
+    uint32_t i, i1;  // nodes
+    float w;         // weight of node i1
+};
+GEO_HD FanPos fan_pos(uint32_t n, float st) {
     const float theta = asinf_(st);
     const float a = kPi2 - theta;
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -1037,8 +1041,10 @@ GEO_HD float fan_lerp(const float* fan, uint32_t n, float st) {
     const float w = t - fl;
 #endif
     const uint32_t i1 = (i + 1u < n) ? i + 1u : n - 1u;
-    return fan[i] * (1.0f - w) + fan[i1] * w;
+    return FanPos{i, i1, w};
 }
+GEO_HD float fan_at(const float* fan, const FanPos& p) { return fan[p.i] * (1.0f - p.w) + fan[p.i1] * p.w; }
+GEO_HD float fan_lerp(const float* fan, uint32_t n, float st) { return fan_at(fan, fan_pos(n, st)); }
 
 // sin theta of the central-frame direction, c2z clamped to [-1, 1] (to_polar's
 // asin argument, :75) by one v_med3_f32 (a NaN becomes -1, where a compare-

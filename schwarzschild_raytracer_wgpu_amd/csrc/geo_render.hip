@@ -239,22 +239,83 @@ __device__ __forceinline__ float pixel_lambda(const RenderArgs& a, float st, flo
     }
 }
 
+// Pixels per lane: a fan-mode lane (level-0 sampler) draws two, rows
+// kWaveRows apart, so one wave covers 16 x 8 pixels and each lane's loads of
+// the second pixel overlap the first's (the fan lerp and the texel quads are
+// the kernel's latency; its VALU work is short).
+__host__ __device__ constexpr uint32_t lane_rows(int mode, bool mips) {
+    return mode == GEO_MODE_FAN && !mips ? 2u : 1u;
+}
+
 template <int MODE, int KIND, bool MIPS>
 __global__ __launch_bounds__(kBlock) void geo_render_kernel(const RenderArgs a) {
+    constexpr uint32_t LR = lane_rows(MODE, MIPS);
     const uint2 tile = make_uint2(blockIdx.x, a.tile_y0 + blockIdx.y);
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x) >> 6;
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t px = tile.x * kTileW + (wave % kWavesX) * kWaveW + lane % kWaveW;
     // local row -> frame row.  band_rows is a multiple of 8 (checked on the
-    // host): each 8-row wave lies in one band and the mapping is wave-uniform
-    // (scalar ops; the band index by a multiply-high, band_rows_magic).
-    const uint32_t wl0 = tile.y * kTileH + (wave / kWavesX) * kWaveRows;
+    // host): each wave's rows (at most 8) lie in one band and the mapping is
+    // wave-uniform (scalar ops; the band index by a multiply-high,
+    // band_rows_magic).
+    const uint32_t wl0 = tile.y * (kTileH * LR) + (wave / kWavesX) * (kWaveRows * LR);
     const uint32_t ly = wl0 + lane / kWaveW;
     const uint32_t band = __umulhi(wl0, a.band_magic);
     const uint32_t py = a.row0 + band * a.band_stride + (wl0 - band * a.band_rows) + (ly - wl0);
     uint32_t steps = 0;
     const bool in_frame = px < a.width && ly < a.nrows && py < a.height;
-    if constexpr (!MIPS) {
+    if constexpr (LR == 2) {
+        // both pixels' rays, then both fan lerps (four loads in flight), then
+        // both epilogues
+        float c2x[2], c2y[2], st[2], ct[2], rct[2], lam[2];
+#pragma unroll
+        for (uint32_t k = 0; k < 2; ++k) {
+            float c2z;
+            geo::pixel_central_dir(a.cam, a.frame.movement_to_central, a.frame.psi_factor_and_position[0], a.kt, px,
+                                   py + k * kWaveRows, &c2x[k], &c2y[k], &c2z);
+            st[k] = geo::central_sin(c2z);
+            ct[k] = geo::central_rho(c2x[k], c2y[k]);
+            rct[k] = geo::rcpf_(ct[k]);
+        }
+        geo::FanPos fp[2];
+#pragma unroll
+        for (uint32_t k = 0; k < 2; ++k) fp[k] = geo::fan_pos(a.n_fan, st[k]);
+#pragma unroll
+        for (uint32_t k = 0; k < 2; ++k) lam[k] = geo::fan_at(a.fan, fp[k]);
+        bool in[2];
+#pragma unroll
+        for (uint32_t k = 0; k < 2; ++k)
+            in[k] = px < a.width && ly + k * kWaveRows < a.nrows && py + k * kWaveRows < a.height;
+        const bool bh0 = lam[0] < geo::kBlackHoleLambda, bh1 = lam[1] < geo::kBlackHoleLambda;
+        if (!a.composite && !a.out_uv && !a.out_mask && !a.out_steps) {
+            // the plain draw: both UVs, then both texel quads (eight loads in
+            // flight), then both stores; a wave with no sky pixel stores the
+            // clear colour only
+            uint32_t rgba[2] = {geo::kBlackRGBA, geo::kBlackRGBA};
+            if (geo::ballot_(!(bh0 && bh1)) != 0) {
+                float U[2], V[2];
+#pragma unroll
+                for (uint32_t k = 0; k < 2; ++k)
+                    geo::sky_uv(a.frame.central_to_uv, c2x[k], c2y[k], ct[k], rct[k], lam[k], &U[k], &V[k]);
+                const PaddedSkyQuad quad{__builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(a.sky), 0,
+                                                                           (int)a.sky_bytes, kBufferRsrcWord3),
+                                         a.sky_pitch_b};
+                uint32_t smp[2];
+#pragma unroll
+                for (uint32_t k = 0; k < 2; ++k) smp[k] = geo::sample_sky_quad_f(quad, a.sky_w256, a.sky_h256, U[k], V[k]);
+                rgba[0] = bh0 ? geo::kBlackRGBA : geo::over_clear(smp[0], a.sky_opaque != 0);
+                rgba[1] = bh1 ? geo::kBlackRGBA : geo::over_clear(smp[1], a.sky_opaque != 0);
+            }
+#pragma unroll
+            for (uint32_t k = 0; k < 2; ++k)
+                if (in[k]) a.out_rgba[(size_t)(ly + k * kWaveRows) * a.width + px] = rgba[k];
+        } else {
+#pragma unroll
+            for (uint32_t k = 0; k < 2; ++k)
+                if (in[k])
+                    shade_pixel(a, c2x[k], c2y[k], ct[k], rct[k], lam[k], 0u, (size_t)(ly + k * kWaveRows) * a.width + px);
+        }
+    } else if constexpr (!MIPS) {
         if (in_frame) {
             float c2x, c2y, c2z;
             geo::pixel_central_dir(a.cam, a.frame.movement_to_central, a.frame.psi_factor_and_position[0], a.kt, px,
@@ -949,7 +1010,8 @@ static int render_impl(geo_ctx* c, const geo_frame* frame, const geo_scene* scen
     const uint32_t tiles_x = (width + kTileW - 1) / kTileW;
     a.cam = geo::camera_consts(frame->display_to_movement, frame->movement_to_central, width, height);
     a.kt = geo::aberration_kt(frame->psi_factor_and_position[0]);
-    const uint32_t tiles_y = (nrows + kTileH - 1) / kTileH;
+    const uint32_t tile_h = kTileH * lane_rows(scene->mode, mips);
+    const uint32_t tiles_y = (nrows + tile_h - 1) / tile_h;
     a.sky = c->sky;
     a.sky_w = c->sky_w;
     a.sky_h = c->sky_h;

@@ -65,7 +65,8 @@ def test_gpu_fuzz_adversarial_bitexact(geo, torch_mod, adaptive):  # noqa: F811
 def test_gpu_fuzz_fan_mode_bitexact(geo, torch_mod):  # noqa: F811
     """Fan mode (the reference's display path) on the fuzz scenes: each
     scene's 400-node fan solved on the GPU, drawn with the fan lerp, and the
-    oracle's f32 lerp over the same fan: mask, UV bits and RGBA equal."""
+    oracle's f32 lerp over the same fan: mask, UV bits and RGBA equal, and the
+    colour-only draw (two pixels per lane) equal to the same RGBA."""
     from schwarzschild_raytracer_wgpu_amd import _lib
     from schwarzschild_raytracer_wgpu_amd.scenes import make_sky
 
@@ -85,9 +86,13 @@ def test_gpu_fuzz_fan_mode_bitexact(geo, torch_mod):  # noqa: F811
         uv = torch.empty(W * H * 2, dtype=torch.float32, device=dev)
         ctx.render_rows(frame, scene, W, H, 0, H, rgba, mask, uv)
         torch.cuda.synchronize()
+        plain = torch.empty(W * H * 4, dtype=torch.uint8, device=dev)
+        ctx.render_rows(frame, scene, W, H, 0, H, plain)
+        torch.cuda.synchronize()
         ref = O.render_f32(frame, scene, sky, W, H, fan=fan, threads=4)
         same = (np.array_equal(mask.cpu().numpy().reshape(H, W), ref["mask"])
                 and np.array_equal(rgba.cpu().numpy().reshape(H, W, 4), ref["rgba"])
+                and np.array_equal(plain.cpu().numpy().reshape(H, W, 4), ref["rgba"])
                 and np.array_equal(uv.cpu().numpy().reshape(H, W, 2).view(np.uint32), ref["uv"].view(np.uint32)))
         if not same:
             bad.append(desc)

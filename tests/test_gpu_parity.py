@@ -345,6 +345,49 @@ def test_fan_solved_on_side_stream_matches_one_stream(geo, torch_mod):
     assert np.mean(np.all(got == ref["rgba"], axis=-1)) > 0.999  # GPU fan within 1 f32 ulp of the oracle's
 
 
+def test_fan_plain_draw_bitexact(geo, torch_mod):
+    """The fan-mode draw with no output but the colour (a lane draws two
+    pixels, 8 rows apart, loads of both in flight): bit for bit the oracle's
+    f32 mirror with the same (host) fan, on ragged frames (partial 32 x 16
+    tiles), row blocks from any row, 8-row bands, an opaque and a
+    translucent sky; and equal to the same draw with every output requested
+    (the per-pixel epilogue)."""
+    from schwarzschild_raytracer_wgpu_amd.scenes import make_sky
+
+    dev = torch_mod.device("cuda:0")
+    fan = O.solve_ray_fan(50.0, 1.0, 1000, math.pi / 100, 400, R_OBS)
+    scene = geo.make_scene(1.0, 50.0, R_OBS, math.pi / 100, 1000, geo.GEO_MODE_FAN)
+    skies = (make_sky("equirect", (256, 128)),
+             np.random.default_rng(21).integers(0, 256, size=(64, 128, 4), dtype=np.uint8))
+    for sky in skies:
+        ctx = geo.Context(0)
+        ctx.set_sky(sky)
+        ctx.set_fan(fan)
+        for (w, h) in ((100, 57), (64, 36), (33, 17)):
+            frame = default_frame(w, h)
+            ref = O.render_f32(frame, scene, sky, w, h, fan=fan, threads=8)
+            for row0, nrows in ((0, h), (3, h - 3), (h - 5, 5)):
+                rgba = torch_mod.empty(nrows * w * 4, dtype=torch_mod.uint8, device=dev)
+                ctx.render_rows(frame, scene, w, h, row0, nrows, rgba)
+                torch_mod.cuda.synchronize()
+                got = rgba.cpu().numpy().reshape(nrows, w, 4)
+                assert np.array_equal(got, ref["rgba"][row0:row0 + nrows]), (w, h, row0)
+            full = render(geo, torch_mod, ctx, frame, scene, w, h)  # every output: the per-pixel path
+            assert_same(full, ref, fields=("mask", "uv", "rgba"))
+            # 8-row bands 1, 3, 5, ... packed
+            nb = (h // 8 - 1) // 2 + 1 if h >= 16 else 1
+            band0 = 1 if h >= 16 else 0
+            rgba = torch_mod.empty(nb * 8 * w * 4, dtype=torch_mod.uint8, device=dev)
+            ctx.render_bands(frame, scene, w, h, 8, band0, 2, nb, rgba)
+            torch_mod.cuda.synchronize()
+            got = rgba.cpu().numpy().reshape(nb * 8, w, 4)
+            for j in range(nb):
+                r0 = (band0 + 2 * j) * 8
+                n = max(0, min(8, h - r0))
+                assert np.array_equal(got[8 * j:8 * j + n], ref["rgba"][r0:r0 + n]), (w, h, j)
+        ctx.close()
+
+
 def test_sphere_buffer_fan_mode_matches_oracle(geo, torch_mod):
     """Reference-exact mode: BasicSphereBuffer.update_ray_fan + draw = fan lerp
     (shader.wgsl:77-84) with the GPU-solved fan."""

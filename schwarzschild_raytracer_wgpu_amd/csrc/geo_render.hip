@@ -242,7 +242,8 @@ __device__ __forceinline__ float pixel_lambda(const RenderArgs& a, float st, flo
 // Pixels per lane: a fan-mode lane (level-0 sampler) draws two, rows
 // kWaveRows apart, so one wave covers 16 x 8 pixels and each lane's loads of
 // the second pixel overlap the first's (the fan lerp and the texel quads are
-// the kernel's latency; its VALU work is short).
+// the kernel's latency; its VALU work is short).  The mip-mapped fan draw
+// measured the same either way (profiles/r03v_fan_mips_ab.txt) and keeps one.
 __host__ __device__ constexpr uint32_t lane_rows(int mode, bool mips) {
     return mode == GEO_MODE_FAN && !mips ? 2u : 1u;
 }

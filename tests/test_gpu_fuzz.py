@@ -102,8 +102,9 @@ def test_gpu_fuzz_fan_mode_bitexact(geo, torch_mod):  # noqa: F811
 
 def test_gpu_fuzz_mips_bitexact(geo, torch_mod):  # noqa: F811
     """GEO_FLAG_MIPS on the fuzz scenes (ragged 65 x 37 frames: helper lanes
-    on the right and bottom quads) with random sky sizes down to 1 x 1: the
-    oracle's mip restatement, bit for bit."""
+    on the right and bottom quads) with random sky sizes down to 1 x 1, in
+    direct, adaptive and fan mode: the oracle's mip restatement, bit for
+    bit."""
     from schwarzschild_raytracer_wgpu_amd import _lib
 
     w, h = W + 1, H + 1
@@ -120,8 +121,12 @@ def test_gpu_fuzz_mips_bitexact(geo, torch_mod):  # noqa: F811
         ctx.set_sky(sky)
         frame, scene, desc = random_scene(seed, w, h, adaptive=seed % 3 == 0)
         scene.flags |= _lib.GEO_FLAG_MIPS
+        fan = None
+        if seed % 3 == 1:
+            scene.mode = _lib.GEO_MODE_FAN
+            fan = ctx.solve_ray_fan(scene.sphere_r, scene.rs, 1000, scene.step, 400, scene.r_obs)
         hip = render(geo, torch_mod, ctx, frame, scene, w, h)
-        ref = O.render_mips_f32(frame, scene, sky, w, h, threads=4)
+        ref = O.render_mips_f32(frame, scene, sky, w, h, fan=fan, threads=4)
         same = all(np.array_equal(hip[f], ref[f]) for f in ("mask", "steps", "rgba")) and np.array_equal(
             hip["uv"].view(np.uint32), ref["uv"].view(np.uint32)) and hip["total"] == ref["steps_total"]
         if not same:

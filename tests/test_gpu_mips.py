@@ -116,6 +116,38 @@ def test_mips_adaptive_and_fan_modes(geo, torch_mod):
         assert np.array_equal(hip[f], ref[f]), f
 
 
+def test_mips_fan_mode_ragged_rows_bands_composite(geo, torch_mod):
+    """The mip-mapped fan draw (the reference's sampler on its display
+    path): ragged frames, even row blocks, 8-row bands and a composite over a
+    target, bit for bit."""
+    sky = sky_of("random_alpha", (200, 90))
+    fan = O.solve_ray_fan(50.0, 1.0, 1000, math.pi / 100, 400, float(np.sqrt(2.5 ** 2 + 0.1 ** 2)))
+    ctx = geo.Context(0)
+    ctx.set_sky(sky)
+    ctx.set_fan(fan)
+    for (w, h) in ((65, 37), (34, 20)):
+        frame = default_frame(w, h)
+        scene = mips(default_scene(mode=geo.GEO_MODE_FAN), geo)
+        ref = O.render_mips_f32(frame, scene, sky, w, h, fan=fan, threads=8)
+        same(render(geo, torch_mod, ctx, frame, scene, w, h), ref)
+        for r0, n in ((2, h - 2), (h - 1 - ((h - 1) & 1), 1 + ((h - 1) & 1))):
+            hip = render(geo, torch_mod, ctx, frame, scene, w, h, row0=r0, nrows=n)
+            assert np.array_equal(hip["rgba"], ref["rgba"][r0:r0 + n]), (w, h, r0)
+        nb = (h + 7) // 8
+        rgba = torch_mod.empty(nb * 8 * w * 4, dtype=torch_mod.uint8, device=torch_mod.device("cuda:0"))
+        ctx.render_bands(frame, scene, w, h, 8, 0, 1, nb, rgba)
+        torch_mod.cuda.synchronize()
+        got = rgba.cpu().numpy().reshape(nb * 8, w, 4)[:h]
+        assert np.array_equal(got, ref["rgba"]), (w, h)
+        target = np.random.default_rng(w).integers(0, 256, size=(h, w, 4), dtype=np.uint8)
+        cs = mips(default_scene(mode=geo.GEO_MODE_FAN), geo)
+        cs.flags |= geo._lib.GEO_FLAG_COMPOSITE
+        hip = render(geo, torch_mod, ctx, frame, cs, w, h, target=target)
+        assert np.array_equal(hip["rgba"], O.render_mips_f32(frame, cs, sky, w, h, fan=fan, threads=8,
+                                                             target=target)["rgba"]), (w, h)
+    ctx.close()
+
+
 def test_mips_composite_over_target(geo, torch_mod):
     sky = sky_of("random_alpha", (128, 64))
     w, h = 80, 46

@@ -48,7 +48,8 @@ constexpr int kWaveRows = 64 / kWaveW;  // steps per wave; tools/ubench/loop_ab.
 constexpr int kWavesX = 2;              // waves side by side in a tile
 constexpr int kTileW = kWaveW * kWavesX;
 constexpr int kTileH = 8;               // a block kTileW x kTileH
-constexpr int kBlock = kTileW * kTileH;  // 256 threads = 4 waves (32 x 8, 2 x 2 waves of 16 x 4)
+constexpr int kBlock = kTileW * kTileH;  // 256 threads = 4 waves (32 x 8, 2 x 2 waves of 16 x 4;
+                                         // twice as tall with two pixels per lane, lane_rows)
 static_assert(kTileH % kWaveRows == 0 && kBlock % 64 == 0, "tile of whole waves");
 // band heights are multiples of 8 (the C-ABI's contract, geo.h), so a wave's
 // rows never straddle a band for any wave shape up to 8 rows

@@ -5,7 +5,7 @@ the present step of the absent wgpu_renderer loop.
 
   python tools/render_frame.py out.png [--width 1920 --height 1080]
         [--sky eso0932a.jpg --planet world_8k.png --clouds transparent_clouds.png]
-        [--frames 60 --orbit 3.2]
+        [--frames 60 --orbit 3.2] [--mipmaps] [--fan]
 
 Without texture files the synthetic equirect sky of the benchmarks is used for
 the sky sphere and the planet/cloud spheres are skipped.  Units: rs = 1 (the
@@ -34,6 +34,9 @@ def main():
     p.add_argument("--orbit", type=float, default=0.0, help="start an orbit with this rotation (observer.rs:162)")
     p.add_argument("--no-disk", action="store_true")
     p.add_argument("--mipmaps", action="store_true", help="trilinear mip-mapped textures, as the reference samples them")
+    p.add_argument("--fan", action="store_true",
+                   help="the reference's display path: per-frame 400-node f64 ray fans and the fan lerp "
+                        "(GEO_MODE_FAN) instead of a geodesic per pixel")
     args = p.parse_args()
 
     import torch
@@ -48,11 +51,14 @@ def main():
     if args.orbit:
         obs.start_orbit(args.orbit)
     sky = imageio.load_texture(args.sky) if args.sky else make_sky("equirect", (4096, 2048))
-    spheres = [g.BasicSphereBuffer(0, 50.0, 1.0, sky, mipmaps=args.mipmaps)]
+    mode = g.GEO_MODE_FAN if args.fan else g.GEO_MODE_DIRECT
+    spheres = [g.BasicSphereBuffer(0, 50.0, 1.0, sky, mode=mode, mipmaps=args.mipmaps)]
     if args.planet:
-        spheres.append(g.BasicSphereBuffer(0, 1.1, 1.0, imageio.load_texture(args.planet), mipmaps=args.mipmaps))
+        spheres.append(g.BasicSphereBuffer(0, 1.1, 1.0, imageio.load_texture(args.planet), mode=mode,
+                                           mipmaps=args.mipmaps))
     if args.clouds:
-        spheres.append(g.BasicSphereBuffer(0, 1.2, 1.0, imageio.load_texture(args.clouds), mipmaps=args.mipmaps))
+        spheres.append(g.BasicSphereBuffer(0, 1.2, 1.0, imageio.load_texture(args.clouds), mode=mode,
+                                           mipmaps=args.mipmaps))
     disk = None if args.no_disk else g.PointCloud.new_accretion_disk(spheres[0].ctx, 1.0, obs.get_position(), True)
     tgt = g.RenderTarget(w, h, torch.empty(w * h * 4, dtype=torch.uint8, device="cuda:0"))
     renderer = g.Renderer(obs)
@@ -68,7 +74,8 @@ def main():
         imageio.save_ppm(args.out, tgt.rgba, w, h)
     else:
         imageio.save_png(args.out, tgt.rgba, w, h)
-    print(f"wrote {args.out} ({w}x{h}, {len(spheres)} sphere(s){', accretion disk' if disk else ''})")
+    print(f"wrote {args.out} ({w}x{h}, {len(spheres)} sphere(s){', accretion disk' if disk else ''}, "
+          f"{'fan lerp' if args.fan else 'per-pixel geodesics'})")
 
 
 if __name__ == "__main__":

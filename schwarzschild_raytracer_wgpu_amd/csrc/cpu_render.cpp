@@ -91,7 +91,9 @@ uint32_t sample_trilinear(const CpuJob& j, float rho2, float U, float V) {
 // GEO_FLAG_MIPS rows: each pixel's level of detail comes from its
 // frame-aligned 2 x 2 quad (partners x ^ 1 and y ^ 1, traced even where they
 // lie outside the frame or the requested rows, like the kernel's helper
-// lanes); rows tid, tid + nthreads, ... as run_rows.
+// lanes).  A thread takes the requested rows of every nthreads-th quad row
+// pair (frame rows 2k, 2k + 1), so a pair is traced once when both of its
+// rows are requested.
 unsigned long long run_rows_mips(const CpuJob& j, unsigned tid, unsigned nthreads) {
     unsigned long long total = 0;
     const bool composite = (j.s->flags & GEO_FLAG_COMPOSITE) != 0;
@@ -106,8 +108,9 @@ unsigned long long run_rows_mips(const CpuJob& j, unsigned tid, unsigned nthread
         have[b] = py;
         return rows[b];
     };
-    for (uint32_t ly = tid; ly < j.nrows; ly += nthreads) {
+    for (uint32_t ly = 0; ly < j.nrows; ++ly) {
         const uint32_t py = j.row0 + ly * j.row_step;
+        if ((py >> 1) % nthreads != tid) continue;
         (void)row_of(py);
         const std::vector<Traced>& ry = row_of(py ^ 1u);  // never evicts row py
         const std::vector<Traced>& rr = have[0] == (int64_t)py ? rows[0] : rows[1];

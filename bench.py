@@ -15,6 +15,10 @@ resident in HBM, sky uploaded once).
 
   python bench.py [--gpus N] [--steps K] [--warmup W]
   torchrun --nproc-per-node N bench.py --gpus N ...
+
+`python bench.py --gpus N` with no WORLD_SIZE in the environment starts the
+N rank processes itself (launch_ranks, before anything touches the GPU),
+waits for them, forwards rank 0's line and exits non-zero if any rank fails.
 """
 from __future__ import annotations
 
@@ -22,7 +26,11 @@ import argparse
 import json
 import math
 import os
+import signal
+import socket
+import subprocess
 import sys
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -91,8 +99,103 @@ def parse():
     return p.parse_args()
 
 
+def _free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n: int, argv: list[str], rank_cmd: list[str] | None = None, grace_s: float = 10.0) -> int:
+    """Start n rank processes and wait for them: one process per GPU, the
+    torch.distributed env contract (RANK, LOCAL_RANK, WORLD_SIZE,
+    LOCAL_WORLD_SIZE, MASTER_ADDR=127.0.0.1, a free MASTER_PORT).  The caller
+    must not have touched the GPU (this process only forks children; it never
+    execs).  Rank 0's JSON lines go to this process's stdout (the one line
+    the contract asks for); everything else a rank prints on stdout (the
+    peers' output, gloo's connection notices) goes to stderr.  When a rank
+    fails, the others are
+    terminated (SIGTERM, SIGKILL after grace_s) and its exit code is returned;
+    0 when every rank exits 0.  rank_cmd replaces `python -u bench.py` (tests
+    use a stub rank)."""
+    cmd = (rank_cmd or [sys.executable, "-u", os.path.abspath(__file__)]) + list(argv)
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE if r == 0 else sys.stderr.fileno()))
+
+    def pump(src):
+        for line in iter(src.readline, b""):
+            dst = sys.stdout if line.lstrip().startswith(b"{") else sys.stderr
+            dst.buffer.write(line)
+            dst.flush()
+
+    pumper = threading.Thread(target=pump, args=(procs[0].stdout,), daemon=True)
+    pumper.start()
+
+    def stop_all(sig=signal.SIGTERM):
+        for p in procs:
+            if p.poll() is None:
+                try:
+                    p.send_signal(sig)
+                except ProcessLookupError:
+                    pass
+
+    prev = {}
+
+    def forward(signum, _frame):  # the launcher's own SIGTERM/SIGINT end the ranks too
+        stop_all(signum)
+
+    for s in (signal.SIGTERM, signal.SIGINT):
+        prev[s] = signal.signal(s, forward)
+    rc = 0
+    try:
+        live = set(range(n))
+        while live:
+            for r in sorted(live):
+                code = procs[r].poll()
+                if code is None:
+                    continue
+                live.discard(r)
+                if code != 0 and rc == 0:
+                    rc = code if code > 0 else 128 - code  # -signal -> 128 + signal
+                    print(f"launch_ranks: rank {r} exited with {code}; stopping the other ranks", file=sys.stderr)
+                    stop_all()
+                    t_end = time.monotonic() + grace_s
+                    while any(p.poll() is None for p in procs) and time.monotonic() < t_end:
+                        time.sleep(0.05)
+                    stop_all(signal.SIGKILL)
+            time.sleep(0.05)
+        for p in procs:
+            p.wait()
+        pumper.join(timeout=5.0)
+    finally:
+        for s, h in prev.items():
+            signal.signal(s, h)
+    return rc
+
+
+def rank_devices(dist, world: int, local: int, rdev) -> list[dict]:
+    """Every rank's HIP device: index and PCI bus id (all-gathered, so rank 0
+    can print the placement the job actually had)."""
+    import torch
+
+    p = torch.cuda.get_device_properties(local)
+    mine = torch.tensor([local, p.pci_domain_id, p.pci_bus_id, p.pci_device_id], dtype=torch.int64, device=rdev)
+    every = [mine]
+    if world > 1:
+        every = [torch.empty_like(mine) for _ in range(world)]
+        dist.all_gather(every, mine)
+    return [{"rank": r, "device": int(t[0]), "pci": "%04x:%02x:%02x.0" % (int(t[1]), int(t[2]), int(t[3]))}
+            for r, t in enumerate(every)]
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # start the N ranks from here, before any GPU call (the parent only waits)
+        raise SystemExit(launch_ranks(args.gpus, sys.argv[1:]))
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -106,6 +209,10 @@ def main():
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     ndev = torch.cuda.device_count()
+    if world > ndev and args.dist_backend == "nccl":
+        # RCCL refuses two ranks on one GPU ("Duplicate GPU detected")
+        raise SystemExit(f"--gpus {world} with the nccl backend needs {world} GPUs, this node has {ndev} "
+                         f"(--dist-backend gloo runs several ranks per GPU, for rehearsals)")
     local = local % max(1, ndev)  # >1 rank per GPU only for gloo rehearsals on a 1-GPU box
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
@@ -114,6 +221,8 @@ def main():
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group("gloo")
+        if dist.get_world_size() != world:
+            raise SystemExit(f"process group has {dist.get_world_size()} ranks, WORLD_SIZE={world}")
 
     if args.frames_per_gather is None:
         args.frames_per_gather = max(1, min(8, args.steps // 10))
@@ -142,6 +251,7 @@ def main():
     from schwarzschild_raytracer_wgpu_amd.dist import ShardedFrame
 
     rdev = dev if args.dist_backend == "nccl" else "cpu"
+    devices = rank_devices(dist, world, local, rdev)
 
     def make_sf(lead):
         return ShardedFrame(ctx, frame, scene, W, H, args.band_rows, rank, world, dev, dist if world > 1 else None,
@@ -199,8 +309,17 @@ def main():
     diag_mask = torch.zeros(n_loc, dtype=torch.uint8, device=dev)
     diag_steps = torch.zeros(n_loc, dtype=torch.int32, device=dev)
     diag_ctr = torch.zeros(1, dtype=torch.int64, device=dev)
-    sf.render_local(sf.bufs[0], out_mask=diag_mask, out_steps=diag_steps, steps_total=diag_ctr)
+    diag_uv = torch.zeros(n_loc * 2, dtype=torch.float32, device=dev) if mode == g.GEO_MODE_FAN else None
+    sf.render_local(sf.bufs[0], out_mask=diag_mask, out_uv=diag_uv, out_steps=diag_steps, steps_total=diag_ctr)
     torch.cuda.synchronize()
+    # the fan-mode draw is a memory-side kernel: its algorithmic bytes are the
+    # RGBA8 it writes plus the distinct sky texels its rows sample (and the fan)
+    sky_touch = None
+    if mode == g.GEO_MODE_FAN:
+        valid = torch.zeros(n_loc, dtype=torch.bool, device=dev)
+        valid.view(-1, W)[: L.rows_mine()] = True  # the packed rows this rank renders
+        sky_touch = sky_bytes_touched(diag_uv.view(-1, 2), (diag_mask == 0) & valid, sky.shape[1], sky.shape[0])
+        del valid
     st = diag_steps.to(torch.int64)
     hits = int(((diag_mask == 0) & (st > 0)).sum().item())  # unwritten (clipped) rows are 0
     rows_mine = L.rows_mine()
@@ -355,7 +474,7 @@ def main():
             raise SystemExit(1)
         return
 
-    value = total_steps / elapsed_max
+    value = total_steps / elapsed_max if mode != g.GEO_MODE_FAN else total_pixels / elapsed_max
     # roofline for the dominant kernel, on this rank: algorithmic flops per
     # launch / avg launch time (event pairs, which add ~2 % to what they time:
     # DESIGN.md §4), and the same flops per frame of the compute-only pass's
@@ -363,7 +482,12 @@ def main():
     achieved_tflops = flops_per_launch / (kernel_ms_avg * 1e-3) / 1e12
     wall_tflops = flops_per_launch / (compute_max / args.steps) / 1e12
     pmc_file, pmc = pmc_profile(args.config, args.mode, world) if not args.mips else (None, {})
-    if mode == g.GEO_MODE_ADAPTIVE:
+    if mode == g.GEO_MODE_FAN:
+        metric = (f"pixels/sec at {W}x{H}, fan-mode draw (the reference's display path: 400-node fan lerp, "
+                  f"shader.wgsl:77-105; whole job)")
+        unit = "pixels/s"
+        stepping = "fan lerp (no per-pixel geodesic)"
+    elif mode == g.GEO_MODE_ADAPTIVE:
         metric = (f"geodesic-step-attempts·pixels/sec at {W}x{H}, adaptive RK5(4) tol {cfg.tol:g} "
                   f"(whole job; /GPU = value/n_gpus)")
         unit = "geodesic-step-attempts·pixels/s"
@@ -399,6 +523,9 @@ def main():
             "render_streams": sf.S,
         },
         "per_gpu": value / world,
+        "world_size": dist.get_world_size() if world > 1 else 1,
+        "dist_backend": args.dist_backend if world > 1 else None,
+        "rank_devices": devices,
         "per_rank": per_rank,
         "pixels_per_s": total_pixels / elapsed_max,
         "frames_per_s": args.steps / elapsed_max,
@@ -412,7 +539,7 @@ def main():
                                  "inside it)" % sf.S)},
         "pipelined": pipelined,
         "link_probe": link_probe,
-        "compute_only": {"value": total_steps / compute_max, "ms_per_step": compute_max / args.steps * 1e3,
+        "compute_only": {"value": (total_steps if mode != g.GEO_MODE_FAN else total_pixels) / compute_max, "ms_per_step": compute_max / args.steps * 1e3,
                          "what": "the same K frames rendered on the same streams without pack, gather or "
                                  "reassembly (max over ranks)"},
         "spinup_frames": spin,
@@ -439,15 +566,87 @@ def main():
             "pmc_profile": pmc_file,
         },
     }
-    if world == 1 and not args.no_cpu_baseline and mode != g.GEO_MODE_FAN:
-        out["cpu_baseline"] = cpu_baseline(frame, scene, sky, W, H, args)
-        out["reference_equivalent"] = reference_fan_cost(ctx, cfg, obs.get_radial_position())
+    if mode == g.GEO_MODE_FAN:
+        out["roofline"] = fan_roofline(sky_touch, rows_mine * W, kernel_ms_avg, compute_max / args.steps, pmc,
+                                       pmc_file, mode)
+    cpu_ok = True
+    if world == 1 and not args.no_cpu_baseline:
+        fan = None
+        if mode == g.GEO_MODE_FAN:  # the fan the draws read, as the host's copy
+            fan = ctx.solve_ray_fan(cfg.sphere_r, cfg.rs, cfg.max_steps, cfg.step, 400, obs.get_radial_position())
+        out["cpu_baseline"] = cpu_baseline(frame, scene, sky, W, H, args, ctx, fan)
+        cpu_ok = out["cpu_baseline"]["matches_gpu"]["ok"]
+        if mode != g.GEO_MODE_FAN:
+            out["reference_equivalent"] = reference_fan_cost(ctx, cfg, obs.get_radial_position())
     out["frame_check"] = frame_check
     print(json.dumps(out), flush=True)
+    if not cpu_ok:
+        raise SystemExit("cpu_baseline: the CPU path's rows differ from the GPU frame's (matches_gpu)")
     if world > 1:
         dist.destroy_process_group()
     if not frame_ok:
         raise SystemExit("frame check failed: an assembled frame differs from the single-launch frame")
+
+
+def sky_bytes_touched(uv, sampled, tw: int, th: int) -> dict:
+    """Distinct sky bytes a frame's level-0 bilinear samples read (device
+    tensors: uv (n, 2) f32, sampled (n,) bool = pixels that take a sample).
+    Texel quads as the sampler forms them (geo_pixel.h sample_sky_quad_f:
+    n = floor(U tw 256 - 128) in one f32 rounding, x0 = n >> 8; U wraps, V
+    clamps), counted once each: the algorithmic read bytes.  Beside them the
+    distinct 128-B lines of the padded sky the device reads them from."""
+    import torch
+
+    u = uv[sampled, 0].double()
+    v = uv[sampled, 1].double()
+    # the product of two f32 is exact in f64, so one rounding of U tw256 - 128
+    # to f32 is the fma's
+    nx = torch.floor((u * (tw * 256.0) - 128.0).float()).to(torch.int64) >> 8
+    ny = torch.floor((v * (th * 256.0) - 128.0).float()).to(torch.int64) >> 8
+    texels, lines = [], []
+    for dx in (0, 1):
+        for dy in (0, 1):
+            x = torch.remainder(nx + dx, tw)
+            y = torch.clamp(ny + dy, 0, th - 1)
+            texels.append(y * tw + x)
+            lines.append(((ny + dy + 1) * (tw + 2) + (nx + dx + 1)) * 4 // 128)  # padded layout (geo::pad_sky)
+    n_tex = int(torch.unique(torch.cat(texels)).numel())
+    n_lines = int(torch.unique(torch.cat(lines)).numel())
+    return {"sampled_pixels": int(u.numel()), "texel_bytes": 4 * n_tex, "line_bytes_padded": 128 * n_lines,
+            "sky_bytes": 4 * tw * th}
+
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md §HBM: 8 TB/s spec)
+
+
+def fan_roofline(touch: dict, pixels: int, kernel_ms: float, wall_ms: float, pmc: dict, pmc_file, mode) -> dict:
+    """The fan-mode draw's roofline: HBM.  Algorithmic bytes per launch = 4 B
+    of RGBA8 written per pixel + the distinct sky texels sampled x 4 B + the
+    400-node fan (1.6 KB), over the kernel's average launch time."""
+    written = 4 * pixels
+    alg = written + touch["texel_bytes"] + 4 * 400
+    achieved = alg / (kernel_ms * 1e-3) / 1e9
+    return {
+        "bound": "hbm",
+        "achieved": achieved,
+        "peak": HBM_PEAK_GBS,
+        "unit": "GB/s",
+        "frac": achieved / HBM_PEAK_GBS,
+        "traffic": pmc.get("traffic_bytes"),
+        "kernel": f"geo_render_kernel<{mode}> (fan-mode draw, two pixels per lane)",
+        "algorithmic_bytes_per_launch": alg,
+        "bytes": "4 B RGBA8 written per pixel + distinct sky texels the frame samples x 4 B (counted once, on the "
+                 "device, from the diagnostic pass's UVs) + the 1.6-KB fan",
+        "written_bytes": written,
+        "sky_texel_bytes": touch["texel_bytes"],
+        "sky_line_bytes_padded": touch["line_bytes_padded"],
+        "sky_bytes": touch["sky_bytes"],
+        "sampled_pixels": touch["sampled_pixels"],
+        "achieved_wall": alg / (wall_ms * 1e-3) / 1e9,
+        "frac_wall": alg / (wall_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+        "valu_per_simd_cycle_pmc": pmc.get("valu_per_simd_cycle"),
+        "pmc_profile": pmc_file,
+    }
 
 
 def spin_up(sf, n):
@@ -502,7 +701,8 @@ def pmc_profile(config, mode, world):
 
     if world != 1:
         return None, {}
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_{config}_pmc.json")))
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_{config}_pmc.json")) +
+                   glob.glob(os.path.join(ROOT, "profiles", f"*_{config}_{mode}_pmc.json")))
     for path in reversed(files):
         with open(path) as f:
             d = json.load(f)
@@ -582,56 +782,150 @@ def cpu_model() -> str:
     return platform.processor() or "unknown"
 
 
-def cpu_baseline(frame, scene, sky, W, H, args):
-    """The same per-pixel integrator on the host cores: geo_render_cpu
-    (libgeo_cpu.so, include/geo/geo_cpu.h), the product's geo_pixel.h built
-    for the host (g++ -O2 -ffp-contract=off), scalar, std::thread row blocks
-    (BASELINE.md §3).  One warm-up, then the median of 3 runs of the frame
-    (every 4th row above 4K)."""
-    import ctypes
-    import statistics
+def cpu_quota() -> float | None:
+    """CPUs this process may use per the cgroup v2 quota (cpu.max), or None."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, p = f.read().split()[:2]
+        return None if q == "max" else int(q) / int(p)
+    except (OSError, ValueError):
+        return None
 
-    import numpy as np
+
+def _cpu_lib():
+    import ctypes
 
     lib = ctypes.CDLL(os.path.join(ROOT, "schwarzschild_raytracer_wgpu_amd", "libgeo_cpu.so"))
     vp, u32 = ctypes.c_void_p, ctypes.c_uint32
     lib.geo_render_cpu.restype = ctypes.c_int
     lib.geo_render_cpu.argtypes = [vp, vp, vp, u32, u32, vp, u32, u32, u32, u32, u32, u32, ctypes.c_int, vp, vp, vp,
                                    vp, vp]
-    threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+    return lib
+
+
+def cpu_baseline(frame, scene, sky, W, H, args, ctx, fan=None):
+    """The same per-pixel integrator on the host cores: geo_render_cpu
+    (libgeo_cpu.so, include/geo/geo_cpu.h), the product's geo_pixel.h built
+    for the host (g++ -O2 -ffp-contract=off), scalar, std::thread row blocks
+    (BASELINE.md §3).  Threads = every core this process may run on
+    (sched_getaffinity, SURVEY.md §8d's hardware_concurrency); the 16-thread
+    figure (the GPU box's CPU share) beside it.  One warm-up, then the median
+    of 3 runs of the frame (every 4th row above 4K).
+
+    North_star's comparator, outside the timed runs: the CPU's rows against
+    the same rows of the GPU frame (geo_render_rows): RGBA bytes, the
+    hit-classification mask and the UV bits; matches_gpu false exits the
+    bench non-zero."""
+    import ctypes
+    import statistics
+
+    import numpy as np
+    import torch
+
+    lib = _cpu_lib()
+    fan_arr = None if fan is None else np.ascontiguousarray(fan, dtype=np.float32)
+    fan_p, n_fan = (None, 0) if fan_arr is None else (fan_arr.ctypes.data, fan_arr.size)
+    all_cores = len(os.sched_getaffinity(0))
     k = args.cpu_row_step or (1 if W * H <= 3840 * 2160 else 4)
+    if args.mips and k > 1 and k % 2:
+        k += 1  # even rows only, so the partner rows traced for the footprint are the odd rows k m + 1
     nrows = (H + k - 1) // k
     sky = np.ascontiguousarray(sky, dtype=np.uint8)
     rgba = np.empty((nrows, W, 4), np.uint8)
     total = ctypes.c_ulonglong()
-    times, steps = [], None
-    for rep in range(4):
-        t0 = time.perf_counter()
-        rc = lib.geo_render_cpu(ctypes.addressof(frame), ctypes.addressof(scene), sky.ctypes.data, sky.shape[1],
-                                sky.shape[0], None, 0, W, H, 0, nrows, k, threads, rgba.ctypes.data, None, None,
+
+    def run(threads, rgba=rgba, mask=None, uv=None, row0=0, n=nrows, flags_scene=scene):
+        rc = lib.geo_render_cpu(ctypes.addressof(frame), ctypes.addressof(flags_scene), sky.ctypes.data, sky.shape[1],
+                                sky.shape[0], fan_p, n_fan, W, H, row0, n, k, threads, rgba.ctypes.data,
+                                None if mask is None else mask.ctypes.data, None if uv is None else uv.ctypes.data,
                                 None, ctypes.addressof(total))
-        dt = time.perf_counter() - t0
         if rc != 0:
             raise SystemExit(f"geo_render_cpu: {rc}")
-        if rep > 0:  # rep 0 warms up
-            times.append(dt)
-        steps = total.value
-    med = statistics.median(times)
+        return total.value
+
+    def timed(threads):
+        times, steps = [], None
+        for rep in range(4):
+            t0 = time.perf_counter()
+            steps = run(threads)
+            dt = time.perf_counter() - t0
+            if rep > 0:  # rep 0 warms up
+                times.append(dt)
+        return statistics.median(times), times, steps
+
+    med, times, steps = timed(all_cores)
+    fixed16 = None
+    if all_cores != 16:
+        m16, t16, _ = timed(16)
+        fixed16 = {"threads": 16, "seconds_per_run": t16, "value": None}
+    # GEO_FLAG_MIPS with k > 1: geo_render_cpu also traces each sampled row's
+    # quad partner (row + 1) for the footprint; those rows' steps are work
+    # done in the timed runs, counted here (the partner rows alone, untimed)
+    partner_steps = 0
+    if args.mips and k > 1:
+        partner = np.empty(((H - 1 + k - 1) // k, W, 4), np.uint8)
+        plain = type(scene).from_buffer_copy(scene)
+        plain.flags = scene.flags & ~g_flag_mips()
+        partner_steps = run(all_cores, rgba=partner, row0=1, n=(H - 1 + k - 1) // k, flags_scene=plain)
+    work = steps + partner_steps
+    if fixed16 is not None:
+        fixed16["value"] = work / statistics.median(fixed16["seconds_per_run"])
+
+    # the comparator (untimed): CPU rows with mask and UV vs the GPU frame's rows
+    mask_c = np.empty((nrows, W), np.uint8)
+    uv_c = np.empty((nrows, W, 2), np.float32)
+    rgba_c = np.empty_like(rgba)
+    run(all_cores, rgba=rgba_c, mask=mask_c, uv=uv_c)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    g_rgba = torch.empty(H * W * 4, dtype=torch.uint8, device=dev)
+    g_mask = torch.empty(H * W, dtype=torch.uint8, device=dev)
+    g_uv = torch.empty(H * W * 2, dtype=torch.float32, device=dev)
+    ctx.render_rows(frame, scene, W, H, 0, H, g_rgba, out_mask=g_mask, out_uv=g_uv)
+    torch.cuda.synchronize()
+    g_rgba = g_rgba.view(H, W, 4)[::k].cpu().numpy()
+    g_mask = g_mask.view(H, W)[::k].cpu().numpy()
+    g_uv = g_uv.view(H, W, 2)[::k].cpu().numpy()
+    rgba_same = bool(np.array_equal(rgba, g_rgba)) and bool(np.array_equal(rgba_c, g_rgba))
+    mask_diff = int((mask_c != g_mask).sum())
+    uv_bits_diff = int((uv_c.view(np.uint32) != g_uv.view(np.uint32)).any(axis=-1).sum())
+    du = np.abs(uv_c[..., 0].astype(np.float64) - g_uv[..., 0])
+    du = np.minimum(du, 1.0 - du)  # U wraps
+    dv = np.abs(uv_c[..., 1].astype(np.float64) - g_uv[..., 1])
+    uv_err = float(max(du.max(initial=0.0), dv.max(initial=0.0)))
+    ok = rgba_same and mask_diff == 0 and uv_err <= 1e-4
     what = "full" if k == 1 else f"every {k}th row of the"
+    unit = ("geodesic-step-attempts·pixels/s" if scene.mode == 2 else
+            "pixels/s" if scene.mode == 1 else "geodesic-steps·pixels/s")
+    value = (nrows * W) / med if scene.mode == 1 else work / med
     return {
-        "value": steps / med,
-        "unit": "geodesic-step-attempts·pixels/s" if scene.mode == 2 else "geodesic-steps·pixels/s",
-        "cores": threads,
+        "value": value,
+        "unit": unit,
+        "cores": all_cores,
         "kind": "port",
         "cpu_model": cpu_model(),
+        "cgroup_cpu_quota": cpu_quota(),
         "sample": f"{what} {W}x{H} frame ({nrows * W} pixels, {steps} steps"
-                  f"{', mip-mapped: quad partner rows traced too' if args.mips and k > 1 else ''}): "
-                  f"median of 3 runs after one warm-up, {threads} threads",
+                  f"{f' + {partner_steps} in the traced quad-partner rows' if partner_steps else ''}): "
+                  f"median of 3 runs after one warm-up, {all_cores} threads (every core in this process's "
+                  f"affinity mask)",
         "seconds_per_run": times,
+        "threads_16": fixed16,
+        "matches_gpu": {
+            "ok": ok, "rows_compared": nrows, "pixels_compared": nrows * W,
+            "rgba_identical": rgba_same, "mask_mismatches": mask_diff, "uv_bit_mismatches": uv_bits_diff,
+            "uv_max_abs_err": uv_err,
+            "what": "geo_render_cpu's rows vs the same rows of a geo_render_rows frame (device): RGBA bytes, "
+                    "hit mask, UV (north_star: mask pixel for pixel, UV within 1e-4)",
+        },
         "implementation": "geo_render_cpu (libgeo_cpu.so): geo_pixel.h compiled for the host, g++ -O2 "
-                          "-ffp-contract=off -mfma -msse4.1, scalar, std::thread row blocks; output bit-identical "
-                          "to the kernel's (tests/test_cpu_baseline.py)",
+                          "-ffp-contract=off -mfma -msse4.1, scalar, std::thread row blocks",
     }
+
+
+def g_flag_mips() -> int:
+    from schwarzschild_raytracer_wgpu_amd import _lib
+
+    return _lib.GEO_FLAG_MIPS
 
 
 if __name__ == "__main__":

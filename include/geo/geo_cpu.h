@@ -32,7 +32,12 @@ extern "C" {
  * fan/n_fan: the ray fan (GEO_MODE_FAN only).  out_rgba8 is required (read
  * too under GEO_FLAG_COMPOSITE); out_mask, out_uv, out_steps and steps_total
  * may be NULL.  threads <= 0: std::thread::hardware_concurrency().  Returns
- * GEO_OK or GEO_EINVAL.  Blocking; reentrant. */
+ * GEO_OK or GEO_EINVAL.  Scenes and skies geo_render_rows or geo_set_sky
+ * reject are rejected here too (max_steps > 2^24, a sky side > 2^20, a
+ * padded mip chain of 2^31 bytes or more), so the bit-for-bit equality holds
+ * for every scene and sky either path accepts; row0 and row_step are free
+ * (the device's GEO_FLAG_MIPS even-row rule does not apply).  Blocking;
+ * reentrant. */
 int geo_render_cpu(const geo_frame* frame, const geo_scene* scene, const uint8_t* sky_rgba8, uint32_t sky_w,
                    uint32_t sky_h, const float* fan, uint32_t n_fan, uint32_t width, uint32_t height, uint32_t row0,
                    uint32_t nrows, uint32_t row_step, int threads, uint8_t* out_rgba8, uint8_t* out_mask,

@@ -207,6 +207,14 @@ extern "C" int geo_render_cpu(const geo_frame* frame, const geo_scene* scene, co
         return GEO_EINVAL;
     const bool adaptive = scene->mode == GEO_MODE_ADAPTIVE;
     if (adaptive ? !(scene->tol >= 0.0f && scene->tol <= 3.0e38f) : scene->tol != 0.0f) return GEO_EINVAL;
+    // what geo_render_rows and geo_set_sky reject, rejected alike: the two
+    // paths accept the same inputs, so "equal bit for bit" covers them all
+    if (scene->max_steps > (1u << 24)) return GEO_EINVAL;  // render_impl: a wave's step sum must fit u32
+    if (sky_w > (1u << 20) || sky_h > (1u << 20)) return GEO_EINVAL;
+    uint64_t chain_bytes = 0;  // geo_set_sky: the padded mip chain below 2^31 bytes
+    for (int l = 0; l < geo::kSkyMipLevels; ++l)
+        chain_bytes += ((uint64_t)geo::mip_dim(sky_w, l) + 2u) * ((uint64_t)geo::mip_dim(sky_h, l) + 2u) * 4u;
+    if (chain_bytes >= (1ull << 31)) return GEO_EINVAL;
     // the texture as u32 texels (any alignment of the caller's bytes)
     std::vector<uint32_t> sky((size_t)sky_w * sky_h);
     std::memcpy(sky.data(), sky_rgba8, sky.size() * 4u);

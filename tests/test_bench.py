@@ -21,7 +21,8 @@ def test_pmc_profile_only_for_the_profiled_workload():
     t = bench.pmc_profile("cfg3_4k", "direct", 1)[1].get("traffic_bytes")
     assert t is not None and 5e7 < t < 2e8  # ~90 MB per 4K frame
     assert bench.pmc_profile("cfg3_4k", "adaptive", 1) == (None, {})  # a direct-mode profile
-    assert bench.pmc_profile("cfg3_4k", "fan", 1) == (None, {})
+    fan = bench.pmc_profile("cfg3_4k", "fan", 1)  # the fan-mode draw's own profile (profiles/*_cfg3_4k_fan_pmc.json)
+    assert fan[0] is not None and "fan" in fan[0] and 3e7 < fan[1]["traffic_bytes"] < 2e8
     assert bench.pmc_profile("cfg3_4k", "direct", 2) == (None, {})  # full-frame bytes vs a rank's share
     assert bench.pmc_profile("cfg5_8k_adaptive", "adaptive", 1)[0] is not None
     assert bench.pmc_profile("cfg2_1080p", "direct", 1)[0] is not None

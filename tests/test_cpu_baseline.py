@@ -111,6 +111,13 @@ def test_cpu_baseline_rejects(cpu):
     assert render_cpu(cpu, frame, fs, sky, w, h)[0] == GEO_EINVAL  # fan mode without a fan
     neg = default_scene(64, step=-0.1)
     assert render_cpu(cpu, frame, neg, sky, w, h)[0] == GEO_EINVAL
+    # what geo_render_rows / geo_set_sky reject: the step budget
+    # past 2^24, a sky side past 2^20
+    big = default_scene(max_steps=(1 << 24) + 1)
+    assert render_cpu(cpu, frame, big, sky, w, h)[0] == GEO_EINVAL
+    assert render_cpu(cpu, frame, default_scene(max_steps=1 << 24), sky, w, h, nrows=1)[0] == GEO_OK
+    tall = np.zeros(((1 << 20) + 1, 1, 4), np.uint8)
+    assert render_cpu(cpu, frame, scene, tall, w, h, nrows=1)[0] == GEO_EINVAL
 
 
 def test_cpu_baseline_mips(cpu):

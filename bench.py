@@ -567,7 +567,7 @@ def main():
         },
     }
     if mode == g.GEO_MODE_FAN:
-        out["roofline"] = fan_roofline(sky_touch, rows_mine * W, kernel_ms_avg, compute_max / args.steps, pmc,
+        out["roofline"] = fan_roofline(sky_touch, rows_mine * W, kernel_ms_avg, compute_max / args.steps * 1e3, pmc,
                                        pmc_file, mode)
     cpu_ok = True
     if world == 1 and not args.no_cpu_baseline:

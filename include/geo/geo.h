@@ -241,6 +241,16 @@ int geo_assemble_lead(geo_ctx* ctx, const uint8_t* lead_src, size_t lead_frame_s
  * bytes on the links for the multi-GPU present.  Asynchronous on `stream`. */
 int geo_pack_rgb(geo_ctx* ctx, const uint8_t* rgba, uint64_t npixels, uint8_t* rgb, void* stream);
 
+/* The workgroup dispatch order of this context's renders: workgroup i draws
+ * tile (order[i] & 0xFFFF, order[i] >> 16) of a tiles_x x tiles_y grid of
+ * 32 x 8-pixel tiles (32 x 16 in fan mode with the level-0 sampler) over the
+ * rendered rows; order must be a permutation of the grid's tiles.  Renders
+ * whose grid is exactly tiles_x x tiles_y use it (longest-first dispatch
+ * from a previous frame's per-tile cost); others, and every
+ * render after order = NULL, use row-major order.  The output is the same in
+ * any order.  Waits for the context's renders in flight. */
+int geo_set_tile_order(geo_ctx* ctx, uint32_t tiles_x, uint32_t tiles_y, const uint32_t* order);
+
 /* Adds the steps accumulated under GEO_FLAG_DEFER_STEPS to *steps_total
  * (device u64) and clears the context's counter.  Asynchronous on `stream`. */
 int geo_steps_flush(geo_ctx* ctx, unsigned long long* steps_total, void* stream);

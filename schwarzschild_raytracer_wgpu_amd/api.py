@@ -147,6 +147,18 @@ class Context:
                                                          out.ctypes.data if host else None, _stream_handle(stream)))
         return out
 
+    def set_tile_order(self, tiles_x: int, tiles_y: int, order=None) -> None:
+        """geo_set_tile_order: workgroup dispatch order (packed y << 16 | x per
+        tile, a permutation of the grid) for renders of a tiles_x x tiles_y grid;
+        order=None restores row-major."""
+        if order is None:
+            check("geo_set_tile_order", lib.geo_set_tile_order(self._h, 0, 0, None))
+            return
+        o = np.ascontiguousarray(order, dtype=np.uint32)
+        if o.size != tiles_x * tiles_y:
+            raise ValueError("order must hold tiles_x * tiles_y tiles")
+        check("geo_set_tile_order", lib.geo_set_tile_order(self._h, tiles_x, tiles_y, o.ctypes.data))
+
     def steps_flush(self, steps_total, stream=None) -> None:
         """geo_steps_flush: add the GEO_FLAG_DEFER_STEPS accumulator to steps_total (device u64)."""
         check("geo_steps_flush", lib.geo_steps_flush(self._h, _ptr(steps_total), _stream_handle(stream)))

@@ -54,6 +54,10 @@ struct geo_ctx {
     hipStream_t render_stream[kRenderStreams];
     hipEvent_t render_done[kRenderStreams];
     int n_render_streams, render_next;
+    // Workgroup dispatch order (geo_set_tile_order) for a tiles_x x tiles_y
+    // grid, packed (y << 16 | x); null = row-major.
+    uint32_t* tile_order;
+    uint32_t tile_order_x, tile_order_y;
 };
 
 // Makes `dev` current for the scope of a C-ABI call, restoring the caller's device.

@@ -66,6 +66,9 @@ struct RenderArgs {
     geo::PixelConsts k;  // frame constants, evaluated once on the host (IEEE f32, same bits)
     uint32_t width, height, row0, nrows;
     uint32_t tile_y0;  // first tile row of this launch (launch_tiles)
+    // dispatch order (geo_set_tile_order): workgroup i draws tile
+    // (order[i] & 0xFFFF, order[i] >> 16); null = row-major
+    const uint32_t* tile_order;
     // local row lr -> row0 + b*band_stride + (lr - b*band_rows), b = lr / band_rows
     // = umulhi(lr, band_magic) (band_rows_magic)
     uint32_t band_rows, band_magic, band_stride;
@@ -252,7 +255,11 @@ __host__ __device__ constexpr uint32_t lane_rows(int mode, bool mips) {
 template <int MODE, int KIND, bool MIPS>
 __global__ __launch_bounds__(kBlock) void geo_render_kernel(const RenderArgs a) {
     constexpr uint32_t LR = lane_rows(MODE, MIPS);
-    const uint2 tile = make_uint2(blockIdx.x, a.tile_y0 + blockIdx.y);
+    uint2 tile = make_uint2(blockIdx.x, a.tile_y0 + blockIdx.y);
+    if (a.tile_order) {
+        const uint32_t t = a.tile_order[blockIdx.y * gridDim.x + blockIdx.x];  // one scalar load
+        tile = make_uint2(t & 0xFFFFu, t >> 16);
+    }
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x) >> 6;
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t px = tile.x * kTileW + (wave % kWavesX) * kWaveW + lane % kWaveW;
@@ -797,6 +804,7 @@ void geo_ctx_destroy(geo_ctx* c) {
     for (int i = 0; i < geo_ctx::kStepCallSets; ++i) (void)hipEventDestroy(c->step_set_free[i]);
     for (int i = 0; i < geo_ctx::kRenderStreams; ++i) (void)hipEventDestroy(c->render_done[i]);
     if (c->step_slots) (void)hipFree(c->step_slots);
+    if (c->tile_order) (void)hipFree(c->tile_order);
     delete c;
 }
 
@@ -1030,6 +1038,9 @@ static int render_impl(geo_ctx* c, const geo_frame* frame, const geo_scene* scen
     a.sky_wf = (float)c->sky_w;
     a.sky_hf = (float)c->sky_h;
     a.sky_total_bytes = c->sky_total_bytes;
+    // a dispatch order set for exactly this tile grid (one launch)
+    a.tile_order = (c->tile_order && c->tile_order_x == tiles_x && c->tile_order_y == tiles_y) ? c->tile_order
+                                                                                                : nullptr;
     const int fb = c->fan_cur;
     a.fan = fb < 0 ? nullptr : c->fan[fb];
     a.n_fan = fb < 0 ? 0u : c->n_fan[fb];
@@ -1183,6 +1194,43 @@ int geo_steps_flush(geo_ctx* c, unsigned long long* steps_total, void* stream) {
     hipExtLaunchKernelGGL(geo_steps_finalize, dim3(1), dim3(kStepSlots), 0, (hipStream_t)stream, nullptr, done, 0,
                           c->step_slots, steps_total);
     return hipGetLastError() == hipSuccess ? GEO_OK : GEO_EHIP;
+}
+
+int geo_set_tile_order(geo_ctx* c, uint32_t tiles_x, uint32_t tiles_y, const uint32_t* order) {
+    if (!c) return GEO_EINVAL;
+    DeviceGuard g(c->device);
+    if (!g.ok) return GEO_EHIP;
+    if (!order) {  // back to row-major
+        if (wait_renders(c) != GEO_OK) return GEO_EHIP;
+        if (c->tile_order) (void)hipFree(c->tile_order);
+        c->tile_order = nullptr;
+        c->tile_order_x = c->tile_order_y = 0;
+        return GEO_OK;
+    }
+    if (tiles_x == 0 || tiles_y == 0 || tiles_x > 0xFFFFu || tiles_y > kMaxGridY) return GEO_EINVAL;
+    const size_t n = (size_t)tiles_x * tiles_y;
+    std::vector<uint8_t> seen(n, 0);  // a permutation of the grid's tiles
+    for (size_t i = 0; i < n; ++i) {
+        const uint32_t x = order[i] & 0xFFFFu, y = order[i] >> 16;
+        if (x >= tiles_x || y >= tiles_y || seen[(size_t)y * tiles_x + x]) return GEO_EINVAL;
+        seen[(size_t)y * tiles_x + x] = 1;
+    }
+    if (wait_renders(c) != GEO_OK) return GEO_EHIP;  // renders in flight may read the old order
+    if (c->tile_order) (void)hipFree(c->tile_order);
+    c->tile_order = nullptr;
+    c->tile_order_x = c->tile_order_y = 0;
+    if (hipMalloc(&c->tile_order, n * sizeof(uint32_t)) != hipSuccess) {
+        c->tile_order = nullptr;
+        return GEO_ENOMEM;
+    }
+    if (hipMemcpy(c->tile_order, order, n * sizeof(uint32_t), hipMemcpyHostToDevice) != hipSuccess) {
+        (void)hipFree(c->tile_order);
+        c->tile_order = nullptr;
+        return GEO_EHIP;
+    }
+    c->tile_order_x = tiles_x;
+    c->tile_order_y = tiles_y;
+    return GEO_OK;
 }
 
 int geo_render_rows(geo_ctx* c, const geo_frame* frame, const geo_scene* scene, uint32_t width,

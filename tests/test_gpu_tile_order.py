@@ -1,0 +1,73 @@
+"""geo_set_tile_order: the workgroup dispatch order changes when tiles run,
+never what they draw.  A random permutation of the tile grid renders the
+same frame byte for byte (direct, fan and adaptive mode, ragged frames); a
+render of another grid ignores the order; invalid orders are rejected."""
+import numpy as np
+import pytest
+import torch
+
+from helpers import default_frame, default_scene
+from schwarzschild_raytracer_wgpu_amd import Context, GeoError, make_scene
+from schwarzschild_raytracer_wgpu_amd._lib import GEO_MODE_ADAPTIVE, GEO_MODE_FAN
+from schwarzschild_raytracer_wgpu_amd.scenes import make_sky
+
+pytestmark = pytest.mark.gpu
+
+
+def _grid(w, h, fan=False):
+    return (w + 31) // 32, (h + (16 if fan else 8) - 1) // (16 if fan else 8)
+
+
+@pytest.mark.parametrize("mode", ["direct", "fan", "adaptive"])
+def test_any_order_same_frame(dev, mode):
+    w, h = 200, 117  # ragged in both tile dimensions
+    frame = default_frame(w, h)
+    base = default_scene(2048)
+    scene = base
+    if mode == "adaptive":
+        scene = make_scene(base.rs, base.sphere_r, base.r_obs, base.step, base.max_steps, GEO_MODE_ADAPTIVE)
+    if mode == "fan":
+        scene = make_scene(base.rs, base.sphere_r, base.r_obs, base.step, base.max_steps, GEO_MODE_FAN)
+    ctx = Context(0)
+    ctx.set_sky(make_sky("equirect", (256, 128)))
+    if mode == "fan":
+        ctx.solve_ray_fan(50.0, 1.0, 2048, base.step, 400, base.r_obs)
+    outs = []
+    tx, ty = _grid(w, h, mode == "fan")
+    rng = np.random.default_rng(11)
+    packed = (np.arange(ty)[:, None] << 16 | np.arange(tx)[None, :]).astype(np.uint32).ravel()
+    for order in (None, rng.permutation(packed), packed[::-1].copy()):
+        ctx.set_tile_order(tx, ty, order)
+        rgba = torch.zeros(h * w * 4, dtype=torch.uint8, device=dev)
+        steps = torch.zeros(h * w, dtype=torch.int32, device=dev)
+        tot = torch.zeros(1, dtype=torch.int64, device=dev)
+        ctx.render_rows(frame, scene, w, h, 0, h, rgba, out_steps=steps, steps_total=tot)
+        torch.cuda.synchronize()
+        outs.append((rgba.cpu(), steps.cpu(), int(tot.item())))
+    for o in outs[1:]:
+        assert torch.equal(o[0], outs[0][0]) and torch.equal(o[1], outs[0][1]) and o[2] == outs[0][2]
+    # a render of another grid (fewer rows) ignores the order: still the same rows
+    ctx.set_tile_order(tx, ty, rng.permutation(packed))
+    part = torch.zeros(64 * w * 4, dtype=torch.uint8, device=dev)
+    ctx.render_rows(frame, scene, w, h, 16, 64, part)
+    torch.cuda.synchronize()
+    assert torch.equal(part.cpu(), outs[0][0][16 * w * 4:80 * w * 4])
+    ctx.close()
+
+
+def test_invalid_orders_rejected(dev):
+    ctx = Context(0)
+    tx, ty = 3, 2
+    packed = (np.arange(ty)[:, None] << 16 | np.arange(tx)[None, :]).astype(np.uint32).ravel()
+    bad_dup = packed.copy()
+    bad_dup[1] = bad_dup[0]
+    bad_range = packed.copy()
+    bad_range[0] = (5 << 16) | 0
+    for bad in (bad_dup, bad_range):
+        with pytest.raises(GeoError):
+            ctx.set_tile_order(tx, ty, bad)
+    with pytest.raises(ValueError):
+        ctx.set_tile_order(tx, ty, packed[:-1])
+    ctx.set_tile_order(tx, ty, packed)
+    ctx.set_tile_order(tx, ty, None)
+    ctx.close()

@@ -11,7 +11,7 @@ TAG=${1:-r04a}
 step() { echo "== $*"; }
 
 step pytest
-timeout -k 10 400 python -u -m pytest tests/test_gpu_cpu_path.py tests/test_bench.py -x -v --timeout 200 \
+GEO_F64_BAR_OUT="$OUT/f64bar_$TAG" timeout -k 10 600 python -u -m pytest tests/test_gpu_cpu_path.py tests/test_gpu_f64_bar.py tests/test_bench.py -x -v --timeout 300 \
     --timeout-method thread > "$OUT/pytest_$TAG.log" 2>&1 || { tail -30 "$OUT/pytest_$TAG.log"; exit 1; }
 tail -3 "$OUT/pytest_$TAG.log"
 

@@ -241,14 +241,31 @@ int geo_assemble_lead(geo_ctx* ctx, const uint8_t* lead_src, size_t lead_frame_s
  * bytes on the links for the multi-GPU present.  Asynchronous on `stream`. */
 int geo_pack_rgb(geo_ctx* ctx, const uint8_t* rgba, uint64_t npixels, uint8_t* rgb, void* stream);
 
-/* The workgroup dispatch order of this context's renders: workgroup i draws
- * tile (order[i] & 0xFFFF, order[i] >> 16) of a tiles_x x tiles_y grid of
- * 32 x 8-pixel tiles (32 x 16 in fan mode with the level-0 sampler) over the
- * rendered rows; order must be a permutation of the grid's tiles.  Renders
- * whose grid is exactly tiles_x x tiles_y use it (longest-first dispatch
- * from a previous frame's per-tile cost); others, and every
- * render after order = NULL, use row-major order.  The output is the same in
- * any order.  Waits for the context's renders in flight. */
+/* The workgroup dispatch order of this context's renders.
+ * A frame's tiles differ ~30x in cost (steps per pixel peak at the photon
+ * ring), and the hardware dispatches workgroups in launch order, so a long
+ * tile dispatched late stretches the kernel's tail.
+ *   GEO_DISPATCH_LONGEST_FIRST (the default): every period-th render of a grid
+ *     (same width, height, rows, bands, mode and sampler) records each 32 x 8
+ *     tile's cost on the device, and two small kernels after it build the
+ *     order, most expensive tile first, for the renders that follow; the
+ *     first render of a new grid records and uses row-major order.  Nothing
+ *     is read back to the host.
+ *   GEO_DISPATCH_ROW_MAJOR: the launch order.
+ * Fan-mode renders (uniform cost) and frames of more than 65 535 tile rows
+ * always use row-major order.  The output is the same in any order.
+ * period: 1 .. 2^20 (default 16). */
+#define GEO_DISPATCH_ROW_MAJOR 0
+#define GEO_DISPATCH_LONGEST_FIRST 1
+#define GEO_DISPATCH_EXPLICIT 2 /* set by geo_set_tile_order */
+int geo_set_dispatch(geo_ctx* ctx, int mode, uint32_t period);
+
+/* An explicit dispatch order (GEO_DISPATCH_EXPLICIT): workgroup i draws tile
+ * (order[i] & 0xFFFF, order[i] >> 16) of a tiles_x x tiles_y grid of
+ * 32 x 8-pixel tiles over the rendered rows; order (host) must be a
+ * permutation of the grid's tiles.  Renders whose grid is exactly
+ * tiles_x x tiles_y use it, others row-major order.  order = NULL selects
+ * GEO_DISPATCH_ROW_MAJOR.  Waits for the context's renders in flight. */
 int geo_set_tile_order(geo_ctx* ctx, uint32_t tiles_x, uint32_t tiles_y, const uint32_t* order);
 
 /* Adds the steps accumulated under GEO_FLAG_DEFER_STEPS to *steps_total

@@ -22,6 +22,9 @@ GEO_MODE_DIRECT = 0
 GEO_MODE_FAN = 1
 GEO_MODE_ADAPTIVE = 2
 GEO_ADAPTIVE_DEFAULT_TOL = 1e-6
+GEO_DISPATCH_ROW_MAJOR = 0
+GEO_DISPATCH_LONGEST_FIRST = 1
+GEO_DISPATCH_EXPLICIT = 2
 GEO_ADAPTIVE_MAX_GROWTH = 16
 GEO_FLAG_DEFER_STEPS = 1
 GEO_FLAG_COMPOSITE = 2
@@ -95,6 +98,7 @@ SIGNATURES = {
     ),
     "geo_steps_flush": (_int, [_vp, _vp, _vp]),
     "geo_set_tile_order": (_int, [_vp, _u32, _u32, _vp]),
+    "geo_set_dispatch": (_int, [_vp, _int, _u32]),
     "geo_assemble_bands": (_int, [_vp, _vp, ctypes.c_size_t, ctypes.c_size_t, _u32, _u32, _u32, _u32, _u32, _u32,
                                   _vp, _vp]),
     "geo_assemble_lead": (_int, [_vp, _vp, ctypes.c_size_t, _u32, _vp, ctypes.c_size_t, ctypes.c_size_t, _u32, _u32,

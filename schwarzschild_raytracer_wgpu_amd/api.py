@@ -147,6 +147,12 @@ class Context:
                                                          out.ctypes.data if host else None, _stream_handle(stream)))
         return out
 
+    def set_dispatch(self, mode: int, period: int = 16) -> None:
+        """geo_set_dispatch: GEO_DISPATCH_LONGEST_FIRST (default; the order is
+        re-learned on the device every `period` renders of a grid) or
+        GEO_DISPATCH_ROW_MAJOR."""
+        check("geo_set_dispatch", lib.geo_set_dispatch(self._h, mode, period))
+
     def set_tile_order(self, tiles_x: int, tiles_y: int, order=None) -> None:
         """geo_set_tile_order: workgroup dispatch order (packed y << 16 | x per
         tile, a permutation of the grid) for renders of a tiles_x x tiles_y grid;

@@ -54,10 +54,31 @@ struct geo_ctx {
     hipStream_t render_stream[kRenderStreams];
     hipEvent_t render_done[kRenderStreams];
     int n_render_streams, render_next;
-    // Workgroup dispatch order (geo_set_tile_order) for a tiles_x x tiles_y
-    // grid, packed (y << 16 | x); null = row-major.
-    uint32_t* tile_order;
-    uint32_t tile_order_x, tile_order_y;
+    // Workgroup dispatch order ("Longest-first dispatch").
+    // GEO_DISPATCH_LONGEST_FIRST: every `dispatch_period`-th render of a grid
+    // records each tile's cost (its waves' largest step counts, atomically
+    // added into tile_cost) and two small kernels after it rebuild the order
+    // from those costs, most expensive tile first, into the order buffer the
+    // current one is not in; later renders of the same grid (learn_key)
+    // dispatch in that order.  The rebuild waits, on the device, for every
+    // render of the context issued before it (render_done), so no render still
+    // reads the buffer it overwrites; a render on another stream waits once
+    // for the rebuild (order_written, order_epoch vs stream_epoch).
+    // GEO_DISPATCH_EXPLICIT: geo_set_tile_order's order for its grid.
+    // Orders are packed (y << 16 | x) per workgroup.
+    int dispatch_mode;
+    uint32_t dispatch_period, since_learn;
+    uint32_t learn_key[9];
+    bool learn_valid;   // learn_key names a grid
+    int order_cur;      // order[order_cur] is the grid's order (-1: none yet)
+    uint32_t* order[2];
+    uint32_t* tile_cost;  // per tile of the learned grid; zero between rebuilds
+    uint32_t* class_hist;
+    uint32_t tile_cap;    // tiles the buffers hold
+    uint32_t explicit_x, explicit_y;  // GEO_DISPATCH_EXPLICIT's grid
+    hipEvent_t order_written;
+    uint32_t order_epoch;
+    uint32_t stream_epoch[kRenderStreams];
 };
 
 // Makes `dev` current for the scope of a C-ABI call, restoring the caller's device.

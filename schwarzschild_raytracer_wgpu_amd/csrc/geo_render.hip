@@ -56,6 +56,11 @@ static_assert(kTileH % kWaveRows == 0 && kBlock % 64 == 0, "tile of whole waves"
 constexpr uint32_t kBandRowAlign = 8;
 static_assert(kBandRowAlign % kWaveRows == 0, "a wave's rows lie in one band");
 constexpr uint32_t kMaxFan = 4096;       // fan nodes (16 KiB)
+constexpr uint32_t kDefaultDispatchPeriod = 16;  // renders of a grid per re-learned order
+// a tile's out-of-loop work in steps of its mode's loop (the set-up, Newton
+// crossing and sky epilogue: ~330 VALU against 14 per RK4 step, ~420 against
+// ~57 per RK5(4) attempt), added to each wave's recorded cost
+constexpr uint32_t kCostOverheadDirect = 24, kCostOverheadAdaptive = 8;
 constexpr int kStepSlots = 256;          // sharded step counters (one per 128-B line)
 constexpr int kSlotStride = 16;          // u64 per slot = 128 B (own cache line)
 constexpr size_t kSlotSetU64 = (size_t)kStepSlots * kSlotStride;  // one set of sharded counters
@@ -66,9 +71,13 @@ struct RenderArgs {
     geo::PixelConsts k;  // frame constants, evaluated once on the host (IEEE f32, same bits)
     uint32_t width, height, row0, nrows;
     uint32_t tile_y0;  // first tile row of this launch (launch_tiles)
-    // dispatch order (geo_set_tile_order): workgroup i draws tile
+    // dispatch order (geo_ctx): workgroup i draws tile
     // (order[i] & 0xFFFF, order[i] >> 16); null = row-major
     const uint32_t* tile_order;
+    // a cost-recording render: each wave adds its largest step count plus
+    // cost_overhead (its out-of-loop work, in steps) into its tile's entry
+    unsigned int* tile_cost;
+    uint32_t cost_overhead;
     // local row lr -> row0 + b*band_stride + (lr - b*band_rows), b = lr / band_rows
     // = umulhi(lr, band_magic) (band_rows_magic)
     uint32_t band_rows, band_magic, band_stride;
@@ -97,6 +106,17 @@ struct RenderArgs {
 
 // MODE: GEO_MODE_DIRECT / GEO_MODE_FAN / GEO_MODE_ADAPTIVE; KIND: geo::kCurvedOut/kCurvedIn/kFlat
 // (frame-uniform integration kind, geo::geodesic_kind; ignored in fan mode).
+// Max of v over the 64 lanes of a fully active wave (the same DPP scan).
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false));
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+
 // Sum of v over the 64 lanes of a fully active wave (DPP inclusive scan:
 // row_shr 1/2/4/8 within rows of 16, then row_bcast 15/31; lane 63 holds it).
 __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
@@ -374,6 +394,70 @@ __global__ __launch_bounds__(kBlock) void geo_render_kernel(const RenderArgs a) 
             if ((threadIdx.x & 63) == 0 && total)
                 atomicAdd(&a.step_slots[slot * kSlotStride], (unsigned long long)total);
         }
+        if (a.tile_cost) {
+            // a wave holds its slot until its slowest lane stops: the tile's
+            // cost is the sum of its waves' largest step counts
+            const uint32_t wmax = wave_max_u32(steps);
+            if ((threadIdx.x & 63) == 0)
+                atomicAdd(&a.tile_cost[tile.y * gridDim.x + tile.x], wmax + a.cost_overhead);
+        }
+    }
+}
+
+// ---- longest-first dispatch: the order from recorded tile costs ---------
+// Cost classes of half an octave, class(c) = floor(2 log2 c) (0 for c = 0),
+// dispatched from the highest class down; within a class, tile order.  Two
+// kernels: per-chunk class histograms, then each chunk's tiles scattered to
+// their positions (and their costs cleared for the next recording).
+constexpr int kCostClasses = 64;
+constexpr uint32_t kOrderChunk = 1024;  // tiles per workgroup
+
+__device__ __forceinline__ uint32_t cost_class(uint32_t c) {
+    if (c == 0u) return 0u;
+    const uint32_t o = 31u - (uint32_t)__clz(c);
+    const uint32_t half = (uint64_t)c * c >= (1ull << (2u * o + 1u)) ? 1u : 0u;  // c >= 2^o sqrt 2
+    const uint32_t k = 2u * o + half;
+    return k < (uint32_t)kCostClasses ? k : (uint32_t)kCostClasses - 1u;
+}
+
+__global__ __launch_bounds__(256) void geo_order_hist(const uint32_t* __restrict__ cost, uint32_t n,
+                                                      uint32_t* __restrict__ hist) {
+    __shared__ uint32_t h[kCostClasses];
+    if (threadIdx.x < kCostClasses) h[threadIdx.x] = 0u;
+    __syncthreads();
+    const uint32_t lo = blockIdx.x * kOrderChunk, hi = min(n, lo + kOrderChunk);
+    for (uint32_t i = lo + threadIdx.x; i < hi; i += 256u) atomicAdd(&h[cost_class(cost[i])], 1u);
+    __syncthreads();
+    if (threadIdx.x < kCostClasses) hist[blockIdx.x * kCostClasses + threadIdx.x] = h[threadIdx.x];
+}
+
+__global__ __launch_bounds__(256) void geo_order_scatter(uint32_t* __restrict__ cost, uint32_t n,
+                                                         const uint32_t* __restrict__ hist, uint32_t tiles_x,
+                                                         uint32_t* __restrict__ order) {
+    __shared__ uint32_t tot[kCostClasses], base[kCostClasses];
+    const uint32_t c = threadIdx.x;
+    if (c < kCostClasses) {
+        uint32_t t = 0u, mine = 0u;
+        for (uint32_t g = 0; g < gridDim.x; ++g) {
+            const uint32_t v = hist[g * kCostClasses + c];
+            t += v;
+            if (g < blockIdx.x) mine += v;
+        }
+        tot[c] = t;
+        base[c] = mine;
+    }
+    __syncthreads();
+    if (c < kCostClasses) {
+        uint32_t above = 0u;  // tiles of the higher classes, dispatched first
+        for (uint32_t k = c + 1u; k < (uint32_t)kCostClasses; ++k) above += tot[k];
+        base[c] += above;
+    }
+    __syncthreads();
+    const uint32_t lo = blockIdx.x * kOrderChunk, hi = min(n, lo + kOrderChunk);
+    for (uint32_t i = lo + threadIdx.x; i < hi; i += 256u) {
+        const uint32_t pos = atomicAdd(&base[cost_class(cost[i])], 1u);
+        order[pos] = ((i / tiles_x) << 16) | (i % tiles_x);
+        cost[i] = 0u;
     }
 }
 
@@ -722,6 +806,10 @@ int geo_ctx_create(int device, geo_ctx** out) {
         ok = hipEventCreateWithFlags(&c->step_set_free[i], kCtxEventFlags) == hipSuccess;
     for (int i = 0; i < geo_ctx::kRenderStreams && ok; ++i)
         ok = hipEventCreateWithFlags(&c->render_done[i], kCtxEventFlags) == hipSuccess;
+    if (ok) ok = hipEventCreateWithFlags(&c->order_written, kCtxEventFlags) == hipSuccess;
+    c->dispatch_mode = GEO_DISPATCH_LONGEST_FIRST;
+    c->dispatch_period = kDefaultDispatchPeriod;
+    c->order_cur = -1;
     int st = ok ? GEO_OK : GEO_EHIP;
     if (ok && hipMalloc(&c->step_slots, sizeof(unsigned long long) * kSlotSetU64 * kSlotSets) != hipSuccess) {
         c->step_slots = nullptr;
@@ -740,6 +828,7 @@ int geo_ctx_create(int device, geo_ctx** out) {
             if (c->step_set_free[i]) (void)hipEventDestroy(c->step_set_free[i]);
         for (int i = 0; i < geo_ctx::kRenderStreams; ++i)
             if (c->render_done[i]) (void)hipEventDestroy(c->render_done[i]);
+        if (c->order_written) (void)hipEventDestroy(c->order_written);
         delete c;
         return st;
     }
@@ -763,27 +852,36 @@ static int wait_fan(geo_ctx* c, int b) {
     return GEO_OK;
 }
 
-// The event that tracks the context's work on stream s (geo_ctx::render_done):
-// the caller's next kernel on s records it as its stop event
-// (hipExtLaunchKernelGGL), which rides on the dispatch's own completion
+// The slot whose event tracks the context's work on stream s
+// (geo_ctx::render_done): the caller's next kernel on s records it as its stop
+// event (hipExtLaunchKernelGGL), which rides on the dispatch's own completion
 // signal instead of a marker packet after it (a marker per frame cost ~1 % of
-// the event-timed 4K kernel).  Null on a HIP error.
-static hipEvent_t render_event(geo_ctx* c, hipStream_t s) {
+// the event-timed 4K kernel).  With every slot taken, the least recently
+// claimed one is evicted after a HOST wait for its event (a
+// device-side wait would tie the caller's stream to an unrelated stream's
+// work, which may sit behind a collective); that wait is the only blocking
+// step, and only a context rendering on more than kRenderStreams streams
+// reaches it.  -1 on a HIP error.
+static int render_slot(geo_ctx* c, hipStream_t s) {
     int i = 0;
     while (i < c->n_render_streams && c->render_stream[i] != s) ++i;
     if (i == c->n_render_streams) {
         if (c->n_render_streams < geo_ctx::kRenderStreams) {
             ++c->n_render_streams;
         } else {
-            // evict a slot: s first waits for its event, so the event s
-            // records next covers the evicted stream's last render as well
             i = c->render_next;
             c->render_next = (i + 1) % geo_ctx::kRenderStreams;
-            if (hipStreamWaitEvent(s, c->render_done[i], 0) != hipSuccess) return nullptr;
+            if (hipEventSynchronize(c->render_done[i]) != hipSuccess) return -1;
         }
         c->render_stream[i] = s;
+        c->stream_epoch[i] = 0;  // has not waited for any order rebuild
     }
-    return c->render_done[i];
+    return i;
+}
+
+static hipEvent_t render_event(geo_ctx* c, hipStream_t s) {
+    const int i = render_slot(c, s);
+    return i < 0 ? nullptr : c->render_done[i];
 }
 
 void geo_ctx_destroy(geo_ctx* c) {
@@ -804,7 +902,12 @@ void geo_ctx_destroy(geo_ctx* c) {
     for (int i = 0; i < geo_ctx::kStepCallSets; ++i) (void)hipEventDestroy(c->step_set_free[i]);
     for (int i = 0; i < geo_ctx::kRenderStreams; ++i) (void)hipEventDestroy(c->render_done[i]);
     if (c->step_slots) (void)hipFree(c->step_slots);
-    if (c->tile_order) (void)hipFree(c->tile_order);
+    if (c->learn_valid || c->tile_cap) (void)hipEventSynchronize(c->order_written);
+    for (int b = 0; b < 2; ++b)
+        if (c->order[b]) (void)hipFree(c->order[b]);
+    if (c->tile_cost) (void)hipFree(c->tile_cost);
+    if (c->class_hist) (void)hipFree(c->class_hist);
+    (void)hipEventDestroy(c->order_written);
     delete c;
 }
 
@@ -981,6 +1084,39 @@ static int launch_tiles(RenderArgs a, bool mips, uint32_t tiles_x, uint32_t tile
 }
 }
 
+// The order buffers hold at least n tiles (both orders, the costs, the class
+// histograms).  Growing them waits for the context's renders and rebuilds,
+// and forgets the learned order.
+static int ensure_tiles(geo_ctx* c, uint32_t n) {
+    if (c->tile_cap >= n) return GEO_OK;
+    if (wait_renders(c) != GEO_OK || hipEventSynchronize(c->order_written) != hipSuccess) return GEO_EHIP;
+    for (int b = 0; b < 2; ++b) {
+        if (c->order[b]) (void)hipFree(c->order[b]);
+        c->order[b] = nullptr;
+    }
+    if (c->tile_cost) (void)hipFree(c->tile_cost);
+    if (c->class_hist) (void)hipFree(c->class_hist);
+    c->tile_cost = c->class_hist = nullptr;
+    c->tile_cap = 0;
+    c->order_cur = -1;
+    c->learn_valid = false;
+    const size_t chunks = (n + kOrderChunk - 1) / kOrderChunk;
+    if (hipMalloc(&c->order[0], n * sizeof(uint32_t)) != hipSuccess ||
+        hipMalloc(&c->order[1], n * sizeof(uint32_t)) != hipSuccess ||
+        hipMalloc(&c->tile_cost, n * sizeof(uint32_t)) != hipSuccess ||
+        hipMalloc(&c->class_hist, chunks * kCostClasses * sizeof(uint32_t)) != hipSuccess) {
+        for (int b = 0; b < 2; ++b)
+            if (c->order[b]) (void)hipFree(c->order[b]);
+        if (c->tile_cost) (void)hipFree(c->tile_cost);
+        if (c->class_hist) (void)hipFree(c->class_hist);
+        c->order[0] = c->order[1] = c->tile_cost = c->class_hist = nullptr;
+        return GEO_ENOMEM;
+    }
+    if (hipMemset(c->tile_cost, 0, n * sizeof(uint32_t)) != hipSuccess) return GEO_EHIP;
+    c->tile_cap = n;
+    return GEO_OK;
+}
+
 static int render_impl(geo_ctx* c, const geo_frame* frame, const geo_scene* scene, uint32_t width,
                        uint32_t height, uint32_t row0, uint32_t nrows, uint32_t band_rows,
                        uint32_t band_stride, uint8_t* out_rgba8, uint8_t* out_mask, float* out_uv,
@@ -1038,9 +1174,9 @@ static int render_impl(geo_ctx* c, const geo_frame* frame, const geo_scene* scen
     a.sky_wf = (float)c->sky_w;
     a.sky_hf = (float)c->sky_h;
     a.sky_total_bytes = c->sky_total_bytes;
-    // a dispatch order set for exactly this tile grid (one launch)
-    a.tile_order = (c->tile_order && c->tile_order_x == tiles_x && c->tile_order_y == tiles_y) ? c->tile_order
-                                                                                                : nullptr;
+    a.tile_order = nullptr;
+    a.tile_cost = nullptr;
+    a.cost_overhead = adaptive ? kCostOverheadAdaptive : kCostOverheadDirect;
     const int fb = c->fan_cur;
     a.fan = fb < 0 ? nullptr : c->fan[fb];
     a.n_fan = fb < 0 ? 0u : c->n_fan[fb];
@@ -1060,8 +1196,45 @@ static int render_impl(geo_ctx* c, const geo_frame* frame, const geo_scene* scen
             return GEO_EHIP;
         a.step_slots = c->step_slots + (size_t)(1 + call_set) * kSlotSetU64;
     }
-    const hipEvent_t done = render_event(c, s);
-    if (!done) return GEO_EHIP;
+    const int slot = render_slot(c, s);
+    if (slot < 0) return GEO_EHIP;
+    const hipEvent_t done = c->render_done[slot];
+    // The dispatch order (geo_ctx): a learned or explicit order for exactly
+    // this grid, one launch, not in fan mode (its tiles all cost the same).
+    bool record = false;
+    if (scene->mode != GEO_MODE_FAN && tiles_y <= kMaxGridY) {
+        if (c->dispatch_mode == GEO_DISPATCH_EXPLICIT) {
+            if (c->order_cur >= 0 && tiles_x == c->explicit_x && tiles_y == c->explicit_y)
+                a.tile_order = c->order[c->order_cur];
+        } else if (c->dispatch_mode == GEO_DISPATCH_LONGEST_FIRST) {
+            const uint32_t key[9] = {width, height, row0, nrows, band_rows, band_stride, scene->mode, mips ? 1u : 0u,
+                                     tiles_x * tiles_y};
+            if (!c->learn_valid || std::memcmp(key, c->learn_key, sizeof(key)) != 0) {
+                std::memcpy(c->learn_key, key, sizeof(key));
+                c->learn_valid = true;
+                c->order_cur = -1;
+                c->since_learn = c->dispatch_period;
+            }
+            record = c->since_learn >= c->dispatch_period;
+            c->since_learn = record ? 0u : c->since_learn + 1u;
+            if (record) {
+                int est = ensure_tiles(c, tiles_x * tiles_y);
+                if (est) return est;
+                if (!c->learn_valid) {  // the growth forgot the key: this render learns it again
+                    std::memcpy(c->learn_key, key, sizeof(key));
+                    c->learn_valid = true;
+                }
+                a.tile_cost = c->tile_cost;
+            }
+            if (c->order_cur >= 0) a.tile_order = c->order[c->order_cur];
+        }
+        // the order and the costs this render reads or adds to were last
+        // written by a rebuild, maybe on another stream
+        if ((a.tile_order || a.tile_cost) && c->stream_epoch[slot] != c->order_epoch) {
+            if (hipStreamWaitEvent(s, c->order_written, 0) != hipSuccess) return GEO_EHIP;
+            c->stream_epoch[slot] = c->order_epoch;
+        }
+    }
     int st;
     if (scene->mode == GEO_MODE_FAN) {
         // after the solve that wrote the buffer; then this render joins the
@@ -1087,6 +1260,23 @@ static int render_impl(geo_ctx* c, const geo_frame* frame, const geo_scene* scen
         }
     }
     if (st) return st;
+    if (record) {
+        // rebuild the order into the buffer not in use, after every render of
+        // the context issued so far (renders on this stream are ordered
+        // already; the others may read that buffer)
+        const int nb = c->order_cur < 0 ? 0 : 1 - c->order_cur;
+        for (int i = 0; i < c->n_render_streams; ++i)
+            if (i != slot && hipStreamWaitEvent(s, c->render_done[i], 0) != hipSuccess) return GEO_EHIP;
+        const uint32_t n = tiles_x * tiles_y;
+        const uint32_t chunks = (n + kOrderChunk - 1) / kOrderChunk;
+        hipLaunchKernelGGL(geo_order_hist, dim3(chunks), dim3(256), 0, s, c->tile_cost, n, c->class_hist);
+        hipLaunchKernelGGL(geo_order_scatter, dim3(chunks), dim3(256), 0, s, c->tile_cost, n, c->class_hist, tiles_x,
+                           c->order[nb]);
+        if (hipGetLastError() != hipSuccess) return GEO_EHIP;
+        if (hipEventRecord(c->order_written, s) != hipSuccess) return GEO_EHIP;
+        c->stream_epoch[slot] = ++c->order_epoch;
+        c->order_cur = nb;
+    }
     if (call_set >= 0) {
         hipLaunchKernelGGL(geo_steps_finalize, dim3(1), dim3(kStepSlots), 0, s, a.step_slots, steps_total);
         if (hipGetLastError() != hipSuccess) return GEO_EHIP;
@@ -1196,40 +1386,49 @@ int geo_steps_flush(geo_ctx* c, unsigned long long* steps_total, void* stream) {
     return hipGetLastError() == hipSuccess ? GEO_OK : GEO_EHIP;
 }
 
+int geo_set_dispatch(geo_ctx* c, int mode, uint32_t period) {
+    if (!c || (mode != GEO_DISPATCH_ROW_MAJOR && mode != GEO_DISPATCH_LONGEST_FIRST) || period == 0 ||
+        period > (1u << 20))
+        return GEO_EINVAL;
+    c->dispatch_mode = mode;
+    c->dispatch_period = period;
+    c->learn_valid = false;  // learn again from the next render
+    c->order_cur = -1;
+    return GEO_OK;
+}
+
 int geo_set_tile_order(geo_ctx* c, uint32_t tiles_x, uint32_t tiles_y, const uint32_t* order) {
     if (!c) return GEO_EINVAL;
     DeviceGuard g(c->device);
     if (!g.ok) return GEO_EHIP;
-    if (!order) {  // back to row-major
-        if (wait_renders(c) != GEO_OK) return GEO_EHIP;
-        if (c->tile_order) (void)hipFree(c->tile_order);
-        c->tile_order = nullptr;
-        c->tile_order_x = c->tile_order_y = 0;
+    if (!order) {  // row-major
+        c->dispatch_mode = GEO_DISPATCH_ROW_MAJOR;
+        c->learn_valid = false;
+        c->order_cur = -1;
         return GEO_OK;
     }
     if (tiles_x == 0 || tiles_y == 0 || tiles_x > 0xFFFFu || tiles_y > kMaxGridY) return GEO_EINVAL;
     const size_t n = (size_t)tiles_x * tiles_y;
+    if (n > 0xFFFFFFFFu) return GEO_EINVAL;
     std::vector<uint8_t> seen(n, 0);  // a permutation of the grid's tiles
     for (size_t i = 0; i < n; ++i) {
         const uint32_t x = order[i] & 0xFFFFu, y = order[i] >> 16;
         if (x >= tiles_x || y >= tiles_y || seen[(size_t)y * tiles_x + x]) return GEO_EINVAL;
         seen[(size_t)y * tiles_x + x] = 1;
     }
-    if (wait_renders(c) != GEO_OK) return GEO_EHIP;  // renders in flight may read the old order
-    if (c->tile_order) (void)hipFree(c->tile_order);
-    c->tile_order = nullptr;
-    c->tile_order_x = c->tile_order_y = 0;
-    if (hipMalloc(&c->tile_order, n * sizeof(uint32_t)) != hipSuccess) {
-        c->tile_order = nullptr;
-        return GEO_ENOMEM;
-    }
-    if (hipMemcpy(c->tile_order, order, n * sizeof(uint32_t), hipMemcpyHostToDevice) != hipSuccess) {
-        (void)hipFree(c->tile_order);
-        c->tile_order = nullptr;
+    int st = ensure_tiles(c, (uint32_t)n);
+    if (st) return st;
+    // renders in flight may read either buffer, a rebuild may write one
+    if (wait_renders(c) != GEO_OK || hipEventSynchronize(c->order_written) != hipSuccess) return GEO_EHIP;
+    if (hipMemcpy(c->order[0], order, n * sizeof(uint32_t), hipMemcpyHostToDevice) != hipSuccess) {
+        c->order_cur = -1;
         return GEO_EHIP;
     }
-    c->tile_order_x = tiles_x;
-    c->tile_order_y = tiles_y;
+    c->dispatch_mode = GEO_DISPATCH_EXPLICIT;
+    c->explicit_x = tiles_x;
+    c->explicit_y = tiles_y;
+    c->order_cur = 0;
+    c->learn_valid = false;
     return GEO_OK;
 }
 

@@ -1,14 +1,18 @@
-"""geo_set_tile_order: the workgroup dispatch order changes when tiles run,
-never what they draw.  A random permutation of the tile grid renders the
-same frame byte for byte (direct, fan and adaptive mode, ragged frames); a
-render of another grid ignores the order; invalid orders are rejected."""
+"""The workgroup dispatch order (geo_set_dispatch, geo_set_tile_order) changes
+when tiles run, never what they draw.  An explicit random permutation of the
+tile grid, and the learned longest-first order (re-learned every render or
+every few, on one stream or alternating between two), render the same frames
+byte for byte as row-major order, step counts included (direct, fan and
+adaptive mode, ragged frames); a render of another grid ignores an explicit
+order; invalid orders and settings are rejected."""
 import numpy as np
 import pytest
 import torch
 
 from helpers import default_frame, default_scene
 from schwarzschild_raytracer_wgpu_amd import Context, GeoError, make_scene
-from schwarzschild_raytracer_wgpu_amd._lib import GEO_MODE_ADAPTIVE, GEO_MODE_FAN
+from schwarzschild_raytracer_wgpu_amd._lib import (GEO_DISPATCH_LONGEST_FIRST, GEO_DISPATCH_ROW_MAJOR, GEO_MODE_ADAPTIVE,
+                                                   GEO_MODE_FAN)
 from schwarzschild_raytracer_wgpu_amd.scenes import make_sky
 
 pytestmark = pytest.mark.gpu
@@ -70,4 +74,52 @@ def test_invalid_orders_rejected(dev):
         ctx.set_tile_order(tx, ty, packed[:-1])
     ctx.set_tile_order(tx, ty, packed)
     ctx.set_tile_order(tx, ty, None)
+    ctx.close()
+
+
+@pytest.mark.parametrize("mode", ["direct", "adaptive"])
+@pytest.mark.parametrize("period", [1, 3])
+def test_learned_order_same_frames(dev, mode, period):
+    w, h = 200, 117
+    frame = default_frame(w, h)
+    base = default_scene(2048)
+    scene = base if mode == "direct" else make_scene(base.rs, base.sphere_r, base.r_obs, base.step, base.max_steps,
+                                                      GEO_MODE_ADAPTIVE)
+    ctx = Context(0)
+    ctx.set_sky(make_sky("equirect", (256, 128)))
+
+    def render(stream=None):
+        rgba = torch.zeros(h * w * 4, dtype=torch.uint8, device=dev)
+        steps = torch.zeros(h * w, dtype=torch.int32, device=dev)
+        tot = torch.zeros(1, dtype=torch.int64, device=dev)
+        ctx.render_rows(frame, scene, w, h, 0, h, rgba, out_steps=steps, steps_total=tot, stream=stream)
+        return rgba, steps, tot
+
+    ctx.set_dispatch(GEO_DISPATCH_ROW_MAJOR)
+    ref = render()
+    torch.cuda.synchronize()
+    ctx.set_dispatch(GEO_DISPATCH_LONGEST_FIRST, period)
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    outs = []
+    for i in range(8):  # learn, use, re-learn; alternating streams after the first four
+        st = None if i < 4 else (s1 if i % 2 else s2)
+        with torch.cuda.stream(st or torch.cuda.current_stream()):
+            outs.append(render(st))
+    # a band render in between (another grid) and back
+    band = torch.zeros(64 * w * 4, dtype=torch.uint8, device=dev)
+    ctx.render_rows(frame, scene, w, h, 16, 64, band)
+    outs.append(render())
+    torch.cuda.synchronize()
+    for o in outs:
+        assert torch.equal(o[0], ref[0]) and torch.equal(o[1], ref[1]) and torch.equal(o[2], ref[2])
+    assert torch.equal(band, ref[0][16 * w * 4:80 * w * 4])
+    ctx.close()
+
+
+def test_dispatch_settings_rejected(dev):
+    ctx = Context(0)
+    for mode, period in [(7, 16), (GEO_DISPATCH_LONGEST_FIRST, 0), (GEO_DISPATCH_LONGEST_FIRST, (1 << 20) + 1)]:
+        with pytest.raises(GeoError):
+            ctx.set_dispatch(mode, period)
+    ctx.set_dispatch(GEO_DISPATCH_LONGEST_FIRST, 1 << 20)
     ctx.close()

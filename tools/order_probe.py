@@ -12,6 +12,9 @@ event pairs around each of N back-to-back launches after a spin-up:
            (block i on XCD i % 8), so XCD k gets the k-th eighth of the tiles
            in row-major order, whose sky lines then meet in one L2
   xcd_lpt  the same regions, each in longest-first order
+  auto     the product default: GEO_DISPATCH_LONGEST_FIRST, the order learned
+           on the device every 16 renders (its recording renders and
+           rebuild kernels inside the timed launches)
   python tools/order_probe.py [cfg2_1080p cfg3_4k cfg3_4k:fan ...]
 """
 import json
@@ -92,23 +95,32 @@ def main():
         packed = (np.arange(ty)[:, None] << 16 | np.arange(tx)[None, :]).astype(np.uint32).ravel()
         by_cost = np.argsort(-cost.ravel(), kind="stable")
         orders = {"natural": None, "xcd": xcd_order(packed)}
+        if not fan:
+            orders["auto"] = "auto"
         if not fan:  # fan-mode pixels have no steps: every tile costs the same
             orders.update(lpt=packed[by_cost], rev=packed[by_cost[::-1]],
                           xcd_lpt=xcd_order(packed, rank=-cost.ravel()))
         n = 400 if W * H <= 1920 * 1080 else 200
         res = {k: [] for k in orders}
+        span = {}
         for rep in range(3):
             for k, o in orders.items():
-                ctx.set_tile_order(tx, ty, o)
+                if isinstance(o, str):
+                    ctx.set_dispatch(g._lib.GEO_DISPATCH_LONGEST_FIRST, 16)
+                else:
+                    ctx.set_tile_order(tx, ty, o)
                 for _ in range(300):  # clock spin-up
                     ctx.render_rows(frame, scene, W, H, 0, H, rgba)
                 evs = [(HipEvent(), HipEvent()) for _ in range(n)]
+                t0 = HipEvent()
+                t0.record()
                 for a, b in evs:
                     a.record()
                     ctx.render_rows(frame, scene, W, H, 0, H, rgba)
                     b.record()
                 torch.cuda.synchronize()
                 res[k].append(statistics.median(a.elapsed_time(b) for a, b in evs))
+                span.setdefault(k, []).append(t0.elapsed_time(evs[-1][1]) / n)
         ctx.set_tile_order(tx, ty, None)
         ref = rgba.clone()
         ctx.render_rows(frame, scene, W, H, 0, H, ref)
@@ -118,6 +130,7 @@ def main():
         same = bool(torch.equal(ref, rgba))
         ctx.close()
         out[spec] = {"median_kernel_ms": {k: [round(v, 5) for v in vs] for k, vs in res.items()},
+                     "mean_frame_ms": {k: [round(v, 5) for v in vs] for k, vs in span.items()},
                      "tiles": int(tx * ty), "lpt_frame_identical": same,
                      "cost_top1pct_share": float(np.sort(cost.ravel())[::-1][: max(1, cost.size // 100)].sum()
                                                  / cost.sum())}

@@ -72,7 +72,10 @@ typedef enum geo_status {
                                    pixels untouched: the 2nd, 3rd... sphere of a frame
                                    (lib.rs:67-89).  Without it a sphere is drawn over the
                                    cleared target (0,0,0,1). */
-#define GEO_FLAG_MIPS 4u        /* sample the sky through its 4-level mip chain, trilinear,
+#define GEO_FLAG_MIPS 4u        /* (parity unpinned: the reference's mip generator and sampler
+                                   are in its absent wgpu_renderer submodule; this is the
+                                   repo's own specification of them)
+                                   sample the sky through its 4-level mip chain, trilinear,
                                    with the level of detail from the UV differences across
                                    each 2x2 pixel quad, as textureSample does
                                    (basic_sphere_buffer.rs:31-36, shader.wgsl:101; the

@@ -272,6 +272,66 @@ __host__ __device__ constexpr uint32_t lane_rows(int mode, bool mips) {
     return mode == GEO_MODE_FAN && !mips ? 2u : 1u;
 }
 
+// The fan-mode draw of one 32 x 16 tile, two pixels per lane (lane_rows):
+// both pixels' rays, then both fan lerps (four loads in flight), then both
+// epilogues.
+__device__ __forceinline__ void fan_tile(const RenderArgs& a, uint2 tile, uint32_t wave, uint32_t lane) {
+    constexpr uint32_t LR = 2;
+    const uint32_t px = tile.x * kTileW + (wave % kWavesX) * kWaveW + lane % kWaveW;
+    const uint32_t wl0 = tile.y * (kTileH * LR) + (wave / kWavesX) * (kWaveRows * LR);
+    const uint32_t ly = wl0 + lane / kWaveW;
+    const uint32_t band = __umulhi(wl0, a.band_magic);
+    const uint32_t py = a.row0 + band * a.band_stride + (wl0 - band * a.band_rows) + (ly - wl0);
+    float c2x[2], c2y[2], st[2], ct[2], rct[2], lam[2];
+#pragma unroll
+    for (uint32_t k = 0; k < 2; ++k) {
+        float c2z;
+        geo::pixel_central_dir(a.cam, a.frame.movement_to_central, a.frame.psi_factor_and_position[0], a.kt, px,
+                               py + k * kWaveRows, &c2x[k], &c2y[k], &c2z);
+        st[k] = geo::central_sin(c2z);
+        ct[k] = geo::central_rho(c2x[k], c2y[k]);
+        rct[k] = geo::rcpf_(ct[k]);
+    }
+    geo::FanPos fp[2];
+#pragma unroll
+    for (uint32_t k = 0; k < 2; ++k) fp[k] = geo::fan_pos(a.n_fan, st[k]);
+#pragma unroll
+    for (uint32_t k = 0; k < 2; ++k) lam[k] = geo::fan_at(a.fan, fp[k]);
+    bool in[2];
+#pragma unroll
+    for (uint32_t k = 0; k < 2; ++k)
+        in[k] = px < a.width && ly + k * kWaveRows < a.nrows && py + k * kWaveRows < a.height;
+    const bool bh0 = lam[0] < geo::kBlackHoleLambda, bh1 = lam[1] < geo::kBlackHoleLambda;
+    if (!a.composite && !a.out_uv && !a.out_mask && !a.out_steps) {
+        // the plain draw: both UVs, then both texel quads (eight loads in
+        // flight), then both stores; a wave with no sky pixel stores the
+        // clear colour only
+        uint32_t rgba[2] = {geo::kBlackRGBA, geo::kBlackRGBA};
+        if (geo::ballot_(!(bh0 && bh1)) != 0) {
+            float U[2], V[2];
+#pragma unroll
+            for (uint32_t k = 0; k < 2; ++k)
+                geo::sky_uv(a.frame.central_to_uv, c2x[k], c2y[k], ct[k], rct[k], lam[k], &U[k], &V[k]);
+            const PaddedSkyQuad quad{__builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(a.sky), 0,
+                                                                       (int)a.sky_bytes, kBufferRsrcWord3),
+                                     a.sky_pitch_b};
+            uint32_t smp[2];
+#pragma unroll
+            for (uint32_t k = 0; k < 2; ++k) smp[k] = geo::sample_sky_quad_f(quad, a.sky_w256, a.sky_h256, U[k], V[k]);
+            rgba[0] = bh0 ? geo::kBlackRGBA : geo::over_clear(smp[0], a.sky_opaque != 0);
+            rgba[1] = bh1 ? geo::kBlackRGBA : geo::over_clear(smp[1], a.sky_opaque != 0);
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < 2; ++k)
+            if (in[k]) a.out_rgba[(size_t)(ly + k * kWaveRows) * a.width + px] = rgba[k];
+    } else {
+#pragma unroll
+        for (uint32_t k = 0; k < 2; ++k)
+            if (in[k])
+                shade_pixel(a, c2x[k], c2y[k], ct[k], rct[k], lam[k], 0u, (size_t)(ly + k * kWaveRows) * a.width + px);
+    }
+}
+
 template <int MODE, int KIND, bool MIPS>
 __global__ __launch_bounds__(kBlock) void geo_render_kernel(const RenderArgs a) {
     constexpr uint32_t LR = lane_rows(MODE, MIPS);
@@ -294,56 +354,7 @@ __global__ __launch_bounds__(kBlock) void geo_render_kernel(const RenderArgs a) 
     uint32_t steps = 0;
     const bool in_frame = px < a.width && ly < a.nrows && py < a.height;
     if constexpr (LR == 2) {
-        // both pixels' rays, then both fan lerps (four loads in flight), then
-        // both epilogues
-        float c2x[2], c2y[2], st[2], ct[2], rct[2], lam[2];
-#pragma unroll
-        for (uint32_t k = 0; k < 2; ++k) {
-            float c2z;
-            geo::pixel_central_dir(a.cam, a.frame.movement_to_central, a.frame.psi_factor_and_position[0], a.kt, px,
-                                   py + k * kWaveRows, &c2x[k], &c2y[k], &c2z);
-            st[k] = geo::central_sin(c2z);
-            ct[k] = geo::central_rho(c2x[k], c2y[k]);
-            rct[k] = geo::rcpf_(ct[k]);
-        }
-        geo::FanPos fp[2];
-#pragma unroll
-        for (uint32_t k = 0; k < 2; ++k) fp[k] = geo::fan_pos(a.n_fan, st[k]);
-#pragma unroll
-        for (uint32_t k = 0; k < 2; ++k) lam[k] = geo::fan_at(a.fan, fp[k]);
-        bool in[2];
-#pragma unroll
-        for (uint32_t k = 0; k < 2; ++k)
-            in[k] = px < a.width && ly + k * kWaveRows < a.nrows && py + k * kWaveRows < a.height;
-        const bool bh0 = lam[0] < geo::kBlackHoleLambda, bh1 = lam[1] < geo::kBlackHoleLambda;
-        if (!a.composite && !a.out_uv && !a.out_mask && !a.out_steps) {
-            // the plain draw: both UVs, then both texel quads (eight loads in
-            // flight), then both stores; a wave with no sky pixel stores the
-            // clear colour only
-            uint32_t rgba[2] = {geo::kBlackRGBA, geo::kBlackRGBA};
-            if (geo::ballot_(!(bh0 && bh1)) != 0) {
-                float U[2], V[2];
-#pragma unroll
-                for (uint32_t k = 0; k < 2; ++k)
-                    geo::sky_uv(a.frame.central_to_uv, c2x[k], c2y[k], ct[k], rct[k], lam[k], &U[k], &V[k]);
-                const PaddedSkyQuad quad{__builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(a.sky), 0,
-                                                                           (int)a.sky_bytes, kBufferRsrcWord3),
-                                         a.sky_pitch_b};
-                uint32_t smp[2];
-#pragma unroll
-                for (uint32_t k = 0; k < 2; ++k) smp[k] = geo::sample_sky_quad_f(quad, a.sky_w256, a.sky_h256, U[k], V[k]);
-                rgba[0] = bh0 ? geo::kBlackRGBA : geo::over_clear(smp[0], a.sky_opaque != 0);
-                rgba[1] = bh1 ? geo::kBlackRGBA : geo::over_clear(smp[1], a.sky_opaque != 0);
-            }
-#pragma unroll
-            for (uint32_t k = 0; k < 2; ++k)
-                if (in[k]) a.out_rgba[(size_t)(ly + k * kWaveRows) * a.width + px] = rgba[k];
-        } else {
-#pragma unroll
-            for (uint32_t k = 0; k < 2; ++k)
-                if (in[k])
-                    shade_pixel(a, c2x[k], c2y[k], ct[k], rct[k], lam[k], 0u, (size_t)(ly + k * kWaveRows) * a.width + px);
-        }
+        fan_tile(a, tile, wave, lane);
     } else if constexpr (!MIPS) {
         if (in_frame) {
             float c2x, c2y, c2z;
@@ -459,6 +470,31 @@ __global__ __launch_bounds__(256) void geo_order_scatter(uint32_t* __restrict__ 
         order[pos] = ((i / tiles_x) << 16) | (i % tiles_x);
         cost[i] = 0u;
     }
+}
+
+#ifndef GEO_FAN_PERSIST
+#define GEO_FAN_PERSIST 0
+#endif
+#ifndef GEO_FAN_XCD
+#define GEO_FAN_XCD 0
+#endif
+constexpr uint32_t kPersistGroupsPerCU = GEO_FAN_PERSIST > 0 ? GEO_FAN_PERSIST : 8;
+// The fan-mode draw (level-0 sampler), persistent: gridDim.x workgroups walk
+// the tile grid with a stride of gridDim.x (every tile costs the same).
+__global__ __launch_bounds__(kBlock) void geo_fan_persist_kernel(const RenderArgs a, uint32_t tiles_x,
+                                                                 uint32_t ntiles) {
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x) >> 6;
+    const uint32_t lane = threadIdx.x & 63u;
+#if GEO_FAN_XCD
+    // workgroup b runs on XCD b % 8: XCD k's workgroups walk the k-th eighth
+    // of the tiles (gridDim.x % 8 == 0, checked at launch), so neighbouring
+    // tiles' sky lines meet in one L2
+    const uint32_t k = blockIdx.x & 7u, gx = gridDim.x >> 3;
+    const uint32_t lo = (uint32_t)((uint64_t)k * ntiles / 8u), hi = (uint32_t)((uint64_t)(k + 1u) * ntiles / 8u);
+    for (uint32_t t = lo + (blockIdx.x >> 3); t < hi; t += gx) fan_tile(a, make_uint2(t % tiles_x, t / tiles_x), wave, lane);
+#else
+    for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) fan_tile(a, make_uint2(t % tiles_x, t / tiles_x), wave, lane);
+#endif
 }
 
 // Frame row y of frame f comes from rank r = (y / band_rows) % world, local
@@ -1241,7 +1277,17 @@ static int render_impl(geo_ctx* c, const geo_frame* frame, const geo_scene* scen
         // buffer's chain of readers (the wait is queued after the launch, so
         // it holds back only later work on s, never this render)
         if (c->fan_written_rec[fb] && hipStreamWaitEvent(s, c->fan_written[fb], 0) != hipSuccess) return GEO_EHIP;
-        st = launch_tiles<GEO_MODE_FAN, geo::kCurvedOut>(a, mips, tiles_x, tiles_y, s, done);
+        if (GEO_FAN_PERSIST && !mips) {
+            const uint32_t ntiles = tiles_x * tiles_y;
+            uint32_t groups = min(ntiles, (uint32_t)c->num_cus * kPersistGroupsPerCU);
+            if (GEO_FAN_XCD) groups = max(8u, groups & ~7u);
+            a.tile_y0 = 0;
+            hipExtLaunchKernelGGL(geo_fan_persist_kernel, dim3(groups), dim3(kBlock), 0, s, nullptr, done, 0, a,
+                                  tiles_x, ntiles);
+            st = hipGetLastError() == hipSuccess ? GEO_OK : GEO_EHIP;
+        } else {
+            st = launch_tiles<GEO_MODE_FAN, geo::kCurvedOut>(a, mips, tiles_x, tiles_y, s, done);
+        }
         if (st) return st;
         if (c->fan_read_rec[fb] && hipStreamWaitEvent(s, c->fan_read[fb], 0) != hipSuccess) return GEO_EHIP;
         if (hipEventRecord(c->fan_read[fb], s) != hipSuccess) return GEO_EHIP;

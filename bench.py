@@ -413,9 +413,8 @@ def main():
         # drop), an event pair around each, one sync at the end
         iso = [(HipEvent(), HipEvent()) for _ in range(20)]
         for a, b in iso:
-            a.record()
+            ctx.time_next_render(a, b)
             sf.render_local(sf.bufs[0], scene=scene_defer)
-            b.record()
         torch.cuda.synchronize()
         ctx.steps_flush(torch.zeros(1, dtype=torch.int64, device=dev))  # discard the isolated launches' steps
         evs = {i: ab for i, ab in enumerate(iso)}
@@ -476,9 +475,10 @@ def main():
 
     value = total_steps / elapsed_max if mode != g.GEO_MODE_FAN else total_pixels / elapsed_max
     # roofline for the dominant kernel, on this rank: algorithmic flops per
-    # launch / avg launch time (event pairs, which add ~2 % to what they time:
-    # DESIGN.md §4), and the same flops per frame of the compute-only pass's
-    # wall time (no events; includes launch gaps)
+    # launch / avg launch time (event pairs on the kernel's own dispatch, the
+    # execution time a profiler's timestamps give), and the same flops per
+    # frame of the compute-only pass's wall time (no events; launch gaps
+    # included)
     achieved_tflops = flops_per_launch / (kernel_ms_avg * 1e-3) / 1e12
     wall_tflops = flops_per_launch / (compute_max / args.steps) / 1e12
     pmc_file, pmc = pmc_profile(args.config, args.mode, world) if not args.mips else (None, {})
@@ -533,10 +533,12 @@ def main():
         "mean_steps_per_pixel": total_steps / total_pixels,
         "kernel_ms": {"avg": kernel_ms_avg, "median": kernel_ms[len(kernel_ms) // 2], "min": kernel_ms[0],
                       "max_over_ranks_avg": kernel_ms_max, "frames_timed": len(kernel_ms),
-                      "events": ("hipEventDisableSystemFence pairs on every %d-th timed frame" % args.event_every
-                                 if sf.S == 1 else "hipEventDisableSystemFence pairs on 20 launches back to back on "
-                                 "one stream after the timed region (%d render streams overlap consecutive frames "
-                                 "inside it)" % sf.S)},
+                      "events": ("event pairs on the render kernel's own dispatch (geo_time_next_render: "
+                                 "start/end of its execution, no marker packets) on every %d-th timed frame"
+                                 % args.event_every if sf.S == 1 else
+                                 "event pairs on the render kernel's own dispatch (geo_time_next_render) on 20 "
+                                 "launches back to back on one stream after the timed region (%d render streams "
+                                 "overlap consecutive frames inside it)" % sf.S)},
         "pipelined": pipelined,
         "link_probe": link_probe,
         "compute_only": {"value": (total_steps if mode != g.GEO_MODE_FAN else total_pixels) / compute_max, "ms_per_step": compute_max / args.steps * 1e3,

@@ -263,6 +263,14 @@ int geo_pack_rgb(geo_ctx* ctx, const uint8_t* rgba, uint64_t npixels, uint8_t* r
 #define GEO_DISPATCH_EXPLICIT 2 /* set by geo_set_tile_order */
 int geo_set_dispatch(geo_ctx* ctx, int mode, uint32_t period);
 
+/* Times the next render of this context (geo_render_rows/bands/band_set, on
+ * any stream): its kernel dispatch carries start_event and stop_event
+ * (hipEvent_t created with timing), so hipEventElapsedTime gives the
+ * kernel's own execution time, as a profiler's dispatch timestamps do, with
+ * no marker packets around it.  (A frame of more than 65 535 tile rows: from
+ * the first launch's start to the last one's end.)  Consumed by that render. */
+int geo_time_next_render(geo_ctx* ctx, void* start_event, void* stop_event);
+
 /* An explicit dispatch order (GEO_DISPATCH_EXPLICIT): workgroup i draws tile
  * (order[i] & 0xFFFF, order[i] >> 16) of a tiles_x x tiles_y grid of
  * 32 x 8-pixel tiles over the rendered rows; order (host) must be a

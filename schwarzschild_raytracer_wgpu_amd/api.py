@@ -147,6 +147,11 @@ class Context:
                                                          out.ctypes.data if host else None, _stream_handle(stream)))
         return out
 
+    def time_next_render(self, start, stop) -> None:
+        """geo_time_next_render: the next render's kernel dispatch carries these
+        two HipEvents (timing.HipEvent): its execution time, no marker packets."""
+        check("geo_time_next_render", lib.geo_time_next_render(self._h, start.h, stop.h))
+
     def set_dispatch(self, mode: int, period: int = 16) -> None:
         """geo_set_dispatch: GEO_DISPATCH_LONGEST_FIRST (default; the order is
         re-learned on the device every `period` renders of a grid) or

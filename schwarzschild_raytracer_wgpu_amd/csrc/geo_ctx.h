@@ -79,6 +79,8 @@ struct geo_ctx {
     hipEvent_t order_written;
     uint32_t order_epoch;
     uint32_t stream_epoch[kRenderStreams];
+    // geo_time_next_render: events for the next render's kernel dispatch
+    hipEvent_t time_start, time_stop;
 };
 
 // Makes `dev` current for the scope of a C-ABI call, restoring the caller's device.

@@ -420,15 +420,19 @@ __global__ __launch_bounds__(kBlock) void geo_render_kernel(const RenderArgs a) 
 // dispatched from the highest class down; within a class, tile order.  Two
 // kernels: per-chunk class histograms, then each chunk's tiles scattered to
 // their positions (and their costs cleared for the next recording).
-constexpr int kCostClasses = 64;
+#ifndef GEO_COST_SUBOCTAVE_BITS
+#define GEO_COST_SUBOCTAVE_BITS 1
+#endif
+constexpr uint32_t kSubOctaveBits = GEO_COST_SUBOCTAVE_BITS;
+constexpr int kCostClasses = 32 << kSubOctaveBits;
 constexpr uint32_t kOrderChunk = 1024;  // tiles per workgroup
 
+// class = (octave << bits) + the top `bits` mantissa bits below the leading one
 __device__ __forceinline__ uint32_t cost_class(uint32_t c) {
     if (c == 0u) return 0u;
     const uint32_t o = 31u - (uint32_t)__clz(c);
-    const uint32_t half = (uint64_t)c * c >= (1ull << (2u * o + 1u)) ? 1u : 0u;  // c >= 2^o sqrt 2
-    const uint32_t k = 2u * o + half;
-    return k < (uint32_t)kCostClasses ? k : (uint32_t)kCostClasses - 1u;
+    const uint32_t m = (c << (31u - o)) >> (31u - kSubOctaveBits) & ((1u << kSubOctaveBits) - 1u);
+    return (o << kSubOctaveBits) + m;
 }
 
 __global__ __launch_bounds__(256) void geo_order_hist(const uint32_t* __restrict__ cost, uint32_t n,
@@ -470,31 +474,6 @@ __global__ __launch_bounds__(256) void geo_order_scatter(uint32_t* __restrict__ 
         order[pos] = ((i / tiles_x) << 16) | (i % tiles_x);
         cost[i] = 0u;
     }
-}
-
-#ifndef GEO_FAN_PERSIST
-#define GEO_FAN_PERSIST 0
-#endif
-#ifndef GEO_FAN_XCD
-#define GEO_FAN_XCD 0
-#endif
-constexpr uint32_t kPersistGroupsPerCU = GEO_FAN_PERSIST > 0 ? GEO_FAN_PERSIST : 8;
-// The fan-mode draw (level-0 sampler), persistent: gridDim.x workgroups walk
-// the tile grid with a stride of gridDim.x (every tile costs the same).
-__global__ __launch_bounds__(kBlock) void geo_fan_persist_kernel(const RenderArgs a, uint32_t tiles_x,
-                                                                 uint32_t ntiles) {
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x) >> 6;
-    const uint32_t lane = threadIdx.x & 63u;
-#if GEO_FAN_XCD
-    // workgroup b runs on XCD b % 8: XCD k's workgroups walk the k-th eighth
-    // of the tiles (gridDim.x % 8 == 0, checked at launch), so neighbouring
-    // tiles' sky lines meet in one L2
-    const uint32_t k = blockIdx.x & 7u, gx = gridDim.x >> 3;
-    const uint32_t lo = (uint32_t)((uint64_t)k * ntiles / 8u), hi = (uint32_t)((uint64_t)(k + 1u) * ntiles / 8u);
-    for (uint32_t t = lo + (blockIdx.x >> 3); t < hi; t += gx) fan_tile(a, make_uint2(t % tiles_x, t / tiles_x), wave, lane);
-#else
-    for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) fan_tile(a, make_uint2(t % tiles_x, t / tiles_x), wave, lane);
-#endif
 }
 
 // Frame row y of frame f comes from rank r = (y / band_rows) % world, local
@@ -1100,22 +1079,28 @@ static uint32_t band_rows_magic(uint32_t d) {
 // with its first tile row in tile_y0.  The kernel's mapping is the same.
 constexpr uint32_t kMaxGridY = 65535;
 extern "C++" {
-// The last launch records `done` (render_event) as its stop event.
+// The last launch records `done` (render_event) as its stop event; a timed
+// render (geo_time_next_render) puts the caller's start event on the first
+// launch's dispatch and its stop event on the last one's, and records `done`
+// after it.
 template <int MODE, int KIND>
 static int launch_tiles(RenderArgs a, bool mips, uint32_t tiles_x, uint32_t tiles_y, hipStream_t s,
-                        hipEvent_t done) {
+                        hipEvent_t done, hipEvent_t t_start, hipEvent_t t_stop) {
     for (uint32_t y0 = 0; y0 < tiles_y; y0 += kMaxGridY) {
         a.tile_y0 = y0;
         const uint32_t ny = tiles_y - y0 < kMaxGridY ? tiles_y - y0 : kMaxGridY;
-        hipEvent_t stop = y0 + ny >= tiles_y ? done : nullptr;
+        const bool last = y0 + ny >= tiles_y;
+        hipEvent_t start = y0 == 0 ? t_start : nullptr;
+        hipEvent_t stop = last ? (t_stop ? t_stop : done) : nullptr;
         if (mips)
             hipExtLaunchKernelGGL((geo_render_kernel<MODE, KIND, true>), dim3(tiles_x, ny), dim3(kBlock), 0, s,
-                                  nullptr, stop, 0, a);
+                                  start, stop, 0, a);
         else
             hipExtLaunchKernelGGL((geo_render_kernel<MODE, KIND, false>), dim3(tiles_x, ny), dim3(kBlock), 0, s,
-                                  nullptr, stop, 0, a);
+                                  start, stop, 0, a);
         if (hipGetLastError() != hipSuccess) return GEO_EHIP;
     }
+    if (t_stop && hipEventRecord(done, s) != hipSuccess) return GEO_EHIP;
     return GEO_OK;
 }
 }
@@ -1235,6 +1220,9 @@ static int render_impl(geo_ctx* c, const geo_frame* frame, const geo_scene* scen
     const int slot = render_slot(c, s);
     if (slot < 0) return GEO_EHIP;
     const hipEvent_t done = c->render_done[slot];
+    // geo_time_next_render's events, for this render only
+    const hipEvent_t t_start = c->time_start, t_stop = c->time_stop;
+    c->time_start = c->time_stop = nullptr;
     // The dispatch order (geo_ctx): a learned or explicit order for exactly
     // this grid, one launch, not in fan mode (its tiles all cost the same).
     bool record = false;
@@ -1277,32 +1265,22 @@ static int render_impl(geo_ctx* c, const geo_frame* frame, const geo_scene* scen
         // buffer's chain of readers (the wait is queued after the launch, so
         // it holds back only later work on s, never this render)
         if (c->fan_written_rec[fb] && hipStreamWaitEvent(s, c->fan_written[fb], 0) != hipSuccess) return GEO_EHIP;
-        if (GEO_FAN_PERSIST && !mips) {
-            const uint32_t ntiles = tiles_x * tiles_y;
-            uint32_t groups = min(ntiles, (uint32_t)c->num_cus * kPersistGroupsPerCU);
-            if (GEO_FAN_XCD) groups = max(8u, groups & ~7u);
-            a.tile_y0 = 0;
-            hipExtLaunchKernelGGL(geo_fan_persist_kernel, dim3(groups), dim3(kBlock), 0, s, nullptr, done, 0, a,
-                                  tiles_x, ntiles);
-            st = hipGetLastError() == hipSuccess ? GEO_OK : GEO_EHIP;
-        } else {
-            st = launch_tiles<GEO_MODE_FAN, geo::kCurvedOut>(a, mips, tiles_x, tiles_y, s, done);
-        }
+        st = launch_tiles<GEO_MODE_FAN, geo::kCurvedOut>(a, mips, tiles_x, tiles_y, s, done, t_start, t_stop);
         if (st) return st;
         if (c->fan_read_rec[fb] && hipStreamWaitEvent(s, c->fan_read[fb], 0) != hipSuccess) return GEO_EHIP;
         if (hipEventRecord(c->fan_read[fb], s) != hipSuccess) return GEO_EHIP;
         c->fan_read_rec[fb] = true;
     } else if (adaptive) {
         switch (geo::geodesic_kind(a.k)) {
-            case geo::kCurvedOut: st = launch_tiles<GEO_MODE_ADAPTIVE, geo::kCurvedOut>(a, mips, tiles_x, tiles_y, s, done); break;
-            case geo::kCurvedIn: st = launch_tiles<GEO_MODE_ADAPTIVE, geo::kCurvedIn>(a, mips, tiles_x, tiles_y, s, done); break;
-            default: st = launch_tiles<GEO_MODE_ADAPTIVE, geo::kFlat>(a, mips, tiles_x, tiles_y, s, done);
+            case geo::kCurvedOut: st = launch_tiles<GEO_MODE_ADAPTIVE, geo::kCurvedOut>(a, mips, tiles_x, tiles_y, s, done, t_start, t_stop); break;
+            case geo::kCurvedIn: st = launch_tiles<GEO_MODE_ADAPTIVE, geo::kCurvedIn>(a, mips, tiles_x, tiles_y, s, done, t_start, t_stop); break;
+            default: st = launch_tiles<GEO_MODE_ADAPTIVE, geo::kFlat>(a, mips, tiles_x, tiles_y, s, done, t_start, t_stop);
         }
     } else {
         switch (geo::geodesic_kind(a.k)) {
-            case geo::kCurvedOut: st = launch_tiles<GEO_MODE_DIRECT, geo::kCurvedOut>(a, mips, tiles_x, tiles_y, s, done); break;
-            case geo::kCurvedIn: st = launch_tiles<GEO_MODE_DIRECT, geo::kCurvedIn>(a, mips, tiles_x, tiles_y, s, done); break;
-            default: st = launch_tiles<GEO_MODE_DIRECT, geo::kFlat>(a, mips, tiles_x, tiles_y, s, done);
+            case geo::kCurvedOut: st = launch_tiles<GEO_MODE_DIRECT, geo::kCurvedOut>(a, mips, tiles_x, tiles_y, s, done, t_start, t_stop); break;
+            case geo::kCurvedIn: st = launch_tiles<GEO_MODE_DIRECT, geo::kCurvedIn>(a, mips, tiles_x, tiles_y, s, done, t_start, t_stop); break;
+            default: st = launch_tiles<GEO_MODE_DIRECT, geo::kFlat>(a, mips, tiles_x, tiles_y, s, done, t_start, t_stop);
         }
     }
     if (st) return st;
@@ -1430,6 +1408,13 @@ int geo_steps_flush(geo_ctx* c, unsigned long long* steps_total, void* stream) {
     hipExtLaunchKernelGGL(geo_steps_finalize, dim3(1), dim3(kStepSlots), 0, (hipStream_t)stream, nullptr, done, 0,
                           c->step_slots, steps_total);
     return hipGetLastError() == hipSuccess ? GEO_OK : GEO_EHIP;
+}
+
+int geo_time_next_render(geo_ctx* c, void* start_event, void* stop_event) {
+    if (!c || !start_event || !stop_event) return GEO_EINVAL;
+    c->time_start = (hipEvent_t)start_event;
+    c->time_stop = (hipEvent_t)stop_event;
+    return GEO_OK;
 }
 
 int geo_set_dispatch(geo_ctx* c, int mode, uint32_t period) {

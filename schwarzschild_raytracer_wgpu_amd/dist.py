@@ -360,10 +360,11 @@ class ShardedFrame:
         sh = self._sh[k]
         if sub < self.S:
             self.ev_free[b].wait(sh)  # first render of this stream into the batch buffer
-        if events is not None:
-            events[0].record(sh)
         band_h, row0, cycle, nb = self._band
         lib = self.lib
+        if events is not None:
+            # the render's kernel dispatch carries the pair (no marker packets)
+            lib.geo_time_next_render(self._ctx_h, events[0].h, events[1].h)
         if nb:
             st = lib.geo_render_band_set(
                 self._ctx_h, self._frame_ref, self._scene_ref if scene is None else ctypes.byref(scene), self.width,
@@ -373,8 +374,6 @@ class ShardedFrame:
                 from ._lib import check
 
                 check("geo_render_band_set", st)
-        if events is not None:
-            events[1].record(sh)
         if self.bpp == 3 and self.rank != 0:
             st = lib.geo_pack_rgb(self._ctx_h, self._lv[b][sub], self.slice // 4, self._sv[b][sub], sh)
             if st != 0:

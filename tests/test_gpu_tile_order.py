@@ -123,3 +123,25 @@ def test_dispatch_settings_rejected(dev):
             ctx.set_dispatch(mode, period)
     ctx.set_dispatch(GEO_DISPATCH_LONGEST_FIRST, 1 << 20)
     ctx.close()
+
+
+def test_time_next_render(dev):
+    """geo_time_next_render: the pair times the next render's kernel only; the
+    render is unchanged and the context's own ordering event still fires."""
+    from schwarzschild_raytracer_wgpu_amd.timing import HipEvent
+
+    w, h = 256, 144
+    frame = default_frame(w, h)
+    scene = default_scene(2048)
+    ctx = Context(0)
+    ctx.set_sky(make_sky("equirect", (256, 128)))
+    ref = torch.zeros(h * w * 4, dtype=torch.uint8, device=dev)
+    ctx.render_rows(frame, scene, w, h, 0, h, ref)
+    a, b = HipEvent(), HipEvent()
+    out = torch.zeros_like(ref)
+    ctx.time_next_render(a, b)
+    ctx.render_rows(frame, scene, w, h, 0, h, out)
+    ms = a.elapsed_time(b)
+    assert torch.equal(out, ref) and 0.0 < ms < 50.0
+    ctx.set_sky(make_sky("equirect", (128, 64)))  # waits on the context's event: must not hang
+    ctx.close()

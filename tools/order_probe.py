@@ -15,7 +15,9 @@ event pairs around each of N back-to-back launches after a spin-up:
   auto     the product default: GEO_DISPATCH_LONGEST_FIRST, the order learned
            on the device every 16 renders (its recording renders and
            rebuild kernels inside the timed launches)
-  python tools/order_probe.py [cfg2_1080p cfg3_4k cfg3_4k:fan ...]
+  python tools/order_probe.py [cfg2_1080p cfg3_4k cfg3_4k:fan cfg3_4k@8 ...]
+  (CFG@N: rank 1's share of an N-rank job, the interleaved 8-row bands
+  1, 1 + N, ... rendered by one geo_render_band_set, as bench.py's ranks do)
 """
 import json
 import os
@@ -70,7 +72,9 @@ def main():
     dev = torch.device("cuda", 0)
     out = {}
     for spec in names:
-        name, _, mname = spec.partition(":")
+        spec0, _, nranks = spec.partition("@")
+        name, _, mname = spec0.partition(":")
+        nranks = int(nranks or 1)
         cfg = CONFIGS[name]
         W, H = cfg.width, cfg.height
         obs = g.Observer(cfg.rs, cfg.fov, W, H)
@@ -87,11 +91,22 @@ def main():
         fan = mode == g.GEO_MODE_FAN
         if fan:
             ctx.solve_ray_fan(cfg.sphere_r, cfg.rs, cfg.max_steps, cfg.step, 400, obs.get_radial_position())
-        rgba = torch.empty(H * W * 4, dtype=torch.uint8, device=dev)
-        steps = torch.empty(H * W, dtype=torch.int32, device=dev)
-        ctx.render_rows(frame, scene, W, H, 0, H, rgba, out_steps=steps)
+        if nranks > 1:  # rank 1's bands of an nranks-way interleave (bench.py's layout, lead 1)
+            nb = len(range(1, (H + 7) // 8, nranks))
+            rows = nb * 8
+
+            def draw(out, **kw):
+                ctx.render_band_set(frame, scene, W, H, 8, 8, 8 * nranks, nb, out, **kw)
+        else:
+            rows = H
+
+            def draw(out, **kw):
+                ctx.render_rows(frame, scene, W, H, 0, H, out, **kw)
+        rgba = torch.empty(rows * W * 4, dtype=torch.uint8, device=dev)
+        steps = torch.empty(rows * W, dtype=torch.int32, device=dev)
+        draw(rgba, out_steps=steps)
         torch.cuda.synchronize()
-        cost, tx, ty = tile_costs(steps.view(H, W).cpu().numpy(), W, H, th=16 if fan else TH)
+        cost, tx, ty = tile_costs(steps.view(rows, W).cpu().numpy(), W, rows, th=16 if fan else TH)
         packed = (np.arange(ty)[:, None] << 16 | np.arange(tx)[None, :]).astype(np.uint32).ravel()
         by_cost = np.argsort(-cost.ravel(), kind="stable")
         orders = {"natural": None, "xcd": xcd_order(packed)}
@@ -100,7 +115,10 @@ def main():
         if not fan:  # fan-mode pixels have no steps: every tile costs the same
             orders.update(lpt=packed[by_cost], rev=packed[by_cost[::-1]],
                           xcd_lpt=xcd_order(packed, rank=-cost.ravel()))
-        n = 400 if W * H <= 1920 * 1080 else 200
+        keep = os.environ.get("PROBE_ORDERS")  # e.g. "natural,auto"
+        if keep:
+            orders = {k: v for k, v in orders.items() if k in keep.split(",")}
+        n = 400 if rows * W <= 1920 * 1080 else 200
         res = {k: [] for k in orders}
         span = {}
         for rep in range(3):
@@ -110,22 +128,22 @@ def main():
                 else:
                     ctx.set_tile_order(tx, ty, o)
                 for _ in range(300):  # clock spin-up
-                    ctx.render_rows(frame, scene, W, H, 0, H, rgba)
+                    draw(rgba)
                 evs = [(HipEvent(), HipEvent()) for _ in range(n)]
                 t0 = HipEvent()
                 t0.record()
                 for a, b in evs:
                     a.record()
-                    ctx.render_rows(frame, scene, W, H, 0, H, rgba)
+                    draw(rgba)
                     b.record()
                 torch.cuda.synchronize()
                 res[k].append(statistics.median(a.elapsed_time(b) for a, b in evs))
                 span.setdefault(k, []).append(t0.elapsed_time(evs[-1][1]) / n)
         ctx.set_tile_order(tx, ty, None)
         ref = rgba.clone()
-        ctx.render_rows(frame, scene, W, H, 0, H, ref)
-        ctx.set_tile_order(tx, ty, orders["lpt"])
-        ctx.render_rows(frame, scene, W, H, 0, H, rgba)
+        draw(ref)
+        ctx.set_tile_order(tx, ty, packed[by_cost])
+        draw(rgba)
         torch.cuda.synchronize()
         same = bool(torch.equal(ref, rgba))
         ctx.close()

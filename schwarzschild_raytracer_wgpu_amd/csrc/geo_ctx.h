@@ -22,16 +22,27 @@ struct geo_ctx {
     // Ray fan, double-buffered so that a frame's fan can be solved on a side
     // stream while the previous frame's fan-mode draws still read the other
     // buffer.  fan[fan_cur] is the context's fan (fan_cur < 0: none).  Each
-    // buffer's last writer (geo_solve_ray_fan) and readers (fan-mode renders,
-    // a chained event: every render waits, after its launch, for the previous
-    // reader) are events, so a solve into a buffer waits for the draws that
-    // read it and a draw waits for the solve that wrote its buffer, whatever
-    // streams they run on.
+    // buffer's last writer (geo_solve_ray_fan, on fan_writer[b]) and readers
+    // (fan-mode renders) are tracked so that a solve into a buffer waits for
+    // the draws that read it and a draw waits for the solve that wrote its
+    // buffer, whatever streams they run on, with no event work for what
+    // stream order already gives:
+    //   * a draw on the writer's stream neither waits for the solve nor
+    //     records an event: its slot's bit in fan_read_slots[b] stands for it
+    //     (render_done of that slot completes after it);
+    //   * a draw on another stream waits for fan_written[b] and joins the
+    //     chained reader event fan_read[b] (recorded after its launch; when
+    //     the previous recorder ran on another stream the draw first waits for
+    //     it, so the event covers every recorded reader);
+    //   * a solve into b waits for the writer, the chain and the slots' events
+    //     that are not on its own stream, then starts b's record afresh.
     float* fan[2];
     uint32_t fan_cap, n_fan[2];
     int fan_cur;
     hipEvent_t fan_written[2], fan_read[2];
     bool fan_written_rec[2], fan_read_rec[2];
+    hipStream_t fan_writer[2], fan_reader[2];  // streams of the last solve, of the last chain record
+    uint32_t fan_read_slots[2];               // render slots (bits) whose unrecorded draws read the buffer
     // Sharded step counters: set 0 is the GEO_FLAG_DEFER_STEPS accumulator
     // (geo_steps_flush folds it); a render with a steps_total of its own
     // counts into one of kStepCallSets per-call sets, taken round-robin, and

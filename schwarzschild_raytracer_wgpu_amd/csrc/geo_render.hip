@@ -268,67 +268,88 @@ __device__ __forceinline__ float pixel_lambda(const RenderArgs& a, float st, flo
 // the second pixel overlap the first's (the fan lerp and the texel quads are
 // the kernel's latency; its VALU work is short).  The mip-mapped fan draw
 // measured the same either way (profiles/r03v_fan_mips_ab.txt) and keeps one.
+// Four pixels per lane (a 32 x 32 tile, 47 VGPRs) measured the same as two
+// (4K draw 0.0373 vs 0.0370 ms, 3 x 3 interleaved, profiles/r04g_fan_lr_ab.txt):
+// the draw's waves are not short of independent work.
+constexpr uint32_t kFanLaneRows = 2;
 __host__ __device__ constexpr uint32_t lane_rows(int mode, bool mips) {
-    return mode == GEO_MODE_FAN && !mips ? 2u : 1u;
+    return mode == GEO_MODE_FAN && !mips ? kFanLaneRows : 1u;
 }
 
-// The fan-mode draw of one 32 x 16 tile, two pixels per lane (lane_rows):
-// both pixels' rays, then both fan lerps (four loads in flight), then both
-// epilogues.
+// The fan-mode draw of one 32 x (8 LR) tile, LR pixels per lane (lane_rows)
+// kWaveRows rows apart: every pixel's ray, then every fan lerp (2 LR loads in
+// flight), then every epilogue.  Pixels k and k + 1 (k even) lie in one
+// 8-row-aligned group of the wave's rows, so in one band (band heights are
+// multiples of 8): the band mapping is per group, in scalar ops.
+template <uint32_t LR>
 __device__ __forceinline__ void fan_tile(const RenderArgs& a, uint2 tile, uint32_t wave, uint32_t lane) {
-    constexpr uint32_t LR = 2;
+    static_assert(LR % 2 == 0 && LR * kWaveRows % 8 == 0, "pixel pairs fill 8-row groups");
     const uint32_t px = tile.x * kTileW + (wave % kWavesX) * kWaveW + lane % kWaveW;
     const uint32_t wl0 = tile.y * (kTileH * LR) + (wave / kWavesX) * (kWaveRows * LR);
-    const uint32_t ly = wl0 + lane / kWaveW;
-    const uint32_t band = __umulhi(wl0, a.band_magic);
-    const uint32_t py = a.row0 + band * a.band_stride + (wl0 - band * a.band_rows) + (ly - wl0);
-    float c2x[2], c2y[2], st[2], ct[2], rct[2], lam[2];
+    const uint32_t r = lane / kWaveW;
+    uint32_t ly[LR], py[LR];
 #pragma unroll
-    for (uint32_t k = 0; k < 2; ++k) {
+    for (uint32_t k = 0; k < LR; k += 2) {
+        const uint32_t g0 = wl0 + (k / 2) * 8u;  // 8-row-aligned local row of pixels k, k + 1
+        const uint32_t band = __umulhi(g0, a.band_magic);
+        const uint32_t p0 = a.row0 + band * a.band_stride + (g0 - band * a.band_rows) + r;
+        ly[k] = g0 + r;
+        ly[k + 1] = g0 + r + kWaveRows;
+        py[k] = p0;
+        py[k + 1] = p0 + kWaveRows;
+    }
+    float c2x[LR], c2y[LR], st[LR], ct[LR], rct[LR], lam[LR];
+#pragma unroll
+    for (uint32_t k = 0; k < LR; ++k) {
         float c2z;
         geo::pixel_central_dir(a.cam, a.frame.movement_to_central, a.frame.psi_factor_and_position[0], a.kt, px,
-                               py + k * kWaveRows, &c2x[k], &c2y[k], &c2z);
+                               py[k], &c2x[k], &c2y[k], &c2z);
         st[k] = geo::central_sin(c2z);
         ct[k] = geo::central_rho(c2x[k], c2y[k]);
         rct[k] = geo::rcpf_(ct[k]);
     }
-    geo::FanPos fp[2];
+    geo::FanPos fp[LR];
 #pragma unroll
-    for (uint32_t k = 0; k < 2; ++k) fp[k] = geo::fan_pos(a.n_fan, st[k]);
+    for (uint32_t k = 0; k < LR; ++k) fp[k] = geo::fan_pos(a.n_fan, st[k]);
 #pragma unroll
-    for (uint32_t k = 0; k < 2; ++k) lam[k] = geo::fan_at(a.fan, fp[k]);
-    bool in[2];
+    for (uint32_t k = 0; k < LR; ++k) lam[k] = geo::fan_at(a.fan, fp[k]);
+    bool in[LR], bh[LR];
+    bool all_bh = true;
 #pragma unroll
-    for (uint32_t k = 0; k < 2; ++k)
-        in[k] = px < a.width && ly + k * kWaveRows < a.nrows && py + k * kWaveRows < a.height;
-    const bool bh0 = lam[0] < geo::kBlackHoleLambda, bh1 = lam[1] < geo::kBlackHoleLambda;
+    for (uint32_t k = 0; k < LR; ++k) {
+        in[k] = px < a.width && ly[k] < a.nrows && py[k] < a.height;
+        bh[k] = lam[k] < geo::kBlackHoleLambda;
+        all_bh = all_bh && bh[k];
+    }
     if (!a.composite && !a.out_uv && !a.out_mask && !a.out_steps) {
-        // the plain draw: both UVs, then both texel quads (eight loads in
-        // flight), then both stores; a wave with no sky pixel stores the
+        // the plain draw: every UV, then every texel quad (4 LR loads in
+        // flight), then the stores; a wave with no sky pixel stores the
         // clear colour only
-        uint32_t rgba[2] = {geo::kBlackRGBA, geo::kBlackRGBA};
-        if (geo::ballot_(!(bh0 && bh1)) != 0) {
-            float U[2], V[2];
+        uint32_t rgba[LR];
 #pragma unroll
-            for (uint32_t k = 0; k < 2; ++k)
+        for (uint32_t k = 0; k < LR; ++k) rgba[k] = geo::kBlackRGBA;
+        if (geo::ballot_(!all_bh) != 0) {
+            float U[LR], V[LR];
+#pragma unroll
+            for (uint32_t k = 0; k < LR; ++k)
                 geo::sky_uv(a.frame.central_to_uv, c2x[k], c2y[k], ct[k], rct[k], lam[k], &U[k], &V[k]);
             const PaddedSkyQuad quad{__builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(a.sky), 0,
                                                                        (int)a.sky_bytes, kBufferRsrcWord3),
                                      a.sky_pitch_b};
-            uint32_t smp[2];
+            uint32_t smp[LR];
 #pragma unroll
-            for (uint32_t k = 0; k < 2; ++k) smp[k] = geo::sample_sky_quad_f(quad, a.sky_w256, a.sky_h256, U[k], V[k]);
-            rgba[0] = bh0 ? geo::kBlackRGBA : geo::over_clear(smp[0], a.sky_opaque != 0);
-            rgba[1] = bh1 ? geo::kBlackRGBA : geo::over_clear(smp[1], a.sky_opaque != 0);
+            for (uint32_t k = 0; k < LR; ++k) smp[k] = geo::sample_sky_quad_f(quad, a.sky_w256, a.sky_h256, U[k], V[k]);
+#pragma unroll
+            for (uint32_t k = 0; k < LR; ++k)
+                rgba[k] = bh[k] ? geo::kBlackRGBA : geo::over_clear(smp[k], a.sky_opaque != 0);
         }
 #pragma unroll
-        for (uint32_t k = 0; k < 2; ++k)
-            if (in[k]) a.out_rgba[(size_t)(ly + k * kWaveRows) * a.width + px] = rgba[k];
+        for (uint32_t k = 0; k < LR; ++k)
+            if (in[k]) a.out_rgba[(size_t)ly[k] * a.width + px] = rgba[k];
     } else {
 #pragma unroll
-        for (uint32_t k = 0; k < 2; ++k)
-            if (in[k])
-                shade_pixel(a, c2x[k], c2y[k], ct[k], rct[k], lam[k], 0u, (size_t)(ly + k * kWaveRows) * a.width + px);
+        for (uint32_t k = 0; k < LR; ++k)
+            if (in[k]) shade_pixel(a, c2x[k], c2y[k], ct[k], rct[k], lam[k], 0u, (size_t)ly[k] * a.width + px);
     }
 }
 
@@ -353,8 +374,8 @@ __global__ __launch_bounds__(kBlock) void geo_render_kernel(const RenderArgs a) 
     const uint32_t py = a.row0 + band * a.band_stride + (wl0 - band * a.band_rows) + (ly - wl0);
     uint32_t steps = 0;
     const bool in_frame = px < a.width && ly < a.nrows && py < a.height;
-    if constexpr (LR == 2) {
-        fan_tile(a, tile, wave, lane);
+    if constexpr (LR > 1) {
+        fan_tile<LR>(a, tile, wave, lane);
     } else if constexpr (!MIPS) {
         if (in_frame) {
             float c2x, c2y, c2z;
@@ -861,11 +882,21 @@ static int wait_renders(geo_ctx* c) {
     return GEO_OK;
 }
 
-// The fan buffer b's last writer and readers.
+// The fan buffer b's last writer and readers (geo_ctx: the chained event and
+// the slots of the draws that recorded none).
 static int wait_fan(geo_ctx* c, int b) {
     if (c->fan_written_rec[b] && hipEventSynchronize(c->fan_written[b]) != hipSuccess) return GEO_EHIP;
     if (c->fan_read_rec[b] && hipEventSynchronize(c->fan_read[b]) != hipSuccess) return GEO_EHIP;
+    for (int i = 0; i < c->n_render_streams; ++i)
+        if ((c->fan_read_slots[b] >> i & 1u) && hipEventSynchronize(c->render_done[i]) != hipSuccess) return GEO_EHIP;
     return GEO_OK;
+}
+
+// Buffer b holds no pending writer or reader (after a host wait for them).
+static void fan_forget(geo_ctx* c, int b) {
+    c->fan_written_rec[b] = c->fan_read_rec[b] = false;
+    c->fan_writer[b] = c->fan_reader[b] = nullptr;
+    c->fan_read_slots[b] = 0;
 }
 
 // The slot whose event tracks the context's work on stream s
@@ -888,6 +919,8 @@ static int render_slot(geo_ctx* c, hipStream_t s) {
             i = c->render_next;
             c->render_next = (i + 1) % geo_ctx::kRenderStreams;
             if (hipEventSynchronize(c->render_done[i]) != hipSuccess) return -1;
+            // the evicted stream's draws are done: no fan buffer waits for them
+            for (int b = 0; b < 2; ++b) c->fan_read_slots[b] &= ~(1u << i);
         }
         c->render_stream[i] = s;
         c->stream_epoch[i] = 0;  // has not waited for any order rebuild
@@ -1003,6 +1036,7 @@ static int ensure_fan(geo_ctx* c, uint32_t n) {
         if (c->fan[b]) (void)hipFree(c->fan[b]);
         c->fan[b] = nullptr;
         c->n_fan[b] = 0;
+        fan_forget(c, b);
     }
     c->fan_cap = 0;
     c->fan_cur = -1;
@@ -1017,11 +1051,18 @@ static int ensure_fan(geo_ctx* c, uint32_t n) {
 }
 
 // The buffer a new fan goes to (the one the current fan is not in), ordered
-// on stream s after its previous writer and readers.
+// on stream s after its previous writer and readers (on s itself by stream
+// order).
 static int fan_next(geo_ctx* c, hipStream_t s) {
     const int b = c->fan_cur < 0 ? 0 : 1 - c->fan_cur;
-    if (c->fan_written_rec[b] && hipStreamWaitEvent(s, c->fan_written[b], 0) != hipSuccess) return -1;
-    if (c->fan_read_rec[b] && hipStreamWaitEvent(s, c->fan_read[b], 0) != hipSuccess) return -1;
+    if (c->fan_written_rec[b] && c->fan_writer[b] != s && hipStreamWaitEvent(s, c->fan_written[b], 0) != hipSuccess)
+        return -1;
+    if (c->fan_read_rec[b] && c->fan_reader[b] != s && hipStreamWaitEvent(s, c->fan_read[b], 0) != hipSuccess)
+        return -1;
+    for (int i = 0; i < c->n_render_streams; ++i)
+        if ((c->fan_read_slots[b] >> i & 1u) && c->render_stream[i] != s &&
+            hipStreamWaitEvent(s, c->render_done[i], 0) != hipSuccess)
+            return -1;
     return b;
 }
 
@@ -1036,6 +1077,7 @@ int geo_set_fan(geo_ctx* c, const float* fan, uint32_t n) {
     const int b = c->fan_cur < 0 ? 0 : 1 - c->fan_cur;
     if (wait_fan(c, b) != GEO_OK) return GEO_EHIP;
     if (hipMemcpy(c->fan[b], fan, sizeof(float) * n, hipMemcpyHostToDevice) != hipSuccess) return GEO_EHIP;
+    fan_forget(c, b);  // written and read by nothing in flight
     c->n_fan[b] = n;
     c->fan_cur = b;
     return GEO_OK;
@@ -1055,7 +1097,11 @@ int geo_solve_ray_fan(geo_ctx* c, double sphere_r, double schwarz_r, uint32_t ma
                        schwarz_r, max_iter, step, nr_nodes, r, c->fan[b]);
     if (hipGetLastError() != hipSuccess) return GEO_EHIP;
     if (hipEventRecord(c->fan_written[b], s) != hipSuccess) return GEO_EHIP;
+    // the solve is ordered after every earlier reader of b: later waits for
+    // b's readers start afresh, and a wait for the solve covers the old ones
+    fan_forget(c, b);
     c->fan_written_rec[b] = true;
+    c->fan_writer[b] = s;
     c->n_fan[b] = nr_nodes;
     c->fan_cur = b;
     if (fan_out) {
@@ -1262,15 +1308,27 @@ static int render_impl(geo_ctx* c, const geo_frame* frame, const geo_scene* scen
     }
     int st;
     if (scene->mode == GEO_MODE_FAN) {
-        // after the solve that wrote the buffer; then this render joins the
-        // buffer's chain of readers (the wait is queued after the launch, so
-        // it holds back only later work on s, never this render)
-        if (c->fan_written_rec[fb] && hipStreamWaitEvent(s, c->fan_written[fb], 0) != hipSuccess) return GEO_EHIP;
+        // after the solve that wrote the buffer (geo_ctx: on the solve's own
+        // stream by stream order, with no event work: the reader is its
+        // slot's bit); on another stream this render then joins the buffer's
+        // chain of readers (the wait is queued after the launch, so it holds
+        // back only later work on s, never this render)
+        // (a buffer uploaded by geo_set_fan has no writer in flight: its next
+        // writer waits for its readers on the host, so they need no event)
+        const bool by_slot = !c->fan_written_rec[fb] || c->fan_writer[fb] == s;
+        if (!by_slot && hipStreamWaitEvent(s, c->fan_written[fb], 0) != hipSuccess) return GEO_EHIP;
         st = launch_tiles<GEO_MODE_FAN, geo::kCurvedOut>(a, mips, tiles_x, tiles_y, s, done, t_start, t_stop);
         if (st) return st;
-        if (c->fan_read_rec[fb] && hipStreamWaitEvent(s, c->fan_read[fb], 0) != hipSuccess) return GEO_EHIP;
-        if (hipEventRecord(c->fan_read[fb], s) != hipSuccess) return GEO_EHIP;
-        c->fan_read_rec[fb] = true;
+        if (by_slot) {
+            c->fan_read_slots[fb] |= 1u << slot;
+        } else {
+            if (c->fan_read_rec[fb] && c->fan_reader[fb] != s &&
+                hipStreamWaitEvent(s, c->fan_read[fb], 0) != hipSuccess)
+                return GEO_EHIP;
+            if (hipEventRecord(c->fan_read[fb], s) != hipSuccess) return GEO_EHIP;
+            c->fan_read_rec[fb] = true;
+            c->fan_reader[fb] = s;
+        }
     } else if (adaptive) {
         switch (geo::geodesic_kind(a.k)) {
             case geo::kCurvedOut: st = launch_tiles<GEO_MODE_ADAPTIVE, geo::kCurvedOut>(a, mips, tiles_x, tiles_y, s, done, t_start, t_stop); break;

@@ -345,6 +345,56 @@ def test_fan_solved_on_side_stream_matches_one_stream(geo, torch_mod):
     assert np.mean(np.all(got == ref["rgba"], axis=-1)) > 0.999  # GPU fan within 1 f32 ulp of the oracle's
 
 
+def test_fan_stream_switches_match_one_stream(geo, torch_mod):
+    """The fan buffers' readers on the solve's own stream are tracked by
+    render slot (no per-draw event), readers on other streams by a chained
+    event: solves and draws that switch streams from frame to frame, with a
+    synchronous host upload (geo_set_fan) among them, draw the frames of the
+    same sequence run on one stream with a sync after every frame.  1080p
+    draws, so a solve issued early into a buffer still being read would
+    change the frame."""
+    from schwarzschild_raytracer_wgpu_amd.scenes import make_sky
+
+    w, h = 1920, 1080
+    dev = torch_mod.device("cuda:0")
+    sky = make_sky("equirect", (512, 256))
+    radii = [2.5 + 0.2 * i for i in range(14)]
+    # (solve stream, draw stream) per frame; "set": the fan uploaded from the host
+    plan = [("A", "A"), ("A", "A"), ("B", "A"), ("B", "A"), ("B", "B"), ("A", "B"), ("A", "A"), ("C", "B"),
+            ("set", "A"), ("B", "C"), ("A", "C"), ("A", "A"), ("set", "B"), ("C", "A")]
+    host_fans = {i: O.solve_ray_fan(50.0, 1.0, 1000, math.pi / 100, 400, radii[i])
+                 for i, (s, _) in enumerate(plan) if s == "set"}
+
+    def run(streams, sync_each):
+        ctx = geo.Context(0)
+        ctx.set_sky(sky)
+        tgts = [torch_mod.empty(w * h * 4, dtype=torch_mod.uint8, device=dev) for _ in plan]
+        obs = geo.Observer(1.0, math.pi / 2, w, h)
+        torch_mod.cuda.synchronize()
+        for i, (s, d) in enumerate(plan):
+            obs.set_position(radii[i], 0.0, 0.1)
+            r = obs.get_radial_position()
+            if s == "set":
+                ctx.set_fan(host_fans[i])
+            else:
+                ctx.solve_ray_fan(50.0, 1.0, 1000, math.pi / 100, 400, r, stream=streams[s], host=False)
+            scene = geo.make_scene(1.0, 50.0, r, math.pi / 100, 1000, geo.GEO_MODE_FAN)
+            ctx.render_rows(obs.calc_transformation_pipeline(), scene, w, h, 0, h, tgts[i], stream=streams[d])
+            if sync_each:
+                torch_mod.cuda.synchronize()
+        torch_mod.cuda.synchronize()
+        out = [t.cpu().numpy() for t in tgts]
+        ctx.close()
+        return out
+
+    cur = torch_mod.cuda.current_stream(dev)
+    ref = run({"A": cur, "B": cur, "C": cur}, True)
+    got = run({"A": cur, "B": torch_mod.cuda.Stream(dev), "C": torch_mod.cuda.Stream(dev)}, False)
+    assert len({f.tobytes() for f in ref}) == len(ref)  # every frame needs its own fan
+    for i, (a, b) in enumerate(zip(ref, got)):
+        assert np.array_equal(a, b), (i, plan[i])
+
+
 def test_fan_plain_draw_bitexact(geo, torch_mod):
     """The fan-mode draw with no output but the colour (a lane draws two
     pixels, 8 rows apart, loads of both in flight): bit for bit the oracle's

@@ -54,8 +54,10 @@ def parse():
     p.add_argument("--spinup-frames", type=int, default=300,
                    help="untimed GPU clock spin-up frames x n_gpus before the warmup steps (the clock settles "
                         "after ~100 full frames); a frame count, identical on every rank")
-    p.add_argument("--event-every", type=int, default=4,
-                   help="time every k-th timed frame's kernel with a fence-free HIP event pair")
+    p.add_argument("--event-every", type=int, default=None,
+                   help="time every k-th timed frame's kernel with an event pair on its dispatch (default: --steps "
+                        "/ 10, at least 4: about 10 samples; a timed frame costs ~8 us more wall time than an "
+                        "untimed one, profiles/r04h_event_cost.txt, so every 4th frame read 1-4 %% slower)")
     p.add_argument("--config", default="cfg3_4k")
     p.add_argument("--band-rows", type=int, default=8)
     p.add_argument("--render-streams", type=int, default=None,
@@ -224,6 +226,8 @@ def main():
         if dist.get_world_size() != world:
             raise SystemExit(f"process group has {dist.get_world_size()} ranks, WORLD_SIZE={world}")
 
+    if args.event_every is None:
+        args.event_every = max(4, args.steps // 10)
     if args.frames_per_gather is None:
         args.frames_per_gather = max(1, min(8, args.steps // 10))
     cfg = CONFIGS[args.config]

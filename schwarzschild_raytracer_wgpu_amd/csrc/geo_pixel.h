@@ -728,7 +728,7 @@ GEO_HD float geodesic_finish(const PixelConsts& k, const StopTest<KIND>& stop_at
 
 // RK4 steps per exit test: 4 is the fastest on gfx950 (G = 5, 6, 8 +0.4, +5,
 // +6 % on config 3: the steps a lane wastes in its stopping group outweigh the
-// saved tests; DESIGN.md §4, tools/ubench/loop_ab.hip)
+// saved tests; DESIGN.md §4, tools/ubench/loop_ab.hip at 3cd1aa2)
 constexpr int kGroup = 4;
 
 // Traveled angle of the ray at angle theta to the black hole, or kNoValue.

@@ -44,7 +44,7 @@
 namespace {
 
 constexpr int kWaveW = 16;             // a wave64 covers a compact 16x4 block (few divergent
-constexpr int kWaveRows = 64 / kWaveW;  // steps per wave; tools/ubench/loop_ab.hip)
+constexpr int kWaveRows = 64 / kWaveW;  // steps per wave; tools/ubench/loop_ab.hip at 3cd1aa2)
 constexpr int kWavesX = 2;              // waves side by side in a tile
 constexpr int kTileW = kWaveW * kWavesX;
 constexpr int kTileH = 8;               // a block kTileW x kTileH

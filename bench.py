@@ -72,6 +72,10 @@ def parse():
                         "clamped to [1, 8]: the timed region ends with the last batch's gather and reassembly, "
                         "and its first batch's renders run before any gather starts, so a short run wants "
                         "shallow batches (20 steps: 2) and a long one amortises the host cost (200 steps: 8)")
+    p.add_argument("--batch-launch", default="auto", choices=["auto", "on", "off"],
+                   help="N > 1: render each gather batch's frames in ONE launch (geo_render_band_set_frames), "
+                        "paying a launch's fixed cost (~12.6 us: dispatch, ramp, drain) once per batch instead of per "
+                        "frame; auto = on when --frames-per-gather > 1")
     p.add_argument("--rank0-lead", default="auto", choices=["auto", "1", "2", "3", "4", "6"],
                    help="N > 1: rank 0's band height in 8-row bands per cycle (it renders rows that never cross "
                         "an xGMI link, so a link-bound present wants it larger); auto = the fastest of 1, 2, 3, 4, "
@@ -260,7 +264,8 @@ def main():
     def make_sf(lead):
         return ShardedFrame(ctx, frame, scene, W, H, args.band_rows, rank, world, dev, dist if world > 1 else None,
                             host_gather=args.dist_backend == "gloo", frames_per_gather=args.frames_per_gather,
-                            render_streams=args.render_streams or (1 if world == 1 else 2), lead=lead)
+                            render_streams=args.render_streams or (1 if world == 1 else 2), lead=lead,
+                            batch_launch=args.batch_launch != "off")
 
     # everything that syncs or reads back (lead trials, the diagnostic pass)
     # runs before the clock spin-up below, which flows straight into the
@@ -343,7 +348,7 @@ def main():
     # per-launch kernel time: event pairs inside the timed region with one
     # render stream; with two (N > 1) launches overlap by design, so the
     # launch duration is measured on isolated launches after the timed region
-    timed = set(range(0, args.steps, max(1, args.event_every))) if sf.S == 1 else set()
+    timed = set(range(0, args.steps, max(1, args.event_every))) if sf.S == 1 and not sf.batch else set()
     evs = {i: (HipEvent(), HipEvent()) for i in timed}
     steps_ctr.zero_()
     torch.cuda.synchronize()
@@ -383,9 +388,13 @@ def main():
     if world > 1:
         dist.barrier()
     c0 = time.perf_counter()
-    for i in range(args.steps):
-        with torch.cuda.stream(sf._render_stream(i)):
-            sf.render_local(sf.local_view(i), scene=scene_defer)
+    if sf.batch:
+        for i0 in range(0, args.steps, sf.K):
+            sf.render_batch((i0 // sf.K) % 2, [frame] * min(sf.K, args.steps - i0), scene=scene_defer)
+    else:
+        for i in range(args.steps):
+            with torch.cuda.stream(sf._render_stream(i)):
+                sf.render_local(sf.local_view(i), scene=scene_defer)
     sf._join()
     torch.cuda.synchronize()
     if world > 1:
@@ -411,18 +420,26 @@ def main():
                      "value": steps_diag * args.steps / el2,
                      "what": "the same K frames on two render streams (consecutive frames overlap); informational"}
         del sf2
-    if sf.S > 1:
+    per_launch = 1  # frames per timed launch
+    if sf.S > 1 or sf.batch:
         # one launch at a time: 20 launches back to back on ONE stream (no
         # overlap, and no idle gap between them that would let the clock
-        # drop), an event pair around each, one sync at the end
+        # drop), an event pair around each, one sync at the end; with batched
+        # launches each is a whole batch of K frames, and its time / K the
+        # per-frame figure the flops per frame divide
         iso = [(HipEvent(), HipEvent()) for _ in range(20)]
+        cur = torch.cuda.current_stream().cuda_stream
         for a, b in iso:
-            ctx.time_next_render(a, b)
-            sf.render_local(sf.bufs[0], scene=scene_defer)
+            if sf.batch:
+                sf.render_batch(0, [frame] * sf.K, scene=scene_defer, events=(a, b), stream=cur)
+            else:
+                ctx.time_next_render(a, b)
+                sf.render_local(sf.bufs[0], scene=scene_defer)
         torch.cuda.synchronize()
         ctx.steps_flush(torch.zeros(1, dtype=torch.int64, device=dev))  # discard the isolated launches' steps
         evs = {i: ab for i, ab in enumerate(iso)}
-    kernel_ms = sorted(a.elapsed_time(b) for a, b in evs.values())
+        per_launch = sf.K if sf.batch else 1
+    kernel_ms = sorted(a.elapsed_time(b) / per_launch for a, b in evs.values())
     kernel_ms_avg = sum(kernel_ms) / len(kernel_ms)
 
     steps_done = int(steps_ctr.item())
@@ -525,6 +542,7 @@ def main():
             "rank0_lead": L.lead,
             "lead_trials_ms_per_frame": lead_trials,
             "render_streams": sf.S,
+            "frames_per_launch": sf.K if sf.batch else 1,
         },
         "per_gpu": value / world,
         "world_size": dist.get_world_size() if world > 1 else 1,
@@ -539,10 +557,14 @@ def main():
                       "max_over_ranks_avg": kernel_ms_max, "frames_timed": len(kernel_ms),
                       "events": ("event pairs on the render kernel's own dispatch (geo_time_next_render: "
                                  "start/end of its execution, no marker packets) on every %d-th timed frame"
-                                 % args.event_every if sf.S == 1 else
+                                 % args.event_every if sf.S == 1 and not sf.batch else
                                  "event pairs on the render kernel's own dispatch (geo_time_next_render) on 20 "
                                  "launches back to back on one stream after the timed region (%d render streams "
-                                 "overlap consecutive frames inside it)" % sf.S)},
+                                 "overlap consecutive frames inside it)" % sf.S if not sf.batch else
+                                 "event pairs on the render kernel's own dispatch (geo_time_next_render) on 20 "
+                                 "batched launches of %d frames back to back on one stream after the timed region, "
+                                 "each launch's time / %d (the timed region renders each gather batch in one launch)"
+                                 % (sf.K, sf.K))},
         "pipelined": pipelined,
         "link_probe": link_probe,
         "compute_only": {"value": (total_steps if mode != g.GEO_MODE_FAN else total_pixels) / compute_max, "ms_per_step": compute_max / args.steps * 1e3,

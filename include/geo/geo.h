@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define GEO_ABI_VERSION 3
+#define GEO_ABI_VERSION 4  /* 4: geo_render_band_set_frames */
 
 typedef enum geo_status {
     GEO_OK = 0,
@@ -219,6 +219,25 @@ int geo_render_band_set(geo_ctx* ctx, const geo_frame* frame, const geo_scene* s
                         uint32_t row_stride, uint32_t nbands, uint8_t* out_rgba8, uint8_t* out_mask,
                         float* out_uv, uint32_t* out_steps, unsigned long long* steps_total,
                         void* stream);
+
+/* A batch of nframes (1 .. GEO_MAX_BATCH_FRAMES) frames of one scene in ONE
+ * launch: frame f's uniform is frames[f], its packed bands (the layout of
+ * geo_render_band_set) go to out_rgba8 + f*out_frame_stride bytes
+ * (out_frame_stride a multiple of 4, at least the packed bands' bytes).  The
+ * frames share the scene (observer radius, step, budget, mode), so a batch is
+ * frames of an observer at one radius (Unmoving, Orbiting, or the same pose
+ * drawn again); fan mode reads the context's current fan for every frame.
+ * Colour only (no mask, UV or per-pixel steps; no GEO_FLAG_MIPS); the
+ * executed steps of all frames go to steps_total or, with
+ * GEO_FLAG_DEFER_STEPS, to the context's accumulator.  One launch pays the
+ * dispatch, ramp and drain of a render once for the whole batch (DESIGN.md
+ * §4: ~12.6 us per launch against ~23 us per 4K megapixel), which is most of
+ * a rank's share at N = 8.  Asynchronous on `stream`. */
+#define GEO_MAX_BATCH_FRAMES 8
+int geo_render_band_set_frames(geo_ctx* ctx, const geo_frame* frames, uint32_t nframes, const geo_scene* scene,
+                               uint32_t width, uint32_t height, uint32_t band_rows, uint32_t row0,
+                               uint32_t row_stride, uint32_t nbands, uint8_t* out_rgba8, size_t out_frame_stride,
+                               unsigned long long* steps_total, void* stream);
 
 /* Rank 0's reassembly for the LEAD layout (multi-GPU present with rank 0
  * taking a larger share: it renders but never sends its rows, while the peers'

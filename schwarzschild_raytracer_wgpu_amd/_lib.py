@@ -29,6 +29,7 @@ GEO_ADAPTIVE_MAX_GROWTH = 16
 GEO_FLAG_DEFER_STEPS = 1
 GEO_FLAG_COMPOSITE = 2
 GEO_FLAG_MIPS = 4
+GEO_MAX_BATCH_FRAMES = 8
 
 GEO_RAYS_NEAR = 1
 GEO_RAYS_FAR = 2
@@ -95,6 +96,11 @@ SIGNATURES = {
         _int,
         [_vp, ctypes.POINTER(GeoFrame), ctypes.POINTER(GeoScene), _u32, _u32, _u32, _u32, _u32, _u32, _vp,
          _vp, _vp, _vp, _vp, _vp],
+    ),
+    "geo_render_band_set_frames": (
+        _int,
+        [_vp, ctypes.POINTER(GeoFrame), _u32, ctypes.POINTER(GeoScene), _u32, _u32, _u32, _u32, _u32, _u32, _vp,
+         ctypes.c_size_t, _vp, _vp],
     ),
     "geo_steps_flush": (_int, [_vp, _vp, _vp]),
     "geo_set_tile_order": (_int, [_vp, _u32, _u32, _vp]),

@@ -204,6 +204,26 @@ class Context:
             _stream_handle(stream)))
 
 
+    def render_band_set_frames(self, frames, scene: GeoScene, width: int, height: int, band_rows: int, row0: int,
+                               row_stride: int, nbands: int, out_rgba, frame_stride: int | None = None,
+                               steps_total=None, stream=None) -> None:
+        """geo_render_band_set_frames: len(frames) (1 .. GEO_MAX_BATCH_FRAMES) frames of one scene in one
+        launch; frame f's packed bands at byte f*frame_stride of out_rgba (default: packed back to back).
+        Colour only."""
+        n = len(frames)
+        if not 1 <= n <= _lib.GEO_MAX_BATCH_FRAMES:
+            raise ValueError(f"1 .. {_lib.GEO_MAX_BATCH_FRAMES} frames per batch")
+        fbytes = nbands * band_rows * width * 4
+        frame_stride = fbytes if frame_stride is None else frame_stride
+        import torch
+
+        _check_buffer("out_rgba", out_rgba, (n - 1) * frame_stride + fbytes)
+        _check_buffer("steps_total", steps_total, 8, (torch.int64, torch.uint64))
+        arr = (GeoFrame * n)(*frames)
+        check("geo_render_band_set_frames", lib.geo_render_band_set_frames(
+            self._h, arr, n, ctypes.byref(scene), width, height, band_rows, row0, row_stride, nbands,
+            _ptr(out_rgba), frame_stride, _ptr(steps_total), _stream_handle(stream)))
+
     def render_bands(self, frame: GeoFrame, scene: GeoScene, width: int, height: int, band_rows: int, band0: int,
                      band_step: int, nbands: int, out_rgba, out_mask=None, out_uv=None, out_steps=None,
                      steps_total=None, stream=None) -> None:

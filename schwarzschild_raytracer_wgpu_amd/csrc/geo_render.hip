@@ -66,9 +66,22 @@ constexpr int kSlotStride = 16;          // u64 per slot = 128 B (own cache line
 constexpr size_t kSlotSetU64 = (size_t)kStepSlots * kSlotStride;  // one set of sharded counters
 constexpr int kSlotSets = 1 + geo_ctx::kStepCallSets;            // the DEFER accumulator + per-call sets
 
-struct RenderArgs {
+// The per-frame part of a launch: the uniform and the camera constants the
+// host derives from it (a second kernel argument, FrameBatch, one per frame
+// of a batched launch, geo_render_band_set_frames).
+struct FrameK {
     geo_frame frame;
-    geo::PixelConsts k;  // frame constants, evaluated once on the host (IEEE f32, same bits)
+    geo::CameraConsts cam;  // the pixel's camera ray (geo::camera_consts)
+    float kt;               // geo::aberration_kt
+};
+constexpr uint32_t kMaxBatchFrames = GEO_MAX_BATCH_FRAMES;
+template <uint32_t NF>
+struct FrameBatch {
+    FrameK f[NF];
+};
+
+struct RenderArgs {
+    geo::PixelConsts k;  // scene constants, evaluated once on the host (IEEE f32, same bits)
     uint32_t width, height, row0, nrows;
     uint32_t tile_y0;  // first tile row of this launch (launch_tiles)
     // dispatch order (geo_ctx): workgroup i draws tile
@@ -83,8 +96,6 @@ struct RenderArgs {
     uint32_t band_rows, band_magic, band_stride;
     uint32_t sky_opaque;
     uint32_t composite;  // GEO_FLAG_COMPOSITE
-    geo::CameraConsts cam;  // the pixel's camera ray, frame constants (geo::camera_consts)
-    float kt;
     const uint32_t* sky;  // padded (geo::pad_sky): (sky_w + 2) x (sky_h + 2) texels
     uint32_t sky_w, sky_h;
     float sky_w256, sky_h256;  // sky_w * 256, sky_h * 256 (exact; geo::sample_sky_quad_f)
@@ -102,6 +113,7 @@ struct RenderArgs {
     float2* out_uv;
     uint32_t* out_steps;
     unsigned long long* step_slots;
+    uint64_t out_frame_px;  // batched launch: pixels from one frame's output to the next (colour only)
 };
 
 // MODE: GEO_MODE_DIRECT / GEO_MODE_FAN / GEO_MODE_ADAPTIVE; KIND: geo::kCurvedOut/kCurvedIn/kFlat
@@ -206,15 +218,15 @@ __device__ __forceinline__ float lane_xor16(float v) {
 
 // Epilogue of one pixel (shader.wgsl:88-105): black-hole test, sky UV,
 // bilinear sample, blend and the optional outputs at index o.
-__device__ __forceinline__ void shade_pixel(const RenderArgs& a, float c2x, float c2y, float ct, float rct,
-                                            float lam, uint32_t steps, size_t o) {
+__device__ __forceinline__ void shade_pixel(const RenderArgs& a, const float* central_to_uv, float c2x, float c2y,
+                                            float ct, float rct, float lam, uint32_t steps, size_t o) {
     const bool bh = lam < geo::kBlackHoleLambda;
     // A black-hole pixel is discarded (shader.wgsl:88): it needs its UV
     // only when the caller asks for it, so a wave inside the shadow skips
     // the sincos/atan2/asin and the sample (config 3 -0.3 %, config 5 -4.4 %)
     float U = 0.0f, V = 0.0f;
     if (!bh || a.out_uv)
-        geo::sky_uv(a.frame.central_to_uv, c2x, c2y, ct, rct, lam, &U, &V);
+        geo::sky_uv(central_to_uv, c2x, c2y, ct, rct, lam, &U, &V);
     const PaddedSkyQuad quad{__builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(a.sky), 0,
                                                                (int)a.sky_bytes, kBufferRsrcWord3),
                              a.sky_pitch_b};
@@ -282,7 +294,8 @@ __host__ __device__ constexpr uint32_t lane_rows(int mode, bool mips) {
 // 8-row-aligned group of the wave's rows, so in one band (band heights are
 // multiples of 8): the band mapping is per group, in scalar ops.
 template <uint32_t LR>
-__device__ __forceinline__ void fan_tile(const RenderArgs& a, uint2 tile, uint32_t wave, uint32_t lane) {
+__device__ __forceinline__ void fan_tile(const RenderArgs& a, const FrameK& f, size_t obase, uint2 tile, uint32_t wave,
+                                         uint32_t lane) {
     static_assert(LR % 2 == 0 && LR * kWaveRows % 8 == 0, "pixel pairs fill 8-row groups");
     const uint32_t px = tile.x * kTileW + (wave % kWavesX) * kWaveW + lane % kWaveW;
     const uint32_t wl0 = tile.y * (kTileH * LR) + (wave / kWavesX) * (kWaveRows * LR);
@@ -302,7 +315,7 @@ __device__ __forceinline__ void fan_tile(const RenderArgs& a, uint2 tile, uint32
 #pragma unroll
     for (uint32_t k = 0; k < LR; ++k) {
         float c2z;
-        geo::pixel_central_dir(a.cam, a.frame.movement_to_central, a.frame.psi_factor_and_position[0], a.kt, px,
+        geo::pixel_central_dir(f.cam, f.frame.movement_to_central, f.frame.psi_factor_and_position[0], f.kt, px,
                                py[k], &c2x[k], &c2y[k], &c2z);
         st[k] = geo::central_sin(c2z);
         ct[k] = geo::central_rho(c2x[k], c2y[k]);
@@ -332,7 +345,7 @@ __device__ __forceinline__ void fan_tile(const RenderArgs& a, uint2 tile, uint32
             float U[LR], V[LR];
 #pragma unroll
             for (uint32_t k = 0; k < LR; ++k)
-                geo::sky_uv(a.frame.central_to_uv, c2x[k], c2y[k], ct[k], rct[k], lam[k], &U[k], &V[k]);
+                geo::sky_uv(f.frame.central_to_uv, c2x[k], c2y[k], ct[k], rct[k], lam[k], &U[k], &V[k]);
             const PaddedSkyQuad quad{__builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(a.sky), 0,
                                                                        (int)a.sky_bytes, kBufferRsrcWord3),
                                      a.sky_pitch_b};
@@ -345,17 +358,24 @@ __device__ __forceinline__ void fan_tile(const RenderArgs& a, uint2 tile, uint32
         }
 #pragma unroll
         for (uint32_t k = 0; k < LR; ++k)
-            if (in[k]) a.out_rgba[(size_t)ly[k] * a.width + px] = rgba[k];
+            if (in[k]) a.out_rgba[obase + (size_t)ly[k] * a.width + px] = rgba[k];
     } else {
 #pragma unroll
         for (uint32_t k = 0; k < LR; ++k)
-            if (in[k]) shade_pixel(a, c2x[k], c2y[k], ct[k], rct[k], lam[k], 0u, (size_t)ly[k] * a.width + px);
+            if (in[k])
+                shade_pixel(a, f.frame.central_to_uv, c2x[k], c2y[k], ct[k], rct[k], lam[k], 0u,
+                            obase + (size_t)ly[k] * a.width + px);
     }
 }
 
-template <int MODE, int KIND, bool MIPS>
-__global__ __launch_bounds__(kBlock) void geo_render_kernel(const RenderArgs a) {
+// NF: frames of the launch (FrameBatch; 1, or up to kMaxBatchFrames with the
+// frame in blockIdx.z and its output a.out_frame_px pixels after the last's).
+template <int MODE, int KIND, bool MIPS, uint32_t NF>
+__global__ __launch_bounds__(kBlock) void geo_render_kernel(const RenderArgs a, const FrameBatch<NF> fb) {
     constexpr uint32_t LR = lane_rows(MODE, MIPS);
+    const uint32_t z = NF > 1 ? blockIdx.z : 0u;
+    const FrameK& f = fb.f[z];
+    const size_t obase = NF > 1 ? (size_t)z * a.out_frame_px : 0;
     uint2 tile = make_uint2(blockIdx.x, a.tile_y0 + blockIdx.y);
     if (a.tile_order) {
         const uint32_t t = a.tile_order[blockIdx.y * gridDim.x + blockIdx.x];  // one scalar load
@@ -375,17 +395,17 @@ __global__ __launch_bounds__(kBlock) void geo_render_kernel(const RenderArgs a) 
     uint32_t steps = 0;
     const bool in_frame = px < a.width && ly < a.nrows && py < a.height;
     if constexpr (LR > 1) {
-        fan_tile<LR>(a, tile, wave, lane);
+        fan_tile<LR>(a, f, obase, tile, wave, lane);
     } else if constexpr (!MIPS) {
         if (in_frame) {
             float c2x, c2y, c2z;
-            geo::pixel_central_dir(a.cam, a.frame.movement_to_central, a.frame.psi_factor_and_position[0], a.kt, px,
+            geo::pixel_central_dir(f.cam, f.frame.movement_to_central, f.frame.psi_factor_and_position[0], f.kt, px,
                                    py, &c2x, &c2y, &c2z);
             const float st = geo::central_sin(c2z);
             const float ct = geo::central_rho(c2x, c2y);
             const float rct = geo::rcpf_(ct);  // shared by the ray's 1/b^2 and its sky direction
             const float lam = pixel_lambda<MODE, KIND>(a, st, ct, rct, &steps);
-            shade_pixel(a, c2x, c2y, ct, rct, lam, steps, (size_t)ly * a.width + px);
+            shade_pixel(a, f.frame.central_to_uv, c2x, c2y, ct, rct, lam, steps, obase + (size_t)ly * a.width + px);
         }
     } else {
         // Every lane traces its pixel, the ones outside the frame or the
@@ -394,7 +414,7 @@ __global__ __launch_bounds__(kBlock) void geo_render_kernel(const RenderArgs a) 
         // Black-hole pixels keep their UV as well (textureSample runs before
         // the discard, shader.wgsl:101-104).
         float c2x, c2y, c2z;
-        geo::pixel_central_dir(a.cam, a.frame.movement_to_central, a.frame.psi_factor_and_position[0], a.kt, px, py,
+        geo::pixel_central_dir(f.cam, f.frame.movement_to_central, f.frame.psi_factor_and_position[0], f.kt, px, py,
                                &c2x, &c2y, &c2z);
         const float st = geo::central_sin(c2z);
         const float ct = geo::central_rho(c2x, c2y);
@@ -406,12 +426,12 @@ __global__ __launch_bounds__(kBlock) void geo_render_kernel(const RenderArgs a) 
         // footprint (a wave-uniform branch)
         float U = 0.0f, V = 0.0f, rho2 = 0.0f;
         if (geo::ballot_(!(lam < geo::kBlackHoleLambda)) != 0 || a.out_uv) {
-            geo::sky_uv(a.frame.central_to_uv, c2x, c2y, ct, rct, lam, &U, &V);
+            geo::sky_uv(f.frame.central_to_uv, c2x, c2y, ct, rct, lam, &U, &V);
             const float ux = lane_xor1(U), vx = lane_xor1(V), uy = lane_xor16(U), vy = lane_xor16(V);
             rho2 = geo::mip_rho2(U - ux, V - vx, U - uy, V - vy, a.sky_wf, a.sky_hf);
         }
         if (in_frame)
-            shade_pixel_mips(a, lam, U, V, rho2, steps, (size_t)ly * a.width + px);
+            shade_pixel_mips(a, lam, U, V, rho2, steps, obase + (size_t)ly * a.width + px);
         else
             steps = 0;
     }
@@ -426,9 +446,10 @@ __global__ __launch_bounds__(kBlock) void geo_render_kernel(const RenderArgs a) 
             if ((threadIdx.x & 63) == 0 && total)
                 atomicAdd(&a.step_slots[slot * kSlotStride], (unsigned long long)total);
         }
-        if (a.tile_cost) {
+        if (a.tile_cost && z == 0u) {
             // a wave holds its slot until its slowest lane stops: the tile's
-            // cost is the sum of its waves' largest step counts
+            // cost is the sum of its waves' largest step counts (frame 0's
+            // of a batch: the order is per tile)
             const uint32_t wmax = wave_max_u32(steps);
             if ((threadIdx.x & 63) == 0)
                 atomicAdd(&a.tile_cost[tile.y * gridDim.x + tile.x], wmax + a.cost_overhead);
@@ -1130,25 +1151,49 @@ extern "C++" {
 // render (geo_time_next_render) puts the caller's start event on the first
 // launch's dispatch and its stop event on the last one's, and records `done`
 // after it.
-template <int MODE, int KIND>
-static int launch_tiles(RenderArgs a, bool mips, uint32_t tiles_x, uint32_t tiles_y, hipStream_t s,
-                        hipEvent_t done, hipEvent_t t_start, hipEvent_t t_stop) {
+template <int MODE, int KIND, uint32_t NF>
+static int launch_tiles(RenderArgs a, const FrameBatch<NF>& fb, uint32_t nframes, bool mips, uint32_t tiles_x,
+                        uint32_t tiles_y, hipStream_t s, hipEvent_t done, hipEvent_t t_start, hipEvent_t t_stop) {
     for (uint32_t y0 = 0; y0 < tiles_y; y0 += kMaxGridY) {
         a.tile_y0 = y0;
         const uint32_t ny = tiles_y - y0 < kMaxGridY ? tiles_y - y0 : kMaxGridY;
         const bool last = y0 + ny >= tiles_y;
         hipEvent_t start = y0 == 0 ? t_start : nullptr;
         hipEvent_t stop = last ? (t_stop ? t_stop : done) : nullptr;
-        if (mips)
-            hipExtLaunchKernelGGL((geo_render_kernel<MODE, KIND, true>), dim3(tiles_x, ny), dim3(kBlock), 0, s,
-                                  start, stop, 0, a);
-        else
-            hipExtLaunchKernelGGL((geo_render_kernel<MODE, KIND, false>), dim3(tiles_x, ny), dim3(kBlock), 0, s,
-                                  start, stop, 0, a);
+        const dim3 grid(tiles_x, ny, nframes);
+        if constexpr (NF == 1) {
+            if (mips)
+                hipExtLaunchKernelGGL((geo_render_kernel<MODE, KIND, true, 1>), grid, dim3(kBlock), 0, s, start, stop,
+                                      0, a, fb);
+            else
+                hipExtLaunchKernelGGL((geo_render_kernel<MODE, KIND, false, 1>), grid, dim3(kBlock), 0, s, start,
+                                      stop, 0, a, fb);
+        } else {
+            hipExtLaunchKernelGGL((geo_render_kernel<MODE, KIND, false, NF>), grid, dim3(kBlock), 0, s, start, stop,
+                                  0, a, fb);
+        }
         if (hipGetLastError() != hipSuccess) return GEO_EHIP;
     }
     if (t_stop && hipEventRecord(done, s) != hipSuccess) return GEO_EHIP;
     return GEO_OK;
+}
+
+// One frame (FrameBatch<1>, the kernel arguments as before batching), or a
+// batch of 2 .. kMaxBatchFrames in one launch (FrameBatch<kMaxBatchFrames>,
+// the frame in blockIdx.z; no mip-mapped sampler).
+template <int MODE, int KIND>
+static int launch_frames(const RenderArgs& a, const FrameK* fk, uint32_t nframes, bool mips, uint32_t tiles_x,
+                         uint32_t tiles_y, hipStream_t s, hipEvent_t done, hipEvent_t t_start, hipEvent_t t_stop) {
+    if (nframes == 1) {
+        FrameBatch<1> fb;
+        fb.f[0] = fk[0];
+        return launch_tiles<MODE, KIND, 1>(a, fb, 1, mips, tiles_x, tiles_y, s, done, t_start, t_stop);
+    }
+    FrameBatch<kMaxBatchFrames> fb;
+    std::memset(&fb, 0, sizeof(fb));
+    for (uint32_t i = 0; i < nframes; ++i) fb.f[i] = fk[i];
+    return launch_tiles<MODE, KIND, kMaxBatchFrames>(a, fb, nframes, false, tiles_x, tiles_y, s, done, t_start,
+                                                     t_stop);
 }
 }
 
@@ -1185,16 +1230,22 @@ static int ensure_tiles(geo_ctx* c, uint32_t n) {
     return GEO_OK;
 }
 
-static int render_impl(geo_ctx* c, const geo_frame* frame, const geo_scene* scene, uint32_t width,
-                       uint32_t height, uint32_t row0, uint32_t nrows, uint32_t band_rows,
-                       uint32_t band_stride, uint8_t* out_rgba8, uint8_t* out_mask, float* out_uv,
-                       uint32_t* out_steps, unsigned long long* steps_total, void* stream) {
+// frames: nframes uniforms (1 .. kMaxBatchFrames); frame f's output starts
+// out_frame_stride bytes after frame f - 1's (a batch draws colour only).
+static int render_impl(geo_ctx* c, const geo_frame* frames, uint32_t nframes, size_t out_frame_stride,
+                       const geo_scene* scene, uint32_t width, uint32_t height, uint32_t row0, uint32_t nrows,
+                       uint32_t band_rows, uint32_t band_stride, uint8_t* out_rgba8, uint8_t* out_mask,
+                       float* out_uv, uint32_t* out_steps, unsigned long long* steps_total, void* stream) {
     if (scene->mode != GEO_MODE_DIRECT && scene->mode != GEO_MODE_FAN && scene->mode != GEO_MODE_ADAPTIVE)
         return GEO_EINVAL;
     if ((scene->flags & ~(GEO_FLAG_DEFER_STEPS | GEO_FLAG_COMPOSITE | GEO_FLAG_MIPS)) != 0) return GEO_EINVAL;
     // frame-aligned 2 x 2 quads: the rows a wave covers start on even frame rows
     const bool mips = (scene->flags & GEO_FLAG_MIPS) != 0;
     if (mips && ((row0 | band_stride) & 1u) != 0) return GEO_EINVAL;
+    if (nframes == 0 || nframes > kMaxBatchFrames) return GEO_EINVAL;
+    if (nframes > 1 && (mips || out_mask || out_uv || out_steps || out_frame_stride % 4u != 0 ||
+                        out_frame_stride < (size_t)nrows * width * 4u))
+        return GEO_EINVAL;
     const bool adaptive = scene->mode == GEO_MODE_ADAPTIVE;
     // tol: 0 (default) or a positive finite tolerance in the adaptive mode, 0 otherwise
     if (adaptive ? !(scene->tol >= 0.0f && scene->tol <= 3.0e38f) : scene->tol != 0.0f) return GEO_EINVAL;
@@ -1210,7 +1261,14 @@ static int render_impl(geo_ctx* c, const geo_frame* frame, const geo_scene* scen
     DeviceGuard g(c->device);
     if (!g.ok) return GEO_EHIP;
     RenderArgs a;
-    std::memcpy(&a.frame, frame, sizeof(geo_frame));
+    FrameK fk[kMaxBatchFrames];
+    for (uint32_t i = 0; i < nframes; ++i) {
+        const geo_frame& fr = frames[i];
+        std::memcpy(&fk[i].frame, &fr, sizeof(geo_frame));
+        fk[i].cam = geo::camera_consts(fr.display_to_movement, fr.movement_to_central, width, height);
+        fk[i].kt = geo::aberration_kt(fr.psi_factor_and_position[0]);
+    }
+    a.out_frame_px = out_frame_stride / 4u;
     a.k = geo::make_consts(scene->rs, scene->sphere_r, scene->r_obs, scene->step, scene->max_steps, scene->tol);
     a.width = width;
     a.height = height;
@@ -1222,8 +1280,6 @@ static int render_impl(geo_ctx* c, const geo_frame* frame, const geo_scene* scen
     a.sky_opaque = c->sky_opaque ? 1u : 0u;
     a.composite = (scene->flags & GEO_FLAG_COMPOSITE) ? 1u : 0u;
     const uint32_t tiles_x = (width + kTileW - 1) / kTileW;
-    a.cam = geo::camera_consts(frame->display_to_movement, frame->movement_to_central, width, height);
-    a.kt = geo::aberration_kt(frame->psi_factor_and_position[0]);
     const uint32_t tile_h = kTileH * lane_rows(scene->mode, mips);
     const uint32_t tiles_y = (nrows + tile_h - 1) / tile_h;
     a.sky = c->sky;
@@ -1317,7 +1373,7 @@ static int render_impl(geo_ctx* c, const geo_frame* frame, const geo_scene* scen
         // writer waits for its readers on the host, so they need no event)
         const bool by_slot = !c->fan_written_rec[fb] || c->fan_writer[fb] == s;
         if (!by_slot && hipStreamWaitEvent(s, c->fan_written[fb], 0) != hipSuccess) return GEO_EHIP;
-        st = launch_tiles<GEO_MODE_FAN, geo::kCurvedOut>(a, mips, tiles_x, tiles_y, s, done, t_start, t_stop);
+        st = launch_frames<GEO_MODE_FAN, geo::kCurvedOut>(a, fk, nframes, mips, tiles_x, tiles_y, s, done, t_start, t_stop);
         if (st) return st;
         if (by_slot) {
             c->fan_read_slots[fb] |= 1u << slot;
@@ -1331,15 +1387,15 @@ static int render_impl(geo_ctx* c, const geo_frame* frame, const geo_scene* scen
         }
     } else if (adaptive) {
         switch (geo::geodesic_kind(a.k)) {
-            case geo::kCurvedOut: st = launch_tiles<GEO_MODE_ADAPTIVE, geo::kCurvedOut>(a, mips, tiles_x, tiles_y, s, done, t_start, t_stop); break;
-            case geo::kCurvedIn: st = launch_tiles<GEO_MODE_ADAPTIVE, geo::kCurvedIn>(a, mips, tiles_x, tiles_y, s, done, t_start, t_stop); break;
-            default: st = launch_tiles<GEO_MODE_ADAPTIVE, geo::kFlat>(a, mips, tiles_x, tiles_y, s, done, t_start, t_stop);
+            case geo::kCurvedOut: st = launch_frames<GEO_MODE_ADAPTIVE, geo::kCurvedOut>(a, fk, nframes, mips, tiles_x, tiles_y, s, done, t_start, t_stop); break;
+            case geo::kCurvedIn: st = launch_frames<GEO_MODE_ADAPTIVE, geo::kCurvedIn>(a, fk, nframes, mips, tiles_x, tiles_y, s, done, t_start, t_stop); break;
+            default: st = launch_frames<GEO_MODE_ADAPTIVE, geo::kFlat>(a, fk, nframes, mips, tiles_x, tiles_y, s, done, t_start, t_stop);
         }
     } else {
         switch (geo::geodesic_kind(a.k)) {
-            case geo::kCurvedOut: st = launch_tiles<GEO_MODE_DIRECT, geo::kCurvedOut>(a, mips, tiles_x, tiles_y, s, done, t_start, t_stop); break;
-            case geo::kCurvedIn: st = launch_tiles<GEO_MODE_DIRECT, geo::kCurvedIn>(a, mips, tiles_x, tiles_y, s, done, t_start, t_stop); break;
-            default: st = launch_tiles<GEO_MODE_DIRECT, geo::kFlat>(a, mips, tiles_x, tiles_y, s, done, t_start, t_stop);
+            case geo::kCurvedOut: st = launch_frames<GEO_MODE_DIRECT, geo::kCurvedOut>(a, fk, nframes, mips, tiles_x, tiles_y, s, done, t_start, t_stop); break;
+            case geo::kCurvedIn: st = launch_frames<GEO_MODE_DIRECT, geo::kCurvedIn>(a, fk, nframes, mips, tiles_x, tiles_y, s, done, t_start, t_stop); break;
+            default: st = launch_frames<GEO_MODE_DIRECT, geo::kFlat>(a, fk, nframes, mips, tiles_x, tiles_y, s, done, t_start, t_stop);
         }
     }
     if (st) return st;
@@ -1531,7 +1587,7 @@ int geo_render_rows(geo_ctx* c, const geo_frame* frame, const geo_scene* scene, 
     if ((uint64_t)row0 + nrows > height || width > (1u << 20) || height > (1u << 20))
         return GEO_EINVAL;
     // one band covering every row (2^21 >= nrows)
-    return render_impl(c, frame, scene, width, height, row0, nrows, 1u << 21, 1u << 21, out_rgba8, out_mask,
+    return render_impl(c, frame, 1, 0, scene, width, height, row0, nrows, 1u << 21, 1u << 21, out_rgba8, out_mask,
                        out_uv, out_steps, steps_total, stream);
 }
 
@@ -1547,26 +1603,43 @@ int geo_render_bands(geo_ctx* c, const geo_frame* frame, const geo_scene* scene,
     const uint64_t last = first + (uint64_t)(nbands - 1) * band_step * band_rows;
     const uint64_t nrows = (uint64_t)nbands * band_rows;
     if (first >= height || last >= height || nrows > (1u << 20)) return GEO_EINVAL;
-    return render_impl(c, frame, scene, width, height, (uint32_t)first, (uint32_t)nrows,
+    return render_impl(c, frame, 1, 0, scene, width, height, (uint32_t)first, (uint32_t)nrows,
                        band_rows, band_step * band_rows, out_rgba8, out_mask, out_uv,
                        out_steps, steps_total, stream);
+}
+
+// The band set's arguments, checked (geo_render_band_set, geo_render_band_set_frames).
+static bool band_set_ok(uint32_t width, uint32_t height, uint32_t band_rows, uint32_t row0, uint32_t row_stride,
+                        uint32_t nbands) {
+    // band_rows: a multiple of 8, at most 4096 unless a power of two (band_rows_magic)
+    if (width == 0 || height == 0 || band_rows == 0 || nbands == 0 || row_stride < band_rows ||
+        band_rows % kBandRowAlign != 0 || ((band_rows & (band_rows - 1)) != 0 && band_rows > 4096u))
+        return false;
+    if (width > (1u << 20) || height > (1u << 20)) return false;
+    const uint64_t last = (uint64_t)row0 + (uint64_t)(nbands - 1) * row_stride;
+    const uint64_t nrows = (uint64_t)nbands * band_rows;
+    return row0 < height && last < height && nrows <= (1u << 20);
 }
 
 int geo_render_band_set(geo_ctx* c, const geo_frame* frame, const geo_scene* scene, uint32_t width,
                         uint32_t height, uint32_t band_rows, uint32_t row0, uint32_t row_stride, uint32_t nbands,
                         uint8_t* out_rgba8, uint8_t* out_mask, float* out_uv, uint32_t* out_steps,
                         unsigned long long* steps_total, void* stream) {
-    // band_rows: a multiple of 8, at most 4096 unless a power of two (band_rows_magic)
-    if (!c || !frame || !scene || !out_rgba8 || width == 0 || height == 0 || band_rows == 0 || nbands == 0 ||
-        row_stride < band_rows || band_rows % kBandRowAlign != 0 ||
-        ((band_rows & (band_rows - 1)) != 0 && band_rows > 4096u))
+    if (!c || !frame || !scene || !out_rgba8 || !band_set_ok(width, height, band_rows, row0, row_stride, nbands))
         return GEO_EINVAL;
-    if (width > (1u << 20) || height > (1u << 20)) return GEO_EINVAL;
-    const uint64_t last = (uint64_t)row0 + (uint64_t)(nbands - 1) * row_stride;
-    const uint64_t nrows = (uint64_t)nbands * band_rows;
-    if (row0 >= height || last >= height || nrows > (1u << 20)) return GEO_EINVAL;
-    return render_impl(c, frame, scene, width, height, row0, (uint32_t)nrows, band_rows, row_stride, out_rgba8,
-                       out_mask, out_uv, out_steps, steps_total, stream);
+    return render_impl(c, frame, 1, 0, scene, width, height, row0, nbands * band_rows, band_rows, row_stride,
+                       out_rgba8, out_mask, out_uv, out_steps, steps_total, stream);
+}
+
+int geo_render_band_set_frames(geo_ctx* c, const geo_frame* frames, uint32_t nframes, const geo_scene* scene,
+                               uint32_t width, uint32_t height, uint32_t band_rows, uint32_t row0,
+                               uint32_t row_stride, uint32_t nbands, uint8_t* out_rgba8, size_t out_frame_stride,
+                               unsigned long long* steps_total, void* stream) {
+    if (!c || !frames || !scene || !out_rgba8 || nframes == 0 || nframes > kMaxBatchFrames ||
+        !band_set_ok(width, height, band_rows, row0, row_stride, nbands))
+        return GEO_EINVAL;
+    return render_impl(c, frames, nframes, out_frame_stride, scene, width, height, row0, nbands * band_rows,
+                       band_rows, row_stride, out_rgba8, nullptr, nullptr, nullptr, steps_total, stream);
 }
 
 }  // extern "C"

@@ -192,13 +192,18 @@ class ShardedFrame:
 
     def __init__(self, ctx, frame, scene, width: int, height: int, band_rows: int, rank: int, world: int, device,
                  dist=None, host_gather: bool = False, frames_per_gather: int = 1, render_streams: int = 1,
-                 present_rgb: bool = True, lead: int = 1):
+                 present_rgb: bool = True, lead: int = 1, batch_launch: bool = False):
         """host_gather: stage through host memory (gloo backend; rehearsals only).
         present_rgb: peers send RGB24 (geo_pack_rgb after each render; 25 %
         fewer bytes on the links) when the width is a multiple of 4.
         lead: rank 0's band height in band_rows (BandLayout); rank 0 never
         sends its own rows, its reassembly reads them from its local bands
-        (geo_assemble_lead)."""
+        (geo_assemble_lead).
+        batch_launch: render each batch's K frames in ONE launch
+        (geo_render_band_set_frames) when it is complete, on render stream
+        (batch buffer % S): a launch's fixed cost (dispatch, ramp, drain;
+        ~12.6 us) is paid once per batch instead of per frame,
+        which at N = 8 is a third of a rank's share.  K <= GEO_MAX_BATCH_FRAMES."""
         import torch
 
         from ._lib import lib
@@ -212,6 +217,13 @@ class ShardedFrame:
         self.rank, self.world, self.dist = rank, world, dist
         self.K = max(1, int(frames_per_gather)) if world > 1 else 1
         self.S = min(2, max(1, int(render_streams)))
+        from ._lib import GEO_MAX_BATCH_FRAMES
+
+        self.batch = bool(batch_launch) and self.K > 1
+        if self.batch and self.K > GEO_MAX_BATCH_FRAMES:
+            raise ValueError(f"batch_launch: at most {GEO_MAX_BATCH_FRAMES} frames per gather")
+        self.pending_frames = []     # batch mode: the open batch's uniforms
+        self.pending_scene = None    # and the scene its steps passed
         L = self.layout
         self.row_bytes = width * 4
         # one frame's packed bands: rank 0's share, or the largest peer share
@@ -259,6 +271,7 @@ class ShardedFrame:
         self._frame_ref = ctypes.byref(frame)
         self._scene_ref = ctypes.byref(scene)
         self._band = (L.band_height(), L.row0(), L.cycle_rows, L.nbands())
+        self._frame_arr = None  # batch mode: the uniforms of the last batch launched (kept alive for ctypes)
         self._lv = [[self.bufs[b].data_ptr() + sub * self.slice for sub in range(self.K)] for b in range(2)]
         self._sv = [[self.sbufs[b].data_ptr() + sub * self.tslice for sub in range(self.K)] for b in range(2)]
         self.pending = [None, None]  # (work, nframes, batch number, streams that rendered) per batch buffer
@@ -286,8 +299,29 @@ class ShardedFrame:
                                src_bpp=self.bpp, stream=stream)
 
     def _render_stream(self, i: int):
-        k = i % self.S
+        k = (i // self.K) % 2 % self.S if self.batch else i % self.S
         return self.stream0 if k == 0 else self.extra[k - 1]
+
+    def render_batch(self, b: int, frames, scene=None, events=None, stream=None) -> None:
+        """The frames of batch buffer b (slots 0 .. len(frames) - 1) in one
+        launch (geo_render_band_set_frames), on `stream` (a handle; default the
+        buffer's render stream)."""
+        import ctypes
+
+        from ._lib import GeoFrame, check
+
+        band_h, row0, cycle, nb = self._band
+        if not nb:
+            return
+        sh = self._sh[b % self.S] if stream is None else stream
+        if events is not None:
+            self.lib.geo_time_next_render(self._ctx_h, events[0].h, events[1].h)
+        self._frame_arr = (GeoFrame * len(frames))(*frames)
+        st = self.lib.geo_render_band_set_frames(
+            self._ctx_h, self._frame_arr, len(frames), self._scene_ref if scene is None else ctypes.byref(scene),
+            self.width, self.height, band_h, row0, cycle, nb, self._lv[b][0], self.slice, None, sh)
+        if st != 0:
+            check("geo_render_band_set_frames", st)
 
     def _join(self) -> None:
         """The current stream waits for every render stream."""
@@ -352,10 +386,49 @@ class ShardedFrame:
         if self.last is None or seq > self.last[0]:
             self.last = (seq, b, n - 1)
 
-    def step(self, i: int, steps_total=None, events=None, scene=None) -> None:
+    def _step_batch(self, b: int, sub: int, events, scene, frame) -> None:
+        """Batch mode: record frame `sub` of the open batch; at its K-th frame
+        render the batch in one launch, pack it (peers) and launch its gather."""
+        self.pending_frames.append(self.frame if frame is None else frame)
+        self.pending_scene = scene  # a partial batch flushed by drain() keeps the steps' scene
+        self.rendered = sub + 1
+        self.open = b
+        if sub == self.K - 1:
+            self._flush_batch(b, events, scene)
+            self._launch(b, self.K)
+            self.rendered = 0
+
+    def _flush_batch(self, b: int, events=None, scene=None) -> None:
+        n = len(self.pending_frames)
+        scene = self.pending_scene if scene is None else scene
+        k = b % self.S
+        sh = self._sh[k]
+        self.ev_free[b].wait(sh)
+        self.render_batch(b, self.pending_frames, scene=scene, events=events, stream=sh)
+        self.pending_frames = []
+        if self.bpp == 3 and self.rank != 0:
+            st = self.lib.geo_pack_rgb(self._ctx_h, self._lv[b][0], n * self.slice // 4, self._sv[b][0], sh)
+            if st != 0:
+                from ._lib import check
+
+                check("geo_pack_rgb", st)
+        if self.world > 1:
+            self.ev_rendered[b][k].record(sh)
+            self.rendered_in[b][k] = True
+
+    def step(self, i: int, steps_total=None, events=None, scene=None, frame=None) -> None:
+        """Frame i: its bands rendered (batch mode: recorded, and the batch
+        rendered in one launch at its K-th frame; `events` time that launch)
+        into slot i % K of batch buffer (i // K) % 2.  frame: this frame's
+        uniform (default the one the object was built with)."""
         b, sub = (i // self.K) % 2, i % self.K
         if sub == 0:
             self._retire(b)  # the batch that used this buffer two batches ago
+        if self.batch:
+            if steps_total is not None:
+                raise ValueError("batch mode counts steps with GEO_FLAG_DEFER_STEPS only")
+            self._step_batch(b, sub, events, scene, frame)
+            return
         k = i % self.S
         sh = self._sh[k]
         if sub < self.S:
@@ -367,7 +440,8 @@ class ShardedFrame:
             lib.geo_time_next_render(self._ctx_h, events[0].h, events[1].h)
         if nb:
             st = lib.geo_render_band_set(
-                self._ctx_h, self._frame_ref, self._scene_ref if scene is None else ctypes.byref(scene), self.width,
+                self._ctx_h, self._frame_ref if frame is None else ctypes.byref(frame),
+                self._scene_ref if scene is None else ctypes.byref(scene), self.width,
                 self.height, band_h, row0, cycle, nb, self._lv[b][sub], None, None, None,
                 None if steps_total is None else steps_total.data_ptr(), sh)
             if st != 0:
@@ -392,6 +466,8 @@ class ShardedFrame:
     def drain(self) -> None:
         """Finish every batch; afterwards the current stream is ordered after all work."""
         if self.rendered:  # a partial batch
+            if self.batch:
+                self._flush_batch(self.open)
             self._launch(self.open, self.rendered)
             self.rendered = 0
         for b in (0, 1):

@@ -37,7 +37,7 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_abi_and_status():
-    assert _lib.lib.geo_abi_version() == 3
+    assert _lib.lib.geo_abi_version() == 4
     assert _lib.status_str(0) == "ok"
     assert "invalid" in _lib.status_str(-1)
 
@@ -52,6 +52,12 @@ def test_null_args_rejected():
     assert lib.geo_ctx_create(0, None) == _lib.GEO_EINVAL
     assert lib.geo_render_rows(None, None, None, 1, 1, 0, 1, None, None, None, None, None, None) == _lib.GEO_EINVAL
     assert lib.geo_set_sky(None, None, 1, 1) == _lib.GEO_EINVAL
+    fr = (g.GeoFrame * 9)()
+    sc = g.GeoScene()
+    buf = ctypes.create_string_buffer(64)
+    for n in (0, _lib.GEO_MAX_BATCH_FRAMES + 1):  # batch sizes out of range, before any device work
+        assert lib.geo_render_band_set_frames(None, fr, n, ctypes.byref(sc), 8, 8, 8, 0, 8, 1, buf, 256, None,
+                                              None) == _lib.GEO_EINVAL
 
 
 def test_ctx_without_gpu_fails_loudly():

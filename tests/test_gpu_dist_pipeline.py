@@ -63,12 +63,13 @@ def _peer_bands(ctx, torch, frame, scene, W, H, B, r, world, lead, dev, bpp):
     return one
 
 
+@pytest.mark.parametrize("batch", [False, True], ids=["per-frame", "batched"])
 @pytest.mark.parametrize("rgb", [True, False], ids=["rgb24", "rgba8"])
 @pytest.mark.parametrize("S", [1, 2])
 @pytest.mark.parametrize("world,K,nframes,lead", [(2, 4, 41, 1), (3, 3, 10, 1), (8, 4, 16, 1), (8, 1, 5, 1),
                                                   (2, 4, 13, 2), (2, 2, 7, 4), (4, 3, 10, 2), (8, 4, 9, 2),
                                                   (8, 2, 6, 4), (2, 3, 8, 3), (8, 4, 9, 3), (4, 2, 5, 6)])
-def test_rank0_pipeline_assembles_frames(world, K, nframes, lead, S, rgb):
+def test_rank0_pipeline_assembles_frames(world, K, nframes, lead, S, rgb, batch):
     import torch
 
     if not torch.cuda.is_available():
@@ -84,7 +85,8 @@ def test_rank0_pipeline_assembles_frames(world, K, nframes, lead, S, rgb):
     frame, scene = default_frame(W, H), default_scene(512)
     fake = FakeRcclGather(torch, [])
     sf = ShardedFrame(ctx, frame, scene, W, H, B, 0, world, dev, dist=fake, frames_per_gather=K, render_streams=S,
-                      present_rgb=rgb, lead=lead)
+                      present_rgb=rgb, lead=lead, batch_launch=batch)
+    assert sf.batch == (batch and K > 1)
     assert sf.side is not None and sf.bpp == (3 if rgb else 4) and sf.layout.lead == lead
     # the peers' K-frame batches (every frame identical), in the travelling format
     for r in range(1, world):
@@ -105,9 +107,10 @@ def test_rank0_pipeline_assembles_frames(world, K, nframes, lead, S, rgb):
         assert torch.equal(sf.frame_rgba(k), ref), k
 
 
+@pytest.mark.parametrize("batch", [False, True], ids=["per-frame", "batched"])
 @pytest.mark.parametrize("lead", [1, 2, 3])
 @pytest.mark.parametrize("S", [1, 2])
-def test_peer_rank_pipeline_runs_batches(S, lead):
+def test_peer_rank_pipeline_runs_batches(S, lead, batch):
     """A peer rank (rank 3 of 4): batches of K frames, each sent with one
     gather; the send buffer is re-rendered only after its gather completed."""
     import torch
@@ -141,7 +144,7 @@ def test_peer_rank_pipeline_runs_batches(S, lead):
     frame, scene = default_frame(W, H), default_scene(256)
     pg = PeerGather()
     sf = ShardedFrame(ctx, frame, scene, W, H, B, rank, world, dev, dist=pg, frames_per_gather=K, render_streams=S,
-                      lead=lead)
+                      lead=lead, batch_launch=batch)
     for i in range(10):
         sf.step(i)
     sf.drain()

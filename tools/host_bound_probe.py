@@ -5,7 +5,7 @@ gather stand-in that only orders streams (no copy, no links): the host time
 of the step loop against the wall time to drain it.  wall ~ host means the
 Python/HIP launch path, not the GPU, sets the per-frame time of that rank.
 
-  python tools/host_bound_probe.py [world] [lead] [K] [S] [frames]
+  python tools/host_bound_probe.py [world] [lead] [K] [S] [frames] [batch 0/1]
 """
 import os
 import sys
@@ -27,6 +27,7 @@ def main():
     K = int(sys.argv[3]) if len(sys.argv) > 3 else 4
     S = int(sys.argv[4]) if len(sys.argv) > 4 else 2
     n = int(sys.argv[5]) if len(sys.argv) > 5 else 400
+    batch = bool(int(sys.argv[6])) if len(sys.argv) > 6 else False
     cfg = CONFIGS["cfg3_4k"]
     W, H = cfg.width, cfg.height
     obs = g.Observer(cfg.rs, cfg.fov, W, H)
@@ -65,7 +66,7 @@ def main():
 
     for rank in (0, 1):
         sf = ShardedFrame(ctx, frame, scene, W, H, 8, rank, world, dev, dist=OrderOnly(), frames_per_gather=K,
-                          render_streams=S, lead=lead)
+                          render_streams=S, lead=lead, batch_launch=batch)
         for i in range(40):
             sf.step(i)
         sf.drain()
@@ -77,7 +78,7 @@ def main():
         sf.drain()
         torch.cuda.synchronize()
         t_wall = time.perf_counter() - t0
-        print(f"world {world} lead {lead} K {K} S {S} rank {rank}: host {t_host / n * 1e6:.1f} us/frame, "
+        print(f"world {world} lead {lead} K {K} S {S} batch {int(sf.batch)} rank {rank}: host {t_host / n * 1e6:.1f} us/frame, "
               f"wall {t_wall / n * 1e6:.1f} us/frame, rows {sf.layout.rows_mine()}", flush=True)
 
 

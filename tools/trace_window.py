@@ -17,7 +17,7 @@ import statistics
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("trace")
-    p.add_argument("--kernel", default="geo_render_kernel<0, 0, false>")
+    p.add_argument("--kernel", default="geo_render_kernel<0, 0, false, 1u>")
     p.add_argument("--spinup", type=int, default=300)
     p.add_argument("--warmup", type=int, default=20)
     p.add_argument("--steps", type=int, default=200)

@@ -230,9 +230,9 @@ int geo_render_band_set(geo_ctx* ctx, const geo_frame* frame, const geo_scene* s
  * Colour only (no mask, UV or per-pixel steps; no GEO_FLAG_MIPS); the
  * executed steps of all frames go to steps_total or, with
  * GEO_FLAG_DEFER_STEPS, to the context's accumulator.  One launch pays the
- * dispatch, ramp and drain of a render once for the whole batch (DESIGN.md
- * §4: ~12.6 us per launch against ~23 us per 4K megapixel), which is most of
- * a rank's share at N = 8.  Asynchronous on `stream`. */
+ * dispatch, ramp and drain of a render once for the whole batch: a rank's
+ * share of a 4K frame at N = 8 (about two waves per slot) draws 10-12 %
+ * faster per frame.  Asynchronous on `stream`. */
 #define GEO_MAX_BATCH_FRAMES 8
 int geo_render_band_set_frames(geo_ctx* ctx, const geo_frame* frames, uint32_t nframes, const geo_scene* scene,
                                uint32_t width, uint32_t height, uint32_t band_rows, uint32_t row0,

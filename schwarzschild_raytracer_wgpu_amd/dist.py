@@ -201,9 +201,9 @@ class ShardedFrame:
         (geo_assemble_lead).
         batch_launch: render each batch's K frames in ONE launch
         (geo_render_band_set_frames) when it is complete, on render stream
-        (batch buffer % S): a launch's fixed cost (dispatch, ramp, drain;
-        ~12.6 us) is paid once per batch instead of per frame,
-        which at N = 8 is a third of a rank's share.  K <= GEO_MAX_BATCH_FRAMES."""
+        (batch buffer % S): a launch's fixed cost (dispatch, ramp, drain) is
+        paid once per batch instead of per frame; a peer's share at N = 8
+        draws 10-12 % faster per frame.  K <= GEO_MAX_BATCH_FRAMES."""
         import torch
 
         from ._lib import lib

@@ -76,10 +76,11 @@ def parse():
                    help="N > 1: render each gather batch's frames in ONE launch (geo_render_band_set_frames), "
                         "paying a launch's fixed cost (~12.6 us: dispatch, ramp, drain) once per batch instead of per "
                         "frame; auto = on when --frames-per-gather > 1")
-    p.add_argument("--rank0-lead", default="auto", choices=["auto", "1", "2", "3", "4", "6"],
-                   help="N > 1: rank 0's band height in 8-row bands per cycle (it renders rows that never cross "
-                        "an xGMI link, so a link-bound present wants it larger); auto = the fastest of 1, 2, 3, 4, "
-                        "6 measured on the whole pipeline before the timed region")
+    p.add_argument("--rank0-lead", default="auto", type=_lead_spec,
+                   help="N > 1: rank 0's share per cycle against a peer's, as 'a' or 'a:b' (rank 0 a 8-row bands, "
+                        "each peer b; it renders rows that never cross an xGMI link, so a link-bound present wants "
+                        "it larger); auto = the fastest of %s measured on the whole pipeline before the timed "
+                        "region" % ", ".join("%d:%d" % ab for ab in LEAD_TRIALS))
     p.add_argument("--lead-trial-frames", type=int, default=120,
                    help="frames per --rank0-lead auto trial (after a quarter as many warm-up frames)")
     p.add_argument("--pipelined", action="store_true",
@@ -103,6 +104,27 @@ def parse():
     p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                    help="nccl (= RCCL over xGMI); gloo stages the gather through host memory (tests only)")
     return p.parse_args()
+
+
+# --rank0-lead auto: (rank 0's bands, each peer's bands) per cycle, in the
+# order tried (shares of rank 0 at N = 8: 1/15, 1/8, 3/17, 2/9, 5/19, 3/10,
+# 4/11, 6/13).  Rank 0 also reassembles every frame, so with fast links it
+# may want less than a peer's share (1:2).
+LEAD_TRIALS = [(1, 2), (1, 1), (3, 2), (2, 1), (5, 2), (3, 1), (4, 1), (6, 1)]
+
+
+def _lead_spec(v: str):
+    """'auto', 'a' or 'a:b' -> 'auto' or (a, b)."""
+    if v == "auto":
+        return v
+    a, _, b = v.partition(":")
+    try:
+        ab = (int(a), int(b) if b else 1)
+    except ValueError:
+        raise argparse.ArgumentTypeError(f"--rank0-lead: 'auto', 'a' or 'a:b', got {v!r}")
+    if ab[0] < 1 or ab[1] < 1:
+        raise argparse.ArgumentTypeError("--rank0-lead: a and b must be >= 1")
+    return ab
 
 
 def _free_port() -> int:
@@ -261,22 +283,23 @@ def main():
     rdev = dev if args.dist_backend == "nccl" else "cpu"
     devices = rank_devices(dist, world, local, rdev)
 
-    def make_sf(lead):
+    def make_sf(ld):
+        lead, peer_bands = ld
         return ShardedFrame(ctx, frame, scene, W, H, args.band_rows, rank, world, dev, dist if world > 1 else None,
                             host_gather=args.dist_backend == "gloo", frames_per_gather=args.frames_per_gather,
                             render_streams=args.render_streams or (1 if world == 1 else 2), lead=lead,
-                            batch_launch=args.batch_launch != "off")
+                            peer_bands=peer_bands, batch_launch=args.batch_launch != "off")
 
     # everything that syncs or reads back (lead trials, the diagnostic pass)
     # runs before the clock spin-up below, which flows straight into the
     # warmup and the timed region
     if world == 1:
-        leads = [1]
+        leads = [(1, 1)]
     elif args.rank0_lead == "auto":
-        leads = [1, 2, 3, 4, 6]
+        leads = list(LEAD_TRIALS)
     else:
-        leads = [int(args.rank0_lead)]
-    sf = make_sf(leads[0])
+        leads = [args.rank0_lead]
+    sf = make_sf((1, 1) if (1, 1) in leads else leads[0])
     steps_ctr = torch.zeros(1, dtype=torch.int64, device=dev)
 
     # rank 0's share (--rank0-lead auto): every layout runs the whole pipeline
@@ -289,7 +312,7 @@ def main():
         spin_up(sf, args.spinup_frames * world)  # the trials compare layouts at the settled clock
         times = []
         for ld in leads:
-            t_sf = sf if ld == sf.layout.lead else make_sf(ld)
+            t_sf = sf if ld == (sf.layout.lead, sf.layout.peer_bands) else make_sf(ld)
             for i in range(args.lead_trial_frames // 4):
                 t_sf.step(i)
             t_sf.drain()
@@ -307,8 +330,8 @@ def main():
         tt = torch.tensor(times, dtype=torch.float64, device=rdev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         best = leads[int(torch.argmin(tt).item())]
-        lead_trials = {str(ld): float(tt[j]) / args.lead_trial_frames * 1e3 for j, ld in enumerate(leads)}
-        if best != sf.layout.lead:
+        lead_trials = {"%d:%d" % ld: float(tt[j]) / args.lead_trial_frames * 1e3 for j, ld in enumerate(leads)}
+        if best != (sf.layout.lead, sf.layout.peer_bands):
             sf = make_sf(best)
     L = sf.layout
 
@@ -539,7 +562,7 @@ def main():
             "parallelism": f"rowbands{world}" if world > 1 else "single",
             "band_rows": args.band_rows,
             "frames_per_gather": sf.K,
-            "rank0_lead": L.lead,
+            "rank0_lead": "%d:%d" % (L.lead, L.peer_bands),
             "lead_trials_ms_per_frame": lead_trials,
             "render_streams": sf.S,
             "frames_per_launch": sf.K if sf.batch else 1,

@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define GEO_ABI_VERSION 4  /* 4: geo_render_band_set_frames */
+#define GEO_ABI_VERSION 4  /* 4: geo_render_band_set_frames, geo_assemble_shares */
 
 typedef enum geo_status {
     GEO_OK = 0,
@@ -257,6 +257,17 @@ int geo_assemble_lead(geo_ctx* ctx, const uint8_t* lead_src, size_t lead_frame_s
                       const uint8_t* src, size_t rank_stride, size_t frame_stride, uint32_t world,
                       uint32_t band_rows, uint32_t width, uint32_t height, uint32_t nframes, uint32_t src_bpp,
                       uint8_t* dst, void* stream);
+
+/* geo_assemble_lead with rank 0's rows per cycle given directly: cycles of
+ * lead_rows + (world - 1) * band_rows rows, rank 0's first (one lead_rows
+ * band), then one band_rows band per peer.  Any lead_rows, so rank 0's share
+ * need not be a whole number of peer bands (e.g. 24 rows against peers' 16:
+ * bench.py --rank0-lead 3:2).  geo_assemble_lead(lead) is
+ * geo_assemble_shares(lead * band_rows).  Same buffers and alignment rules. */
+int geo_assemble_shares(geo_ctx* ctx, const uint8_t* lead_src, size_t lead_frame_stride, uint32_t lead_rows,
+                        const uint8_t* src, size_t rank_stride, size_t frame_stride, uint32_t world,
+                        uint32_t band_rows, uint32_t width, uint32_t height, uint32_t nframes, uint32_t src_bpp,
+                        uint8_t* dst, void* stream);
 
 /* RGBA8 -> RGB24 (the alpha byte dropped: frames are opaque after the clear,
  * renderer.rs:233-238) of npixels (a multiple of 4) device pixels: 25 % fewer

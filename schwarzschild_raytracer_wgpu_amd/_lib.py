@@ -110,6 +110,8 @@ SIGNATURES = {
                                   _vp, _vp]),
     "geo_assemble_lead": (_int, [_vp, _vp, ctypes.c_size_t, _u32, _vp, ctypes.c_size_t, ctypes.c_size_t, _u32, _u32,
                                  _u32, _u32, _u32, _u32, _vp, _vp]),
+    "geo_assemble_shares": (_int, [_vp, _vp, ctypes.c_size_t, _u32, _vp, ctypes.c_size_t, ctypes.c_size_t, _u32,
+                                   _u32, _u32, _u32, _u32, _u32, _vp, _vp]),
     "geo_pack_rgb": (_int, [_vp, _vp, ctypes.c_uint64, _vp, _vp]),
     "geo_rays_create": (_int, [_vp, ctypes.c_float, _u32, _u32, _vp, ctypes.POINTER(_vp)]),
     "geo_rays_destroy": (None, [_vp]),

@@ -190,6 +190,14 @@ class Context:
             self._h, _ptr(lead_src), lead_frame_stride, lead, _ptr(src), rank_stride, frame_stride, world, band_rows,
             width, height, nframes, src_bpp, _ptr(dst), _stream_handle(stream)))
 
+    def assemble_shares(self, lead_src, lead_frame_stride: int, lead_rows: int, src, rank_stride: int,
+                        frame_stride: int, world: int, band_rows: int, width: int, height: int, nframes: int, dst,
+                        src_bpp: int = 4, stream=None) -> None:
+        """geo_assemble_shares: geo_assemble_lead with rank 0's rows per cycle (lead_rows) given directly."""
+        check("geo_assemble_shares", lib.geo_assemble_shares(
+            self._h, _ptr(lead_src), lead_frame_stride, lead_rows, _ptr(src), rank_stride, frame_stride, world,
+            band_rows, width, height, nframes, src_bpp, _ptr(dst), _stream_handle(stream)))
+
     def pack_rgb(self, rgba, npixels: int, rgb, stream=None) -> None:
         """geo_pack_rgb: RGBA8 -> RGB24 on the device (npixels % 4 == 0)."""
         check("geo_pack_rgb", lib.geo_pack_rgb(self._h, _ptr(rgba), npixels, _ptr(rgb), _stream_handle(stream)))

@@ -571,16 +571,15 @@ __global__ __launch_bounds__(256) void geo_assemble_rgb_kernel(const uint8_t* __
 // The row's source (rank 0's own bands or a peer's) is block-uniform.
 template <bool QUAD>
 __global__ __launch_bounds__(256) void geo_assemble_lead_kernel(
-    const uint8_t* __restrict__ lead_src, size_t lead_frame_stride, uint32_t lead, const uint8_t* __restrict__ src,
-    size_t rank_stride, size_t frame_stride, uint32_t world, uint32_t band_rows, uint32_t units, uint32_t height,
-    uint32_t src_bpp, uint8_t* __restrict__ dst) {
+    const uint8_t* __restrict__ lead_src, size_t lead_frame_stride, uint32_t lead_rows,
+    const uint8_t* __restrict__ src, size_t rank_stride, size_t frame_stride, uint32_t world, uint32_t band_rows,
+    uint32_t units, uint32_t height, uint32_t src_bpp, uint8_t* __restrict__ dst) {
     using T = typename std::conditional<QUAD, uint4, uint32_t>::type;
     constexpr uint32_t kPix = QUAD ? 4u : 1u;  // pixels per unit
     const uint32_t x = blockIdx.x * 256u + threadIdx.x;
     const uint32_t y = blockIdx.y;
     const uint32_t f = blockIdx.z;
     if (x >= units) return;
-    const uint32_t lead_rows = lead * band_rows;
     const uint32_t cycle = lead_rows + (world - 1u) * band_rows;
     const uint32_t c = y / cycle, off = y % cycle;
     const size_t rgba_row = (size_t)units * sizeof(T);
@@ -1460,18 +1459,18 @@ int geo_assemble_bands(geo_ctx* c, const uint8_t* src, size_t rank_stride, size_
     return hipGetLastError() == hipSuccess ? GEO_OK : GEO_EHIP;
 }
 
-int geo_assemble_lead(geo_ctx* c, const uint8_t* lead_src, size_t lead_frame_stride, uint32_t lead,
-                      const uint8_t* src, size_t rank_stride, size_t frame_stride, uint32_t world,
-                      uint32_t band_rows, uint32_t width, uint32_t height, uint32_t nframes, uint32_t src_bpp,
-                      uint8_t* dst, void* stream) {
-    if (!c || !lead_src || !dst || world == 0 || lead == 0 || band_rows == 0 || width == 0 || height == 0 ||
+int geo_assemble_shares(geo_ctx* c, const uint8_t* lead_src, size_t lead_frame_stride, uint32_t lead_rows,
+                        const uint8_t* src, size_t rank_stride, size_t frame_stride, uint32_t world,
+                        uint32_t band_rows, uint32_t width, uint32_t height, uint32_t nframes, uint32_t src_bpp,
+                        uint8_t* dst, void* stream) {
+    if (!c || !lead_src || !dst || world == 0 || lead_rows == 0 || band_rows == 0 || width == 0 || height == 0 ||
         nframes == 0 || height > 65535u || nframes > 65535u || (src_bpp != 3u && src_bpp != 4u))
         return GEO_EINVAL;
     // 16-B units need width % 4 == 0 and aligned buffers; RGB24 peers need them
     const size_t lead_align = width % 4u == 0 ? 16u : 4u;
     if (src_bpp == 3u && width % 4u != 0) return GEO_EINVAL;
-    if ((uint64_t)(lead + world - 1u) * band_rows > (1u << 20)) return GEO_EINVAL;
-    const uint32_t lead_rows = lead * band_rows, cycle = lead_rows + (world - 1u) * band_rows;
+    if ((uint64_t)lead_rows + (uint64_t)(world - 1u) * band_rows > (1u << 20)) return GEO_EINVAL;
+    const uint32_t cycle = lead_rows + (world - 1u) * band_rows;
     // rank 0 has ceil(H / cycle) bands; rank 1, the first peer, the most of the peers
     const size_t nb0 = (height + cycle - 1u) / cycle;
     const size_t nb1 = height > lead_rows ? (height - lead_rows + cycle - 1u) / cycle : 0;
@@ -1492,14 +1491,23 @@ int geo_assemble_lead(geo_ctx* c, const uint8_t* lead_src, size_t lead_frame_str
     if (width % 4u == 0) {
         const uint32_t quads = width / 4u;
         hipLaunchKernelGGL(geo_assemble_lead_kernel<true>, dim3((quads + 255u) / 256u, height, nframes), dim3(256),
-                           0, s, lead_src, lead_frame_stride, lead, src, rank_stride, frame_stride, world, band_rows,
-                           quads, height, src_bpp, dst);
+                           0, s, lead_src, lead_frame_stride, lead_rows, src, rank_stride, frame_stride, world,
+                           band_rows, quads, height, src_bpp, dst);
     } else {
         hipLaunchKernelGGL(geo_assemble_lead_kernel<false>, dim3((width + 255u) / 256u, height, nframes), dim3(256),
-                           0, s, lead_src, lead_frame_stride, lead, src, rank_stride, frame_stride, world, band_rows,
-                           width, height, src_bpp, dst);
+                           0, s, lead_src, lead_frame_stride, lead_rows, src, rank_stride, frame_stride, world,
+                           band_rows, width, height, src_bpp, dst);
     }
     return hipGetLastError() == hipSuccess ? GEO_OK : GEO_EHIP;
+}
+
+int geo_assemble_lead(geo_ctx* c, const uint8_t* lead_src, size_t lead_frame_stride, uint32_t lead,
+                      const uint8_t* src, size_t rank_stride, size_t frame_stride, uint32_t world,
+                      uint32_t band_rows, uint32_t width, uint32_t height, uint32_t nframes, uint32_t src_bpp,
+                      uint8_t* dst, void* stream) {
+    if (lead == 0 || (uint64_t)lead * band_rows > (1u << 20)) return GEO_EINVAL;
+    return geo_assemble_shares(c, lead_src, lead_frame_stride, lead * band_rows, src, rank_stride, frame_stride,
+                               world, band_rows, width, height, nframes, src_bpp, dst, stream);
 }
 
 int geo_pack_rgb(geo_ctx* c, const uint8_t* rgba, uint64_t npixels, uint8_t* rgb, void* stream) {

@@ -21,38 +21,41 @@ from dataclasses import dataclass
 class BandLayout:
     """Rows of a `height`-row frame owned by each of `world` ranks.
 
-    The frame is cut into cycles of (lead + world - 1) * band_rows rows: rank 0
-    owns the first lead * band_rows rows of every cycle (one band of that
-    height), rank r >= 1 the band_rows rows after rank r - 1's.  lead = 1 is
-    the plain interleave (band b of band_rows rows belongs to rank b % world).
-    lead > 1 is the LEAD layout: rank 0 renders but never sends its rows, so
-    when the present gather is link-bound it takes a larger share
-    (bench.py --rank0-lead picks lead by measurement)."""
+    The frame is cut into cycles of (lead + (world - 1) * peer_bands) *
+    band_rows rows: rank 0 owns the first lead * band_rows rows of every
+    cycle (one band of that height), rank r >= 1 the peer_bands * band_rows
+    rows after rank r - 1's.  lead = peer_bands = 1 is the plain interleave
+    (band b of band_rows rows belongs to rank b % world).  lead > peer_bands
+    is the LEAD layout: rank 0 renders but never sends its rows, so when the
+    present gather is link-bound it takes a larger share, lead / peer_bands
+    times a peer's (bench.py --rank0-lead picks it by measurement; a ratio
+    like 3:2 falls between the whole numbers)."""
     height: int
     band_rows: int
     world: int
     rank: int
     lead: int = 1
+    peer_bands: int = 1
 
     def __post_init__(self):
-        if self.lead < 1 or self.band_rows < 1 or self.world < 1:
-            raise ValueError("lead, band_rows and world must be >= 1")
+        if self.lead < 1 or self.peer_bands < 1 or self.band_rows < 1 or self.world < 1:
+            raise ValueError("lead, peer_bands, band_rows and world must be >= 1")
 
     @property
     def cycle_rows(self) -> int:
-        return (self.lead + self.world - 1) * self.band_rows
+        return (self.lead + (self.world - 1) * self.peer_bands) * self.band_rows
 
     def _r(self, rank):
         return self.rank if rank is None else rank
 
     def band_height(self, rank: int | None = None) -> int:
-        """Rows per band of a rank (lead * band_rows for rank 0)."""
-        return self.lead * self.band_rows if self._r(rank) == 0 else self.band_rows
+        """Rows per band of a rank (lead * band_rows for rank 0, peer_bands * band_rows for a peer)."""
+        return (self.lead if self._r(rank) == 0 else self.peer_bands) * self.band_rows
 
     def row0(self, rank: int | None = None) -> int:
         """First frame row of a rank's first band."""
         r = self._r(rank)
-        return 0 if r == 0 else (self.lead + r - 1) * self.band_rows
+        return 0 if r == 0 else (self.lead + (r - 1) * self.peer_bands) * self.band_rows
 
     def nbands(self, rank: int | None = None) -> int:
         r0 = self.row0(rank)
@@ -79,8 +82,8 @@ class BandLayout:
         return self.packed_rows(0) // self.band_rows
 
     def bands(self, rank: int | None = None) -> range:
-        if self.lead != 1:
-            raise ValueError("bands() indexes the plain interleave (lead = 1)")
+        if self.lead != 1 or self.peer_bands != 1:
+            raise ValueError("bands() indexes the plain interleave (lead = peer_bands = 1)")
         r = self._r(rank)
         return range(r, self.nb_total, self.world)
 
@@ -192,13 +195,14 @@ class ShardedFrame:
 
     def __init__(self, ctx, frame, scene, width: int, height: int, band_rows: int, rank: int, world: int, device,
                  dist=None, host_gather: bool = False, frames_per_gather: int = 1, render_streams: int = 1,
-                 present_rgb: bool = True, lead: int = 1, batch_launch: bool = False):
+                 present_rgb: bool = True, lead: int = 1, batch_launch: bool = False, peer_bands: int = 1):
         """host_gather: stage through host memory (gloo backend; rehearsals only).
         present_rgb: peers send RGB24 (geo_pack_rgb after each render; 25 %
         fewer bytes on the links) when the width is a multiple of 4.
         lead: rank 0's band height in band_rows (BandLayout); rank 0 never
         sends its own rows, its reassembly reads them from its local bands
-        (geo_assemble_lead).
+        (geo_assemble_shares); peer_bands: a peer's band height in band_rows
+        (BandLayout; rank 0's share is lead / peer_bands times a peer's).
         batch_launch: render each batch's K frames in ONE launch
         (geo_render_band_set_frames) when it is complete, on render stream
         (batch buffer % S): a launch's fixed cost (dispatch, ramp, drain) is
@@ -213,7 +217,8 @@ class ShardedFrame:
         self.host_gather = host_gather
         self.ctx, self.frame, self.scene = ctx, frame, scene
         self.width, self.height = width, height
-        self.layout = BandLayout(height, band_rows, world, rank, lead if world > 1 else 1)
+        self.layout = BandLayout(height, band_rows, world, rank, lead if world > 1 else 1,
+                                 peer_bands if world > 1 else 1)
         self.rank, self.world, self.dist = rank, world, dist
         self.K = max(1, int(frames_per_gather)) if world > 1 else 1
         self.S = min(2, max(1, int(render_streams)))
@@ -294,9 +299,10 @@ class ShardedFrame:
 
     def _assemble(self, b: int, src, n: int, stream=None) -> None:
         """Rank 0: frames of batch b from its own bands (bufs[b]) and the peers' gathered blocks."""
-        self.ctx.assemble_lead(self.bufs[b], self.slice, self.layout.lead, src, self.K * self.tslice, self.tslice,
-                               self.world, self.layout.band_rows, self.width, self.height, n, self.frames,
-                               src_bpp=self.bpp, stream=stream)
+        L = self.layout
+        self.ctx.assemble_shares(self.bufs[b], self.slice, L.band_height(0), src, self.K * self.tslice, self.tslice,
+                                 self.world, L.band_height(1), self.width, self.height, n, self.frames,
+                                 src_bpp=self.bpp, stream=stream)
 
     def _render_stream(self, i: int):
         k = (i // self.K) % 2 % self.S if self.batch else i % self.S

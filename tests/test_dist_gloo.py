@@ -152,6 +152,25 @@ def test_lead_layout_owns_every_row_once(H, B, world, lead):
         assert abs(L[0].rows_mine() / L[1].rows_mine() / lead - 1) < 0.03
 
 
+@pytest.mark.parametrize("H,B,world,lead,pb", [(2160, 8, 8, 3, 2), (2160, 8, 8, 5, 2), (2160, 8, 4, 3, 2),
+                                               (180, 8, 3, 3, 2), (41, 8, 2, 1, 2), (1080, 16, 4, 5, 3),
+                                               (7, 8, 3, 3, 2), (2160, 8, 2, 2, 2)])
+def test_share_layout_owns_every_row_once(H, B, world, lead, pb):
+    """Peer bands of pb x band_rows: rank 0's share is lead / pb times a
+    peer's (bench.py --rank0-lead a:b); every row owned once."""
+    L = [BandLayout(H, B, world, r, lead, pb) for r in range(world)]
+    owned = sorted(x for l in L for x in l.local_to_frame_rows() if x >= 0)
+    assert owned == list(range(H))
+    assert L[0].band_height() == lead * B and all(l.band_height() == pb * B for l in L[1:])
+    assert L[0].cycle_rows == (lead + (world - 1) * pb) * B
+    assert all(l.packed_rows() <= L[0].peer_packed_rows for l in L[1:])
+    if H >= 16 * L[0].cycle_rows:
+        assert abs(L[0].rows_mine() / L[1].rows_mine() / (lead / pb) - 1) < 0.05
+    if (lead, pb) == (2, 2):  # the same ratio as lead 1 at twice the band height
+        same = [BandLayout(H, 2 * B, world, r, 1) for r in range(world)]
+        assert [l.local_to_frame_rows() for l in L] == [l.local_to_frame_rows() for l in same]
+
+
 def test_lead_one_is_the_plain_interleave():
     for H, B, world in [(2160, 8, 8), (33, 8, 3), (1080, 16, 4)]:
         for r in range(world):
@@ -160,7 +179,7 @@ def test_lead_one_is_the_plain_interleave():
             assert b.local_to_frame_rows() == [f if f < H else -1 for f in rows]
 
 
-def _worker_lead(rank, world, port, W, H, B, lead, K, q):
+def _worker_lead(rank, world, port, W, H, B, lead, K, q, peer_bands=1):
     """The lead layout as dist.ShardedFrame runs it: peers send their packed
     bands (all contributions the size of rank 1's), rank 0 contributes a
     dummy and reassembles its own rows from its local bands."""
@@ -176,7 +195,7 @@ def _worker_lead(rank, world, port, W, H, B, lead, K, q):
 
         sky = make_sky("equirect", (64, 32))
         scene = default_scene(256)
-        L = BandLayout(H, B, world, rank, lead)
+        L = BandLayout(H, B, world, rank, lead, peer_bands)
         row_bytes = W * 4
         frames = [default_frame(W, H, camera=(math.pi + 0.1 * f, 0.05 * f)) for f in range(K)]
         rows = L.packed_rows() if rank == 0 else L.peer_packed_rows
@@ -206,13 +225,14 @@ def _worker_lead(rank, world, port, W, H, B, lead, K, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,W,H,B,lead,K", [(2, 40, 52, 8, 2, 2), (3, 28, 72, 8, 4, 1), (3, 33, 40, 8, 2, 2),
-                                                (2, 40, 60, 8, 3, 2)])
-def test_gloo_lead_layout_reassembles_frames(world, W, H, B, lead, K):
+@pytest.mark.parametrize("world,W,H,B,lead,K,pb", [(2, 40, 52, 8, 2, 2, 1), (3, 28, 72, 8, 4, 1, 1),
+                                                   (3, 33, 40, 8, 2, 2, 1), (2, 40, 60, 8, 3, 2, 1),
+                                                   (3, 28, 88, 8, 3, 1, 2), (2, 36, 70, 8, 5, 2, 2)])
+def test_gloo_lead_layout_reassembles_frames(world, W, H, B, lead, K, pb):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker_lead, args=(r, world, port, W, H, B, lead, K, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker_lead, args=(r, world, port, W, H, B, lead, K, q, pb)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:

@@ -47,15 +47,15 @@ class FakeRcclGather:
         return _Work(t, done)
 
 
-def _peer_bands(ctx, torch, frame, scene, W, H, B, r, world, lead, dev, bpp):
+def _peer_bands(ctx, torch, frame, scene, W, H, B, r, world, lead, dev, bpp, pb=1):
     """Peer r's packed bands in the travelling format, padded to rank 1's size."""
     from schwarzschild_raytracer_wgpu_amd.dist import BandLayout
 
-    L = BandLayout(H, B, world, r, lead)
+    L = BandLayout(H, B, world, r, lead, pb)
     sl = L.peer_packed_rows * W * 4
     one = torch.zeros(sl, dtype=torch.uint8, device=dev)
     if L.nbands():
-        ctx.render_band_set(frame, scene, W, H, B, L.row0(), L.cycle_rows, L.nbands(), one)
+        ctx.render_band_set(frame, scene, W, H, L.band_height(), L.row0(), L.cycle_rows, L.nbands(), one)
     if bpp == 3:
         packed = torch.empty(sl // 4 * 3, dtype=torch.uint8, device=dev)
         ctx.pack_rgb(one, sl // 4, packed)
@@ -68,7 +68,8 @@ def _peer_bands(ctx, torch, frame, scene, W, H, B, r, world, lead, dev, bpp):
 @pytest.mark.parametrize("S", [1, 2])
 @pytest.mark.parametrize("world,K,nframes,lead", [(2, 4, 41, 1), (3, 3, 10, 1), (8, 4, 16, 1), (8, 1, 5, 1),
                                                   (2, 4, 13, 2), (2, 2, 7, 4), (4, 3, 10, 2), (8, 4, 9, 2),
-                                                  (8, 2, 6, 4), (2, 3, 8, 3), (8, 4, 9, 3), (4, 2, 5, 6)])
+                                                  (8, 2, 6, 4), (2, 3, 8, 3), (8, 4, 9, 3), (4, 2, 5, 6),
+                                                  (8, 4, 9, (3, 2)), (4, 3, 7, (5, 2)), (2, 2, 5, (3, 2))])
 def test_rank0_pipeline_assembles_frames(world, K, nframes, lead, S, rgb, batch):
     import torch
 
@@ -84,13 +85,15 @@ def test_rank0_pipeline_assembles_frames(world, K, nframes, lead, S, rgb, batch)
     ctx.set_sky(make_sky("equirect", (256, 128)))
     frame, scene = default_frame(W, H), default_scene(512)
     fake = FakeRcclGather(torch, [])
+    lead, pb = lead if isinstance(lead, tuple) else (lead, 1)  # (rank 0's bands, a peer's bands) per cycle
     sf = ShardedFrame(ctx, frame, scene, W, H, B, 0, world, dev, dist=fake, frames_per_gather=K, render_streams=S,
-                      present_rgb=rgb, lead=lead, batch_launch=batch)
+                      present_rgb=rgb, lead=lead, batch_launch=batch, peer_bands=pb)
     assert sf.batch == (batch and K > 1)
     assert sf.side is not None and sf.bpp == (3 if rgb else 4) and sf.layout.lead == lead
     # the peers' K-frame batches (every frame identical), in the travelling format
     for r in range(1, world):
-        fake.peer_bufs.append(_peer_bands(ctx, torch, frame, scene, W, H, B, r, world, lead, dev, sf.bpp).repeat(K))
+        fake.peer_bufs.append(_peer_bands(ctx, torch, frame, scene, W, H, B, r, world, lead, dev, sf.bpp,
+                                          pb).repeat(K))
     for i in range(nframes):
         sf.step(i)
     sf.drain()
@@ -162,11 +165,15 @@ def test_peer_rank_pipeline_runs_batches(S, lead, batch):
 
 @pytest.mark.parametrize("W,H,B,world,lead,bpp,nframes", [
     (320, 180, 8, 2, 2, 3, 3), (320, 180, 8, 8, 4, 4, 2), (36, 50, 8, 3, 2, 3, 1), (33, 27, 8, 2, 4, 4, 2),
-    (64, 64, 16, 4, 1, 3, 2), (20, 8, 8, 3, 2, 4, 1), (320, 180, 8, 8, 3, 3, 2), (36, 50, 8, 2, 6, 4, 1)])
+    (64, 64, 16, 4, 1, 3, 2), (20, 8, 8, 3, 2, 4, 1), (320, 180, 8, 8, 3, 3, 2), (36, 50, 8, 2, 6, 4, 1),
+    (320, 180, 8, 8, (3, 2), 3, 2), (36, 90, 8, 3, (5, 2), 4, 2), (33, 60, 8, 2, (3, 2), 4, 1),
+    (64, 100, 8, 4, (1, 2), 3, 1)])
 def test_assemble_lead_matches_host_assembly(W, H, B, world, lead, bpp, nframes):
     """geo_assemble_lead on random bytes == dist.assemble (the host reassembly
     the gloo tests check against the oracle), RGB24 and RGBA8 peers, widths
-    that are and are not multiples of 4, frames with empty peer shares."""
+    that are and are not multiples of 4, frames with empty peer shares; with
+    a (lead, peer_bands) pair, geo_assemble_shares with rank 0's rows per
+    cycle not a multiple of a peer's band."""
     import torch
 
     if not torch.cuda.is_available():
@@ -176,8 +183,9 @@ def test_assemble_lead_matches_host_assembly(W, H, B, world, lead, bpp, nframes)
 
     dev = torch.device("cuda:0")
     ctx = g.Context(0)
-    L = BandLayout(H, B, world, 0, lead)
-    gen = torch.Generator().manual_seed(W * 7919 + H * 31 + world * 7 + lead)
+    lead, pb = lead if isinstance(lead, tuple) else (lead, 1)
+    L = BandLayout(H, B, world, 0, lead, pb)
+    gen = torch.Generator().manual_seed(W * 7919 + H * 31 + world * 7 + lead * 3 + pb)
     own_sl = L.packed_rows(0) * W * 4
     own_sl += (-own_sl) % 16
     tsl = L.peer_packed_rows * W * bpp
@@ -185,8 +193,12 @@ def test_assemble_lead_matches_host_assembly(W, H, B, world, lead, bpp, nframes)
     own = torch.randint(0, 256, (nframes * own_sl,), dtype=torch.uint8, generator=gen)
     peers = torch.randint(0, 256, (world * nframes * max(tsl, 1),), dtype=torch.uint8, generator=gen)
     out = torch.full((nframes * H * W * 4,), 7, dtype=torch.uint8, device=dev)
-    ctx.assemble_lead(own.to(dev), own_sl, lead, peers.to(dev), nframes * tsl, tsl, world, B, W, H, nframes, out,
-                      src_bpp=bpp)
+    if pb == 1:
+        ctx.assemble_lead(own.to(dev), own_sl, lead, peers.to(dev), nframes * tsl, tsl, world, B, W, H, nframes, out,
+                          src_bpp=bpp)
+    else:
+        ctx.assemble_shares(own.to(dev), own_sl, lead * B, peers.to(dev), nframes * tsl, tsl, world, pb * B, W, H,
+                            nframes, out, src_bpp=bpp)
     torch.cuda.synchronize()
     got = out.cpu()
     for f in range(nframes):

@@ -23,6 +23,7 @@ waits for them, forwards rank 0's line and exits non-zero if any rank fails.
 from __future__ import annotations
 
 import argparse
+import datetime
 import json
 import math
 import os
@@ -246,9 +247,12 @@ def main():
     dev = torch.device("cuda", local)
     if world > 1:
         if args.dist_backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
+            # a collective stuck for 5 minutes (a peer died or hangs; the
+            # whole bench takes well under one) aborts the rank, so the
+            # launcher stops the others instead of waiting for the driver's kill
+            dist.init_process_group("nccl", device_id=dev, timeout=datetime.timedelta(minutes=5))
         else:
-            dist.init_process_group("gloo")
+            dist.init_process_group("gloo", timeout=datetime.timedelta(minutes=5))
         if dist.get_world_size() != world:
             raise SystemExit(f"process group has {dist.get_world_size()} ranks, WORLD_SIZE={world}")
 

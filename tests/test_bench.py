@@ -61,3 +61,25 @@ def test_bench_short_run_prints_the_contract_line():
     assert len(cb["seconds_per_run"]) == 3
     # the frames of the timed run's last batch equal a single-launch frame
     assert d["frame_check"]["ok"] is True and d["frame_check"]["frames"] >= 1
+
+
+def test_rank0_lead_specs_and_trials():
+    """--rank0-lead: 'auto', 'a' or 'a:b'; every layout the auto trial tries
+    owns each row of the 4K frame exactly once at every N the driver runs."""
+    import argparse
+
+    from schwarzschild_raytracer_wgpu_amd.dist import BandLayout
+
+    assert bench._lead_spec("auto") == "auto"
+    assert bench._lead_spec("2") == (2, 1)
+    assert bench._lead_spec("3:2") == (3, 2)
+    for bad in ("0", "1:0", "x", "2:y"):
+        with pytest.raises(argparse.ArgumentTypeError):
+            bench._lead_spec(bad)
+    assert (1, 1) in bench.LEAD_TRIALS and len(set(bench.LEAD_TRIALS)) == len(bench.LEAD_TRIALS)
+    for n in (2, 4, 8):
+        for a, b in bench.LEAD_TRIALS:
+            L = [BandLayout(2160, 8, n, r, a, b) for r in range(n)]
+            owned = sorted(x for lay in L for x in lay.local_to_frame_rows() if x >= 0)
+            assert owned == list(range(2160)), (n, a, b)
+            assert all(lay.band_height() % 8 == 0 for lay in L)  # a wave's rows lie in one band

@@ -136,3 +136,70 @@ def compare(hip_mask, hip_uv, ref, rs, r_obs):
         "uv_max_all": float(e_all.max()) if e_all.size else 0.0,
         "model": f"pred = m u ({A_DIR:g} + {K_AMP:g}/|b/b_c - 1|), u = 2^-24",
     }
+
+
+# ---- fan mode: the reference's display path (shader.wgsl:77-88) ---------
+# A fan-mode pixel lerps the f32 fan (R32Float, ray_fan_texture.rs:65-90) at
+# t = (pi/2 - lambda)/pi (n - 1) and draws the sky direction that lerp gives.
+# Both sides read the same f32 nodes, so they differ only by the pixel's own
+# roundings: an error in its angle to the black hole, a few u, amplified by
+# the asin's conditioning near lambda = +-pi/2 (1/|cos lambda|) and carried
+# into lambda' by the fan's slope there, s = |fan[i+1] - fan[i]| (n - 1)/pi
+# (steep only in the interval where the fan falls to NO_VALUE, the black
+# hole's edge); plus the sky map's own roundings (A_DIR).  So
+#   direction error <= u (A_DIR + C_FAN s q),  q = 1 + 1/|cos lambda|,
+# UV error <= m times that (m as above), and the mask may flip only where
+# |lambda'_f64 + 7| is within the lambda' part, u C_FAN s q (+ the lerp's own
+# rounding, 8 u |lambda'|).  C_FAN is measured on the same calibration set
+# as the direct model (tests/test_f64_bar_cpu.py::test_fan_model_calibration:
+# 2.62), rounded up to a power of two.
+C_FAN = 4.0
+BLACK_HOLE_LAMBDA = -7.0  # shader.wgsl:88
+
+
+def fan_terms(theta, uv_ref, fan):
+    """(m, s q) per pixel of an f64 fan-mode frame: the UV factor and the
+    fan's slope at the pixel times the asin's conditioning."""
+    n = len(fan)
+    f = np.asarray(fan, dtype=np.float64)
+    t = np.clip((math.pi / 2 - theta) / math.pi, 0.0, 1.0) * (n - 1)
+    i = np.minimum(np.floor(t).astype(np.int64), n - 2)
+    s = np.abs(f[i + 1] - f[i]) * (n - 1) / math.pi
+    q = 1.0 + 1.0 / np.maximum(np.abs(np.cos(theta)), 1e-3)
+    lat = math.pi * (0.5 - uv_ref[..., 1].astype(np.float64))
+    m = np.maximum(1.0 / math.pi, 1.0 / (2.0 * math.pi * np.maximum(np.cos(lat), 1e-30)))
+    return m, s * q
+
+
+def fan_model(theta, lam, uv_ref, fan):
+    """(pred UV error, lambda' error bound) per pixel of an f64 fan-mode frame."""
+    m, sq = fan_terms(theta, uv_ref, fan)
+    dlam = U32 * (C_FAN * sq + 8.0 * np.abs(lam))
+    return m * U32 * (A_DIR + C_FAN * sq), dlam
+
+
+def compare_fan(hip_mask, hip_uv, ref, fan):
+    """The bar's statistics for fan-mode rows against the f64 literal fan-mode rows."""
+    pred, dlam = fan_model(ref["theta"], ref["lam"], ref["uv"], fan)
+    flip = hip_mask != ref["mask"]
+    edge = np.abs(ref["lam"] - BLACK_HOLE_LAMBDA) <= 2.0 * dlam  # where the mask may flip
+    sky = (hip_mask == 0) & (ref["mask"] == 0)
+    band = sky & (pred > UV_BAR)
+    e = uv_err(hip_uv, ref["uv"])
+    e_out = e[sky & ~band]
+    e_in, p_in = e[sky & band], pred[sky & band]
+    return {
+        "pixels": int(hip_mask.size),
+        "edge_pixels": int(edge.sum()),
+        "mask_flips": int(flip.sum()),
+        "mask_flips_outside_edge": int((flip & ~edge).sum()),
+        "uv_band_pixels": int(band.sum()),
+        "sky_pixels_outside_band": int(e_out.size),
+        "uv_p99": float(np.quantile(e_out, 0.99)) if e_out.size else 0.0,
+        "uv_max": float(e_out.max()) if e_out.size else 0.0,
+        "uv_over_bar_outside_band": int((e_out > UV_BAR).sum()),
+        "uv_max_in_band": float(e_in.max()) if e_in.size else 0.0,
+        "in_band_over_model": int((e_in > p_in).sum()),
+        "max_err_over_model": float((e[sky] / pred[sky]).max()) if sky.any() else 0.0,
+        "model": f"pred = m u ({A_DIR:g} + {C_FAN:g} s (1 + 1/|cos lambda|)), u = 2^-24",
+    }

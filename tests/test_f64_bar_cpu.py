@@ -84,3 +84,31 @@ def test_tangential_rays_well_conditioned():
         a64, _ = O.geodesic_at_theta(50.0, 1.0, 2048, math.pi / 100, float(np.float32(R_OBS)), math.atan2(st, ct))
         worst = max(worst, abs(a32 - a64))
     assert worst < 2e-5, worst
+
+
+def test_fan_model_calibration():
+    """Fan mode (the reference's display path): the f32 specification's fan
+    draw (= the kernel's, bit for bit) against the f64 literal restatement of
+    shader.wgsl:57-106 reading the same f32 fan, on the calibration set.
+    C_FAN (tests/f64_bar.py) bounds it, at most 2x above the measurement; no
+    mask flips; UV within the bar on every sky pixel of this set."""
+    w, h = 480, 270
+    fan = O.solve_ray_fan(50.0, 1.0, 1000, math.pi / 100, 400, R_OBS)
+    scene = default_scene(1000, mode=1)
+    c_meas, worst = 0.0, 0.0
+    for cam in SWEEP:
+        frame = default_frame(w, h, camera=cam)
+        p = O.render_f32(frame, scene, make_sky("equirect", (64, 32)), w, h, fan=fan, threads=8)
+        ref = O.render_f64(frame, scene, w, h, fan=fan, threads=8)
+        st = B.compare_fan(p["mask"], p["uv"], ref, fan)
+        assert st["mask_flips"] == 0 and st["in_band_over_model"] == 0 and st["max_err_over_model"] <= 1.0, st
+        worst = max(worst, st["uv_max"], st["uv_max_in_band"])
+        # the constant: (err/(m u) - A_DIR) / (s q) where the error exceeds the well-conditioned part
+        m, sq = B.fan_terms(ref["theta"], ref["uv"], fan)
+        sky = (p["mask"] == 0) & (ref["mask"] == 0)
+        r = B.uv_err(p["uv"], ref["uv"]) / (m * B.U32)
+        over = sky & (r > B.A_DIR) & (sq > 0)
+        if over.any():
+            c_meas = max(c_meas, float(((r[over] - B.A_DIR) / sq[over]).max()))
+    print(f"fan calibration: C measured {c_meas:.2f}, worst UV error {worst:.2e}")
+    assert c_meas <= B.C_FAN <= 2 * c_meas and worst <= B.UV_BAR

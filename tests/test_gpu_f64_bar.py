@@ -163,3 +163,50 @@ def test_default_scene_sweep_f64_bar(geo, torch_mod):
         _assert_bar(st)
         worst = max(worst, st["uv_max"])
     print("default-scene camera sweep: worst UV error outside the band", worst)
+
+
+FAN_CASES = [("cfg2_1080p_fan", "cfg2_1080p", 9), ("cfg3_4k_fan", "cfg3_4k", 27)]
+
+
+@pytest.mark.parametrize("name,cfgname,row_step", FAN_CASES, ids=[c[0] for c in FAN_CASES])
+def test_hip_fan_draw_vs_f64_literal_at_config_size(geo, torch_mod, name, cfgname, row_step):
+    """The reference's display path (fan mode): the fan solved on the GPU
+    (geo_solve_ray_fan, 400 nodes, as bench.py's fan draw), the HIP fan
+    draw against the f64 literal shader.wgsl:57-106 reading the same f32
+    fan, sampled rows of the config frames.  Mask identical off the black
+    hole's edge (where the f64 lambda' is within the model's bound of -7),
+    UV within the bar off the fan-model band and within the model in it."""
+    from schwarzschild_raytracer_wgpu_amd.scenes import CONFIGS, make_sky
+
+    cfg = CONFIGS[cfgname]
+    w, h = cfg.width, cfg.height
+    obs = geo.Observer(cfg.rs, cfg.fov, w, h)
+    obs.set_position(*cfg.position)
+    obs.set_camera(*cfg.camera)
+    obs.set_energy(cfg.energy)
+    frame = obs.calc_transformation_pipeline()
+    r = obs.get_radial_position()
+    scene = geo.make_scene(cfg.rs, cfg.sphere_r, r, cfg.step, cfg.max_steps, geo.GEO_MODE_FAN)
+    ctx = geo.Context(0)
+    ctx.set_sky(make_sky("equirect", (256, 128)))
+    fan = ctx.solve_ray_fan(cfg.sphere_r, cfg.rs, cfg.max_steps, cfg.step, 400, r)  # device fan + host copy
+    dev = torch_mod.device("cuda:0")
+    rgba = torch_mod.empty(h * w * 4, dtype=torch_mod.uint8, device=dev)
+    mask = torch_mod.empty(h * w, dtype=torch_mod.uint8, device=dev)
+    uv = torch_mod.empty(h * w * 2, dtype=torch_mod.float32, device=dev)
+    ctx.render_rows(frame, scene, w, h, 0, h, rgba, mask, uv)
+    torch_mod.cuda.synchronize()
+    row0 = row_step // 2
+    nrows = (h - row0 + row_step - 1) // row_step
+    m = mask.view(h, w)[row0::row_step].cpu().numpy()
+    u = uv.view(h, w, 2)[row0::row_step].cpu().numpy()
+    ctx.close()
+    ref = B.f64_rows(frame, scene, w, h, row0, nrows, row_step, fan=fan)
+    st = B.compare_fan(m, u, ref, fan)
+    st.update(config=cfgname, rows=f"{row0}::{row_step} ({nrows} rows)",
+              reference="f64 literal shader, the same f32 fan (400 nodes)")
+    _record(name, st)
+    assert st["mask_flips_outside_edge"] == 0, st
+    assert st["uv_over_bar_outside_band"] == 0 and st["uv_max"] <= B.UV_BAR, st
+    assert st["in_band_over_model"] == 0 and st["max_err_over_model"] <= 1.0, st
+    assert st["edge_pixels"] <= 0.001 * st["pixels"] and st["uv_band_pixels"] <= 0.01 * st["pixels"], st

@@ -395,6 +395,79 @@ def test_fan_stream_switches_match_one_stream(geo, torch_mod):
         assert np.array_equal(a, b), (i, plan[i])
 
 
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_random_stream_plans_match_one_stream(geo, torch_mod, seed):
+    """Seeded random plans over ten streams (more than the context's eight
+    render slots, so slots are evicted mid-plan): fan solves, host fan
+    uploads, fan-mode draws (some of them two or three per fan), and
+    direct-mode draws with per-call step counts (the learned tile order is
+    rebuilt across streams), each on a random stream with no host sync;
+    every output equals the same plan run on one stream with a sync after
+    every call."""
+    from schwarzschild_raytracer_wgpu_amd.scenes import make_sky
+
+    rng = np.random.default_rng(seed)
+    w, h = 1920, 1080
+    dw, dh = 480, 272
+    dev = torch_mod.device("cuda:0")
+    sky = make_sky("equirect", (512, 256))
+    plan = []  # (op, stream index, radius)
+    for _ in range(36):
+        u = rng.random()
+        op = "solve" if u < 0.3 else "set" if u < 0.38 else "draw" if u < 0.8 else "direct"
+        plan.append((op, int(rng.integers(0, 10)), float(2.3 + 1.5 * rng.random())))
+    plan.insert(0, ("solve", 0, 2.5))
+    host_fans = {i: O.solve_ray_fan(50.0, 1.0, 1000, math.pi / 100, 400, r) for i, (op, _, r) in enumerate(plan)
+                 if op == "set"}
+
+    def run(streams, sync_each):
+        ctx = geo.Context(0)
+        ctx.set_sky(sky)
+        obs = geo.Observer(1.0, math.pi / 2, w, h)
+        dobs = geo.Observer(1.0, math.pi / 2, dw, dh)
+        outs = []
+        torch_mod.cuda.synchronize()
+        fan_r = None
+        for i, (op, k, r) in enumerate(plan):
+            s = streams[k]
+            if op == "solve":
+                obs.set_position(r, 0.0, 0.1)
+                fan_r = obs.get_radial_position()
+                ctx.solve_ray_fan(50.0, 1.0, 1000, math.pi / 100, 400, fan_r, stream=s, host=False)
+            elif op == "set":
+                ctx.set_fan(host_fans[i])
+                obs.set_position(r, 0.0, 0.1)
+                fan_r = obs.get_radial_position()
+            elif op == "draw":
+                obs.set_position(fan_r * 0.999, 0.0, 0.1)  # the pose moves, the fan stays
+                scene = geo.make_scene(1.0, 50.0, fan_r, math.pi / 100, 1000, geo.GEO_MODE_FAN)
+                t = torch_mod.empty(w * h * 4, dtype=torch_mod.uint8, device=dev)
+                ctx.render_rows(obs.calc_transformation_pipeline(), scene, w, h, 0, h, t, stream=s)
+                outs.append(t)
+            else:
+                dobs.set_position(r, 0.0, 0.1)
+                scene = geo.make_scene(1.0, 50.0, dobs.get_radial_position(), math.pi / 100, 512,
+                                       geo.GEO_MODE_DIRECT)
+                t = torch_mod.empty(dw * dh * 4, dtype=torch_mod.uint8, device=dev)
+                st = torch_mod.zeros(1, dtype=torch_mod.int64, device=dev)
+                ctx.render_rows(dobs.calc_transformation_pipeline(), scene, dw, dh, 0, dh, t, stream=s,
+                                steps_total=st)
+                outs += [t, st]
+            if sync_each:
+                torch_mod.cuda.synchronize()
+        torch_mod.cuda.synchronize()
+        res = [t.cpu().numpy() for t in outs]
+        ctx.close()
+        return res
+
+    cur = torch_mod.cuda.current_stream(dev)
+    ref = run([cur] * 10, True)
+    got = run([cur] + [torch_mod.cuda.Stream(dev) for _ in range(9)], False)
+    assert len(ref) == len(got)
+    for i, (a, b) in enumerate(zip(ref, got)):
+        assert np.array_equal(a, b), i
+
+
 def test_fan_plain_draw_bitexact(geo, torch_mod):
     """The fan-mode draw with no output but the colour (a lane draws two
     pixels, 8 rows apart, loads of both in flight): bit for bit the oracle's

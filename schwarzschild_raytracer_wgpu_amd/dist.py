@@ -227,8 +227,9 @@ class ShardedFrame:
         self.batch = bool(batch_launch) and self.K > 1
         if self.batch and self.K > GEO_MAX_BATCH_FRAMES:
             raise ValueError(f"batch_launch: at most {GEO_MAX_BATCH_FRAMES} frames per gather")
-        self.pending_frames = []     # batch mode: the open batch's uniforms
-        self.pending_scene = None    # and the scene its steps passed
+        self.pending_frames = []     # batch mode: the open batch's uniforms not yet rendered,
+        self.pending_scene = None    # the scene their steps passed (None = the object's)
+        self.pending_first = 0       # and the slot of the first of them
         L = self.layout
         self.row_bytes = width * 4
         # one frame's packed bands: rank 0's share, or the largest peer share
@@ -308,10 +309,10 @@ class ShardedFrame:
         k = (i // self.K) % 2 % self.S if self.batch else i % self.S
         return self.stream0 if k == 0 else self.extra[k - 1]
 
-    def render_batch(self, b: int, frames, scene=None, events=None, stream=None) -> None:
-        """The frames of batch buffer b (slots 0 .. len(frames) - 1) in one
-        launch (geo_render_band_set_frames), on `stream` (a handle; default the
-        buffer's render stream)."""
+    def render_batch(self, b: int, frames, scene=None, events=None, stream=None, first: int = 0) -> None:
+        """The frames of batch buffer b (slots first .. first + len(frames) - 1)
+        in one launch (geo_render_band_set_frames), on `stream` (a handle;
+        default the buffer's render stream)."""
         import ctypes
 
         from ._lib import GeoFrame, check
@@ -325,7 +326,7 @@ class ShardedFrame:
         self._frame_arr = (GeoFrame * len(frames))(*frames)
         st = self.lib.geo_render_band_set_frames(
             self._ctx_h, self._frame_arr, len(frames), self._scene_ref if scene is None else ctypes.byref(scene),
-            self.width, self.height, band_h, row0, cycle, nb, self._lv[b][0], self.slice, None, sh)
+            self.width, self.height, band_h, row0, cycle, nb, self._lv[b][first], self.slice, None, sh)
         if st != 0:
             check("geo_render_band_set_frames", st)
 
@@ -394,7 +395,14 @@ class ShardedFrame:
 
     def _step_batch(self, b: int, sub: int, events, scene, frame) -> None:
         """Batch mode: record frame `sub` of the open batch; at its K-th frame
-        render the batch in one launch, pack it (peers) and launch its gather."""
+        render the batch in one launch, pack it (peers) and launch its gather.
+        A launch's frames share one scene (geo_render_band_set_frames): a step
+        whose scene differs from the pending frames' first renders those."""
+        if self.pending_frames and bytes(self.scene if scene is None else scene) != bytes(
+                self.scene if self.pending_scene is None else self.pending_scene):
+            self._flush_batch(b)
+        if not self.pending_frames:
+            self.pending_first = sub
         self.pending_frames.append(self.frame if frame is None else frame)
         self.pending_scene = scene  # a partial batch flushed by drain() keeps the steps' scene
         self.rendered = sub + 1
@@ -405,15 +413,17 @@ class ShardedFrame:
             self.rendered = 0
 
     def _flush_batch(self, b: int, events=None, scene=None) -> None:
-        n = len(self.pending_frames)
+        n, first = len(self.pending_frames), self.pending_first
+        if not n:
+            return
         scene = self.pending_scene if scene is None else scene
         k = b % self.S
         sh = self._sh[k]
         self.ev_free[b].wait(sh)
-        self.render_batch(b, self.pending_frames, scene=scene, events=events, stream=sh)
+        self.render_batch(b, self.pending_frames, scene=scene, events=events, stream=sh, first=first)
         self.pending_frames = []
         if self.bpp == 3 and self.rank != 0:
-            st = self.lib.geo_pack_rgb(self._ctx_h, self._lv[b][0], n * self.slice // 4, self._sv[b][0], sh)
+            st = self.lib.geo_pack_rgb(self._ctx_h, self._lv[b][first], n * self.slice // 4, self._sv[b][first], sh)
             if st != 0:
                 from ._lib import check
 

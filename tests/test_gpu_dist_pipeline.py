@@ -215,3 +215,69 @@ def test_assemble_lead_matches_host_assembly(W, H, B, world, lead, bpp, nframes)
         ref = torch.zeros(H * W * 4, dtype=torch.uint8)
         assemble(ref, blocks, L, W * 4, frame=f, frame_stride=[own_sl] + [peer_stride] * (world - 1))
         assert torch.equal(got[f * H * W * 4:(f + 1) * H * W * 4], ref), f
+
+
+@pytest.mark.parametrize("S", [1, 2])
+def test_batch_splits_on_scene_change(S):
+    """Batch mode, a peer rank: a launch's frames share one scene, so a step
+    whose scene differs from the pending frames' renders those first (into
+    their slots), and the batch's gather still sends all K frames; every sent
+    frame equals that frame's own render with its own scene."""
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    import schwarzschild_raytracer_wgpu_amd as g
+    from schwarzschild_raytracer_wgpu_amd.dist import ShardedFrame
+    from schwarzschild_raytracer_wgpu_amd.scenes import make_sky
+
+    class PeerGather:
+        def __init__(self):
+            self.stream = torch.cuda.Stream()
+            self.sent = []
+
+        def gather(self, src, gather_list=None, dst=0, async_op=True):
+            ready = torch.cuda.Event()
+            ready.record(torch.cuda.current_stream())
+            with torch.cuda.stream(self.stream):
+                self.stream.wait_event(ready)
+                self.sent.append(src.clone())
+                done = torch.cuda.Event()
+                done.record(self.stream)
+            return _Work(torch, done)
+
+    W, H, B, world, rank, K = 256, 144, 8, 2, 1, 4
+    dev = torch.device("cuda:0")
+    ctx = g.Context(0)
+    ctx.set_sky(make_sky("equirect", (128, 64)))
+    poses = []
+    for r in (2.5, 3.4):
+        obs = g.Observer(1.0, math.pi / 2, W, H)
+        obs.set_position(r, 0.0, 0.1)
+        rr = obs.get_radial_position()
+        poses.append((obs.calc_transformation_pipeline(),
+                      g.make_scene(1.0, 50.0, rr, math.pi / 100, 256, g.GEO_MODE_DIRECT)))
+    which = [0, 0, 1, 0, 1, 1, 1, 1, 0, 0]  # scene changes inside batches 0 and 2, none in batch 1
+    pg = PeerGather()
+    sf = ShardedFrame(ctx, poses[0][0], poses[0][1], W, H, B, rank, world, dev, dist=pg, frames_per_gather=K,
+                      render_streams=S, batch_launch=True)
+    assert sf.batch and sf.bpp == 3
+    for i, p in enumerate(which):
+        sf.step(i, frame=poses[p][0], scene=poses[p][1])
+    sf.drain()
+    torch.cuda.synchronize()
+    assert len(pg.sent) == 3 and sf.frames_done == len(which)
+    L = sf.layout
+    ref = []
+    for frame, scene in poses:
+        one = torch.zeros(sf.slice, dtype=torch.uint8, device=dev)
+        ctx.render_band_set(frame, scene, W, H, L.band_height(), L.row0(), L.cycle_rows, L.nbands(), one)
+        packed = torch.empty(sf.tslice, dtype=torch.uint8, device=dev)
+        ctx.pack_rgb(one, sf.slice // 4, packed)
+        ref.append(packed)
+    torch.cuda.synchronize()
+    assert not torch.equal(ref[0], ref[1])
+    for i, p in enumerate(which):
+        batch = pg.sent[i // K]
+        got = batch[(i % K) * sf.tslice:(i % K + 1) * sf.tslice]
+        assert torch.equal(got, ref[p]), i

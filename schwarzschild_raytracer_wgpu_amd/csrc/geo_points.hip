@@ -1,20 +1,23 @@
 // geo_points.hip — the accretion-disk point path on gfx950.
 //
 //   geo_rays_kernel     RayConnector::{reset_ray, update_ray} for a batch of
-//                       connectors, one lane each (SR/simulation/ray_connector.rs:27-132)
-//   geo_orbits_kernel   PointCloud::update's orbit half: Orbit::do_step + the
-//                       respawn of fallen particles, f64, one lane per point
-//                       (SR/schwarzschild_point_shader/point_cloud.rs:117-141, orbit.rs:84-167)
+//                       connectors, one lane each (SR/simulation/ray_connector.rs:27-132);
+//                       <ORBITS>: the whole PointCloud::update with orbits in one
+//                       launch: each connector's lane steps its point's f64 orbit
+//                       (Orbit::do_step + the respawn of fallen particles), then
+//                       its respawn reset and its update_ray
+//                       (SR/schwarzschild_point_shader/point_cloud.rs:117-148, orbit.rs:84-167)
 //   geo_draw_kernel     the point pipeline: vs_main + PointList raster of the
 //                       red fs_main colour, REPLACE blend (shader.wgsl:36-74, pipeline.rs:55-74)
 //
-// Layout (HBM): node values in 64-connector tiles, u[(c/64)*48*64 + node*64 +
-// c%64] (48 x 4 B per connector; a wave's load of one node is 256 contiguous
-// bytes and its 48 loads one contiguous 12-KB block), point positions x[n] y[n]
-// z[n], one needs_reset byte per connector, vertices float4 per connector
-// (near-side connectors first, then far-side: get_vertices /
-// get_vertices_farside).  The 48-node state, the Thomas factors and residuals
-// live in VGPRs for the whole call (no LDS, no scratch).
+// Layout (HBM): node values in 64-connector tiles of node quads,
+// u[(c/64)*48*64 + (node/4)*256 + (c%64)*4 + node%4] (48 x 4 B per connector;
+// a lane moves them with 12 16-B loads, a wave's 12 loads one contiguous 12-KB
+// block), point positions x[n] y[n] z[n], one needs_reset byte per connector,
+// vertices float4 per connector (near-side connectors first, then far-side:
+// get_vertices / get_vertices_farside), orbit states and generators twice
+// (read one copy, write the other).  The 48-node state, the Thomas factors
+// and residuals live in VGPRs for the whole call (no LDS, no scratch).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -33,7 +36,6 @@ namespace {
 // 64-connector tiles of node quads (16-B loads and stores): +4.5 % over
 // single-node tiles, which were +4.5 % over node-major SoA.
 constexpr int kRaysBlock = 64;
-constexpr int kOrbitBlock = 64;  // f64 orbit lanes: few points, long serial chains
 
 // fastrand 2.0.1's generator (wyrand) and its f64 mapping, restated: one
 // independent stream per point (the reference draws from one OS-seeded stream
@@ -75,12 +77,17 @@ struct RaysArgs {
     float rs;
     float ox, oy, oz;            // the other end, when `other` is null
     const float* other;          // per-point other ends (x,y,z interleaved) or null
-    const float* pos;            // SoA x[n] y[n] z[n]
-    const uint8_t* respawn;      // per point: respawned this frame (RESPAWN pass only)
-    const float* respawn_pos;    // SoA
+    float* pos;                  // SoA x[n] y[n] z[n] (ORBITS: written, the stepped positions)
     float* u;                    // [48][n_conn]
     uint8_t* needs_reset;        // [n_conn]
     float4* out;                 // [n_conn]
+    // ORBITS: the orbit state in and out (two buffers, swapped per update:
+    // both connectors of a point step it from the same input)
+    double dt;
+    const geo64::Orbit* orb_in;
+    geo64::Orbit* orb_out;
+    const uint64_t* rng_in;
+    uint64_t* rng_out;
 };
 
 // Node-value stream: read once and written once per call, with non-temporal
@@ -93,12 +100,19 @@ __device__ __forceinline__ void st4_(float* p, f4_ v) {
     __builtin_nontemporal_store(v, reinterpret_cast<f4_*>(p));
 }
 
-// RESPAWN = false: one RayConnector call per connector (update_ray / reset_ray).
-// RESPAWN = true: the respawn pre-pass of PointCloud::update with orbits
-// (point_cloud.rs:129-134) — only the connectors of respawned points run, a
-// reset_ray at the new position; the regular pass follows.  Two launches keep
-// one solve per lane (VGPR budget: 48 nodes + 46 + 46 Thomas values).
-template <bool RESPAWN>
+// One RayConnector call per connector (update_ray / reset_ray).
+// ORBITS: PointCloud::update with orbits (point_cloud.rs:117-148) in one
+// launch.  The lane first steps its point's orbit (f64, Orbit::do_step) and
+// respawns a particle that hit the singularity or fell inside rs; the near
+// side's lane stores the orbit, its generator and the position.  A respawned
+// point's connector then runs reset_ray at the NEW position (:129-134), whose
+// nodes feed this frame's update_ray at the PRE-respawn position: the
+// reference sets the new position, resets the rays, then sets orbit_pos --
+// computed before the respawn -- again (:129-140).  Both calls run in the
+// lane's VGPRs (the first writes the nodes the second loads); before round 4
+// they were three launches (orbits, respawn resets, updates) whose boundaries
+// were most of a 5000-point update's latency.
+template <bool ORBITS>
 __global__ __launch_bounds__(kRaysBlock) void geo_rays_kernel(const RaysArgs a) {
     const uint32_t c = blockIdx.x * kRaysBlock + threadIdx.x;
     if (c >= a.n_conn) return;
@@ -106,8 +120,6 @@ __global__ __launch_bounds__(kRaysBlock) void geo_rays_kernel(const RaysArgs a) 
     const bool far = a.sides == GEO_RAYS_FAR ? true : c >= a.n_points;
     const uint32_t p = c >= a.n_points ? c - a.n_points : c;
     const uint32_t n = a.n_points;
-    if (RESPAWN && !a.respawn[p]) return;
-    float u[geo::kRayNodes];
     bool needs = a.needs_reset[c] != 0;
     float ox = a.ox, oy = a.oy, oz = a.oz;
     if (a.other) {
@@ -115,16 +127,49 @@ __global__ __launch_bounds__(kRaysBlock) void geo_rays_kernel(const RaysArgs a) 
         oy = a.other[3 * (size_t)p + 1];
         oz = a.other[3 * (size_t)p + 2];
     }
-    const float* src = RESPAWN ? a.respawn_pos : a.pos;
-    const float px = src[p], py = src[n + p], pz = src[2 * n + p];
-    const bool reset = RESPAWN || a.reset != 0;
+    float px, py, pz;
+    bool respawned = false;
+    float qx = 0.f, qy = 0.f, qz = 0.f;  // the respawn position
+    if (ORBITS) {
+        geo64::Orbit o = a.orb_in[p];
+        o.do_step(a.dt);
+        const geo64::V3 op = o.get_position();
+        px = (float)op.x;
+        py = (float)op.y;
+        pz = (float)op.z;
+        uint64_t rng = a.rng_in[p];
+        if (o.is_singular() || geo::dot3_(px, py, pz, px, py, pz) <= a.rs * a.rs) {
+            (void)spawn_orbit((double)a.rs, &rng, &o);  // r >= 16 > rs (checked at create): never None
+            const geo64::V3 np = o.get_position();
+            qx = (float)np.x;
+            qy = (float)np.y;
+            qz = (float)np.z;
+            respawned = true;
+        }
+        if (c < n) {  // the point's first connector stores its state
+            a.orb_out[p] = o;
+            a.rng_out[p] = rng;
+            a.pos[p] = px;
+            a.pos[n + p] = py;
+            a.pos[2 * n + p] = pz;
+        }
+    } else {
+        px = a.pos[p];
+        py = a.pos[n + p];
+        pz = a.pos[2 * n + p];
+    }
+    const bool reset = a.reset != 0;
     // node quads in 64-connector tiles, u[(c/64)*48*64 + (i/4)*256 + (c%64)*4 + i%4]: a lane moves
     // its 48 nodes with 12 16-B loads and stores, a wave's quad q is one contiguous 1-KB block.
     // Without a reset pending, ray_connect reads every node (the jump test reads node 0 first),
     // so they are loaded up front; with one, none is read.
     float* const ug = a.u + (size_t)(c / 64u) * (geo::kRayNodes * 64u) + (c % 64u) * 4u;
-    float v[geo::kRayNodes];
-    if (!reset && !needs) {
+    float u[geo::kRayNodes], v[geo::kRayNodes];
+    if (ORBITS && respawned) {
+        // reset_ray at the new position (reads no node): its nodes are v
+        (void)geo::ray_connect(a.rs, !far, qx, qy, qz, ox, oy, oz, true, a.iterations, &needs,
+                               [&](int i) { return v[i]; }, v);
+    } else if (!reset && !needs) {
 #pragma unroll
         for (int q = 0; q < geo::kRayNodes / 4; ++q) {
             const f4_ t = ld4_(ug + q * 256);
@@ -140,39 +185,7 @@ __global__ __launch_bounds__(kRaysBlock) void geo_rays_kernel(const RaysArgs a) 
     for (int q = 0; q < geo::kRayNodes / 4; ++q)
         st4_(ug + q * 256, f4_{u[4 * q], u[4 * q + 1], u[4 * q + 2], u[4 * q + 3]});
     a.needs_reset[c] = needs ? 1 : 0;
-    if (!RESPAWN && a.out) a.out[c] = make_float4(px, py, pz, angle);
-}
-
-// PointCloud::update, orbit half (point_cloud.rs:119-141): step, then respawn
-// a particle that hit the singularity or fell inside rs.  The connectors get
-// the PRE-respawn position for this frame's update_ray (the reference sets
-// the new position, resets the rays, then sets orbit_pos — computed before
-// the respawn — again, :129-140); respawn_pos carries the new one.
-__global__ __launch_bounds__(kOrbitBlock) void geo_orbits_kernel(uint32_t n, double dt, float rs, geo64::Orbit* orbits,
-                                                                 uint64_t* rng, float* pos, uint8_t* respawn,
-                                                                 float* respawn_pos) {
-    const uint32_t i = blockIdx.x * kOrbitBlock + threadIdx.x;
-    if (i >= n) return;
-    geo64::Orbit o = orbits[i];
-    o.do_step(dt);
-    const geo64::V3 op = o.get_position();
-    const float x = (float)op.x, y = (float)op.y, z = (float)op.z;
-    uint8_t rsp = 0;
-    if (o.is_singular() || geo::dot3_(x, y, z, x, y, z) <= rs * rs) {
-        uint64_t s = rng[i];
-        (void)spawn_orbit((double)rs, &s, &o);  // r >= 16 > rs (checked at create): never None
-        rng[i] = s;
-        const geo64::V3 np = o.get_position();
-        respawn_pos[i] = (float)np.x;
-        respawn_pos[n + i] = (float)np.y;
-        respawn_pos[2 * n + i] = (float)np.z;
-        rsp = 1;
-    }
-    orbits[i] = o;
-    respawn[i] = rsp;
-    pos[i] = x;
-    pos[n + i] = y;
-    pos[2 * n + i] = z;
+    if (a.out) a.out[c] = make_float4(px, py, pz, angle);
 }
 
 struct DrawArgs {
@@ -212,11 +225,11 @@ struct geo_rays {
     uint8_t* needs_reset = nullptr;
     float* other = nullptr;        // per-point staging [n_points][3]
     float4* verts = nullptr;       // [n_conn]
-    // orbits (geo_points only)
+    // orbits (geo_points only): two copies of the state, [2][n_points];
+    // the update reads copy orb_cur and writes the other
     geo64::Orbit* orbits = nullptr;
     uint64_t* rng = nullptr;
-    uint8_t* respawn = nullptr;
-    float* respawn_pos = nullptr;
+    uint32_t orb_cur = 0;
     // geo_rays handles: the last geo_rays_update (whatever its stream).  The
     // next update waits for it (it reads and writes the same state), and
     // geo_rays_set_positions waits for it before overwriting the positions.
@@ -243,7 +256,7 @@ namespace {
 
 void rays_free(geo_rays* r) {
     for (void* p : {(void*)r->pos, (void*)r->u, (void*)r->needs_reset, (void*)r->other, (void*)r->verts,
-                    (void*)r->orbits, (void*)r->rng, (void*)r->respawn, (void*)r->respawn_pos})
+                    (void*)r->orbits, (void*)r->rng})
         if (p) (void)hipFree(p);
 }
 
@@ -272,8 +285,9 @@ int rays_init(geo_rays* r, geo_ctx* ctx, float rs, uint32_t n_points, uint32_t s
     return GEO_OK;
 }
 
+// ORBITS (dt >= 0): PointCloud::update with orbits, one launch (geo_rays_kernel<true>)
 int rays_launch(geo_rays* r, float ox, float oy, float oz, const float* other_dev, uint32_t iterations, int reset,
-                bool with_respawn, float* out, hipStream_t s) {
+                double dt, float* out, hipStream_t s) {
     RaysArgs a;
     a.n_points = r->n_points;
     a.n_conn = r->n_conn;
@@ -286,19 +300,25 @@ int rays_launch(geo_rays* r, float ox, float oy, float oz, const float* other_de
     a.oz = oz;
     a.other = other_dev;
     a.pos = r->pos;
-    a.respawn = with_respawn ? r->respawn : nullptr;
-    a.respawn_pos = with_respawn ? r->respawn_pos : nullptr;
     a.u = r->u;
     a.needs_reset = r->needs_reset;
     a.out = out ? reinterpret_cast<float4*>(out) : r->verts;
+    const bool orbits = dt >= 0.0;
+    a.dt = orbits ? dt : 0.0;
+    const size_t n = r->n_points;
+    a.orb_in = orbits ? r->orbits + r->orb_cur * n : nullptr;
+    a.orb_out = orbits ? r->orbits + (1u - r->orb_cur) * n : nullptr;
+    a.rng_in = orbits ? r->rng + r->orb_cur * n : nullptr;
+    a.rng_out = orbits ? r->rng + (1u - r->orb_cur) * n : nullptr;
     if (r->n_conn == 0) return GEO_OK;
     const dim3 grid((r->n_conn + kRaysBlock - 1) / kRaysBlock);
-    if (with_respawn) {
+    if (orbits)
         hipLaunchKernelGGL(geo_rays_kernel<true>, grid, dim3(kRaysBlock), 0, s, a);
-        if (hipGetLastError() != hipSuccess) return GEO_EHIP;
-    }
-    hipLaunchKernelGGL(geo_rays_kernel<false>, grid, dim3(kRaysBlock), 0, s, a);
-    return hipGetLastError() == hipSuccess ? GEO_OK : GEO_EHIP;
+    else
+        hipLaunchKernelGGL(geo_rays_kernel<false>, grid, dim3(kRaysBlock), 0, s, a);
+    if (hipGetLastError() != hipSuccess) return GEO_EHIP;
+    if (orbits) r->orb_cur ^= 1u;
+    return GEO_OK;
 }
 
 bool finite3(const float* v) {
@@ -375,9 +395,9 @@ int geo_rays_update(geo_rays* r, const float* other_xyz, int per_point, uint32_t
                 hipSuccess ||
             hipStreamSynchronize(s) != hipSuccess)
             return GEO_EHIP;
-        st = rays_launch(r, 0.f, 0.f, 0.f, r->other, iterations, reset, false, out_vertices, s);
+        st = rays_launch(r, 0.f, 0.f, 0.f, r->other, iterations, reset, -1.0, out_vertices, s);
     } else {
-        st = rays_launch(r, other_xyz[0], other_xyz[1], other_xyz[2], nullptr, iterations, reset, false,
+        st = rays_launch(r, other_xyz[0], other_xyz[1], other_xyz[2], nullptr, iterations, reset, -1.0,
                          out_vertices, s);
     }
     if (st) return st;
@@ -414,19 +434,17 @@ int geo_points_create(geo_ctx* ctx, float schwarz_r, const float* model_xyz, uin
                 st = GEO_EINVAL;  // the reference unwraps: a vertex inside the horizon panics
             rng[i] = s;
         }
-        if (!st && ((st = dmalloc(&r->orbits, n)) || (st = dmalloc(&r->rng, n)) || (st = dmalloc(&r->respawn, n)) ||
-                    (st = dmalloc(&r->respawn_pos, 3 * (size_t)n))))
+        if (!st && ((st = dmalloc(&r->orbits, 2 * (size_t)n)) || (st = dmalloc(&r->rng, 2 * (size_t)n))))
             st = GEO_ENOMEM;
         if (!st && (hipMemcpy(r->orbits, orb.data(), sizeof(geo64::Orbit) * n, hipMemcpyHostToDevice) != hipSuccess ||
-                    hipMemcpy(r->rng, rng.data(), sizeof(uint64_t) * n, hipMemcpyHostToDevice) != hipSuccess ||
-                    hipMemset(r->respawn, 0, n) != hipSuccess))
+                    hipMemcpy(r->rng, rng.data(), sizeof(uint64_t) * n, hipMemcpyHostToDevice) != hipSuccess))
             st = GEO_EHIP;
     }
     if (!st && (hipEventCreateWithFlags(&p->updated, hipEventDisableTiming) != hipSuccess ||
                 hipEventCreateWithFlags(&p->drawn, hipEventDisableTiming) != hipSuccess))
         st = GEO_EHIP;
     // reset_ray(observer_pos) for every connector (:43, :46)
-    if (!st) st = rays_launch(r, observer_xyz[0], observer_xyz[1], observer_xyz[2], nullptr, 0u, 1, false, nullptr, 0);
+    if (!st) st = rays_launch(r, observer_xyz[0], observer_xyz[1], observer_xyz[2], nullptr, 0u, 1, -1.0, nullptr, 0);
     if (!st && hipStreamSynchronize(nullptr) != hipSuccess) st = GEO_EHIP;  // the reset above, not the device
     if (st) {
         for (hipEvent_t e : {p->updated, p->drawn})
@@ -460,14 +478,9 @@ int geo_points_update(geo_points* p, const float* observer_xyz, double dt, void*
     // update, on whatever stream, wrote the state this one reads
     if (p->drawn_rec && hipStreamWaitEvent(s, p->drawn, 0) != hipSuccess) return GEO_EHIP;
     if (p->updated_rec && hipStreamWaitEvent(s, p->updated, 0) != hipSuccess) return GEO_EHIP;
-    if (p->has_orbits) {
-        hipLaunchKernelGGL(geo_orbits_kernel, dim3((r->n_points + kOrbitBlock - 1) / kOrbitBlock), dim3(kOrbitBlock),
-                           0, s, r->n_points, dt, r->rs, r->orbits, r->rng, r->pos, r->respawn, r->respawn_pos);
-        if (hipGetLastError() != hipSuccess) return GEO_EHIP;
-    }
-    // update_ray(observer_pos, 1) (:143-146)
-    const int st = rays_launch(r, observer_xyz[0], observer_xyz[1], observer_xyz[2], nullptr, 1u, 0, p->has_orbits,
-                               nullptr, s);
+    // (with orbits: the orbit step and respawns, fused) update_ray(observer_pos, 1) (:143-146)
+    const int st = rays_launch(r, observer_xyz[0], observer_xyz[1], observer_xyz[2], nullptr, 1u, 0,
+                               p->has_orbits ? dt : -1.0, nullptr, s);
     if (st) return st;
     if (hipEventRecord(p->updated, s) != hipSuccess) return GEO_EHIP;
     p->updated_rec = true;
@@ -541,14 +554,14 @@ int geo_points_draw(geo_points* p, const geo_frame* frame, uint32_t width, uint3
     if (!g.ok) return GEO_EHIP;
     hipStream_t s = (hipStream_t)stream;
     if (p->updated_rec && hipStreamWaitEvent(s, p->updated, 0) != hipSuccess) return GEO_EHIP;
-    // the near-side mesh, then the far-side one (lib.rs:415-418, renderer.rs:256-264)
+    // the near-side mesh, then the far-side one (lib.rs:415-418, renderer.rs:256-264),
+    // in ONE launch over both: every point writes the same colour with REPLACE
+    // blending, so the order of the two meshes cannot show, and the far side's
+    // vertices (and xy slots) follow the near side's
     const int sides = (r->sides & GEO_RAYS_FAR) ? 2 : 1;
-    for (int far = 0; far < sides; ++far) {
-        const int st = draw_launch(frame, reinterpret_cast<const float*>(r->verts + (far ? r->n_points : 0)),
-                                   r->n_points, width, height, row0, nrows, out_rgba8,
-                                   out_xy ? out_xy + 2 * (size_t)far * r->n_points : nullptr, s);
-        if (st) return st;
-    }
+    const int st = draw_launch(frame, reinterpret_cast<const float*>(r->verts), (uint32_t)sides * r->n_points, width,
+                               height, row0, nrows, out_rgba8, out_xy, s);
+    if (st) return st;
     if (p->drawn_rec && hipStreamWaitEvent(s, p->drawn, 0) != hipSuccess) return GEO_EHIP;  // chain the draws
     if (hipEventRecord(p->drawn, s) != hipSuccess) return GEO_EHIP;
     p->drawn_rec = true;

@@ -450,6 +450,7 @@ def test_random_stream_plans_match_one_stream(geo, torch_mod, seed):
                                        geo.GEO_MODE_DIRECT)
                 t = torch_mod.empty(dw * dh * 4, dtype=torch_mod.uint8, device=dev)
                 st = torch_mod.zeros(1, dtype=torch_mod.int64, device=dev)
+                s.wait_stream(torch_mod.cuda.current_stream(dev))  # the zero fill ran on the current stream
                 ctx.render_rows(dobs.calc_transformation_pipeline(), scene, dw, dh, 0, dh, t, stream=s,
                                 steps_total=st)
                 outs += [t, st]

@@ -357,9 +357,10 @@ int geo_points_create(geo_ctx* ctx, float schwarz_r, const float* model_xyz, uin
 void geo_points_destroy(geo_points* pts);
 int geo_points_count(const geo_points* pts);
 /* PointCloud::update (point_cloud.rs:117-148): orbit step by dt seconds and
- * respawn (orbits), then update_ray(observer, 1) for every connector.
- * Asynchronous on `stream`; it waits for the cloud's previous update and for
- * every geo_points_draw before it, whichever streams they ran on. */
+ * respawn (orbits), then update_ray(observer, 1) for every connector, in
+ * one kernel launch.  Asynchronous on `stream`; it waits for the cloud's
+ * previous update and for every geo_points_draw before it, whichever streams
+ * they ran on. */
 int geo_points_update(geo_points* pts, const float* observer_xyz, double dt, void* stream);
 /* get_vertices / get_vertices_farside: device pointer, 4 floats per point
  * (NULL for the far side of a cloud without one). */
@@ -379,8 +380,9 @@ int geo_draw_points(geo_ctx* ctx, const geo_frame* frame, const float* vertices,
 
 /* The point meshes of a PointCloud (the near-side vertices, then the
  * far-side ones; lib.rs:415-418, renderer.rs:256-264) drawn as by
- * geo_draw_points.  out_xy (device, optional): 2 ints per connector, near
- * side first.  Stream order: the draw waits for the cloud's last
+ * geo_draw_points, both in one launch (every point writes the same colour,
+ * so their order cannot show).  out_xy (device, optional): 2 ints per
+ * connector, near side first.  Stream order: the draw waits for the cloud's last
  * geo_points_update and the next update waits for this draw and every draw
  * before it (events owned by the cloud), whichever streams they run on, so a caller may put the update
  * on a side stream where it overlaps the sphere draws.  Async on `stream`. */

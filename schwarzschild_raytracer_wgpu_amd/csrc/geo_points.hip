@@ -2,11 +2,13 @@
 //
 //   geo_rays_kernel     RayConnector::{reset_ray, update_ray} for a batch of
 //                       connectors, one lane each (SR/simulation/ray_connector.rs:27-132);
-//                       <ORBITS>: the whole PointCloud::update with orbits in one
-//                       launch: each connector's lane steps its point's f64 orbit
-//                       (Orbit::do_step + the respawn of fallen particles), then
-//                       its respawn reset and its update_ray
+//                       <kOrbitsFused>: the whole PointCloud::update with orbits in
+//                       one launch: each connector's lane steps its point's f64
+//                       orbit (Orbit::do_step + the respawn of fallen particles),
+//                       then its respawn reset and its update_ray (small clouds);
+//                       <kOrbitsStepped>: the same after geo_orbits_kernel (large ones)
 //                       (SR/schwarzschild_point_shader/point_cloud.rs:117-148, orbit.rs:84-167)
+//   geo_orbits_kernel   the orbit half alone, one lane per point
 //   geo_draw_kernel     the point pipeline: vs_main + PointList raster of the
 //                       red fs_main colour, REPLACE blend (shader.wgsl:36-74, pipeline.rs:55-74)
 //
@@ -36,6 +38,15 @@ namespace {
 // 64-connector tiles of node quads (16-B loads and stores): +4.5 % over
 // single-node tiles, which were +4.5 % over node-major SoA.
 constexpr int kRaysBlock = 64;
+// geo_rays_kernel's modes: plain RayConnector calls, or PointCloud::update
+// with orbits stepped in the ray lanes (fused) or by geo_orbits_kernel first
+enum RaysMode { kPlain = 0, kOrbitsFused = 1, kOrbitsStepped = 2 };
+// From this many connectors on (two waves per SIMD of the chip), the fused
+// update's doubled orbit work (a point's near and far lanes both step it)
+// costs more than the launch it saves: 2 M points with orbits 0.49 -> 0.54 ms
+// fused (profiles/r04u_disk_fused/points_bench_ab.txt), 5000 points 3 -> 1
+// launches and the reference's frame -12 to -16 %.
+constexpr uint32_t kFusedMaxConnectors = 1024u * 64u * 2u;
 
 // fastrand 2.0.1's generator (wyrand) and its f64 mapping, restated: one
 // independent stream per point (the reference draws from one OS-seeded stream
@@ -81,13 +92,17 @@ struct RaysArgs {
     float* u;                    // [48][n_conn]
     uint8_t* needs_reset;        // [n_conn]
     float4* out;                 // [n_conn]
-    // ORBITS: the orbit state in and out (two buffers, swapped per update:
-    // both connectors of a point step it from the same input)
+    // kOrbitsFused: the orbit state in and out (two buffers, swapped per
+    // update: both connectors of a point step it from the same input)
     double dt;
     const geo64::Orbit* orb_in;
     geo64::Orbit* orb_out;
     const uint64_t* rng_in;
     uint64_t* rng_out;
+    // kOrbitsStepped: geo_orbits_kernel's output (the stepped positions in
+    // pos, per point whether it respawned and where)
+    const uint8_t* step_respawn;
+    const float* step_respawn_pos;
 };
 
 // Node-value stream: read once and written once per call, with non-temporal
@@ -112,7 +127,7 @@ __device__ __forceinline__ void st4_(float* p, f4_ v) {
 // lane's VGPRs (the first writes the nodes the second loads); before round 4
 // they were three launches (orbits, respawn resets, updates) whose boundaries
 // were most of a 5000-point update's latency.
-template <bool ORBITS>
+template <int MODE>
 __global__ __launch_bounds__(kRaysBlock) void geo_rays_kernel(const RaysArgs a) {
     const uint32_t c = blockIdx.x * kRaysBlock + threadIdx.x;
     if (c >= a.n_conn) return;
@@ -130,7 +145,7 @@ __global__ __launch_bounds__(kRaysBlock) void geo_rays_kernel(const RaysArgs a) 
     float px, py, pz;
     bool respawned = false;
     float qx = 0.f, qy = 0.f, qz = 0.f;  // the respawn position
-    if (ORBITS) {
+    if (MODE == kOrbitsFused) {
         geo64::Orbit o = a.orb_in[p];
         o.do_step(a.dt);
         const geo64::V3 op = o.get_position();
@@ -157,6 +172,12 @@ __global__ __launch_bounds__(kRaysBlock) void geo_rays_kernel(const RaysArgs a) 
         px = a.pos[p];
         py = a.pos[n + p];
         pz = a.pos[2 * n + p];
+        if (MODE == kOrbitsStepped && a.step_respawn[p]) {
+            qx = a.step_respawn_pos[p];
+            qy = a.step_respawn_pos[n + p];
+            qz = a.step_respawn_pos[2 * n + p];
+            respawned = true;
+        }
     }
     const bool reset = a.reset != 0;
     // node quads in 64-connector tiles, u[(c/64)*48*64 + (i/4)*256 + (c%64)*4 + i%4]: a lane moves
@@ -165,7 +186,7 @@ __global__ __launch_bounds__(kRaysBlock) void geo_rays_kernel(const RaysArgs a) 
     // so they are loaded up front; with one, none is read.
     float* const ug = a.u + (size_t)(c / 64u) * (geo::kRayNodes * 64u) + (c % 64u) * 4u;
     float u[geo::kRayNodes], v[geo::kRayNodes];
-    if (ORBITS && respawned) {
+    if (MODE != kPlain && respawned) {
         // reset_ray at the new position (reads no node): its nodes are v
         (void)geo::ray_connect(a.rs, !far, qx, qy, qz, ox, oy, oz, true, a.iterations, &needs,
                                [&](int i) { return v[i]; }, v);
@@ -186,6 +207,38 @@ __global__ __launch_bounds__(kRaysBlock) void geo_rays_kernel(const RaysArgs a) 
         st4_(ug + q * 256, f4_{u[4 * q], u[4 * q + 1], u[4 * q + 2], u[4 * q + 3]});
     a.needs_reset[c] = needs ? 1 : 0;
     if (a.out) a.out[c] = make_float4(px, py, pz, angle);
+}
+
+// PointCloud::update, orbit half (point_cloud.rs:119-141), for large clouds
+// (kOrbitsStepped): step, then respawn a particle that hit the singularity or
+// fell inside rs.  pos gets the PRE-respawn position (this frame's
+// update_ray), respawn_pos the new one (the respawn's reset_ray).
+__global__ __launch_bounds__(kRaysBlock) void geo_orbits_kernel(uint32_t n, double dt, float rs,
+                                                                const geo64::Orbit* orb_in, geo64::Orbit* orb_out,
+                                                                const uint64_t* rng_in, uint64_t* rng_out, float* pos,
+                                                                uint8_t* respawn, float* respawn_pos) {
+    const uint32_t i = blockIdx.x * kRaysBlock + threadIdx.x;
+    if (i >= n) return;
+    geo64::Orbit o = orb_in[i];
+    o.do_step(dt);
+    const geo64::V3 op = o.get_position();
+    const float x = (float)op.x, y = (float)op.y, z = (float)op.z;
+    uint64_t s = rng_in[i];
+    uint8_t rsp = 0;
+    if (o.is_singular() || geo::dot3_(x, y, z, x, y, z) <= rs * rs) {
+        (void)spawn_orbit((double)rs, &s, &o);  // r >= 16 > rs (checked at create): never None
+        const geo64::V3 np = o.get_position();
+        respawn_pos[i] = (float)np.x;
+        respawn_pos[n + i] = (float)np.y;
+        respawn_pos[2 * n + i] = (float)np.z;
+        rsp = 1;
+    }
+    orb_out[i] = o;
+    rng_out[i] = s;
+    respawn[i] = rsp;
+    pos[i] = x;
+    pos[n + i] = y;
+    pos[2 * n + i] = z;
 }
 
 struct DrawArgs {
@@ -230,6 +283,8 @@ struct geo_rays {
     geo64::Orbit* orbits = nullptr;
     uint64_t* rng = nullptr;
     uint32_t orb_cur = 0;
+    uint8_t* step_respawn = nullptr;  // kOrbitsStepped: [n_points], and positions [3][n_points]
+    float* step_respawn_pos = nullptr;
     // geo_rays handles: the last geo_rays_update (whatever its stream).  The
     // next update waits for it (it reads and writes the same state), and
     // geo_rays_set_positions waits for it before overwriting the positions.
@@ -256,7 +311,7 @@ namespace {
 
 void rays_free(geo_rays* r) {
     for (void* p : {(void*)r->pos, (void*)r->u, (void*)r->needs_reset, (void*)r->other, (void*)r->verts,
-                    (void*)r->orbits, (void*)r->rng})
+                    (void*)r->orbits, (void*)r->rng, (void*)r->step_respawn, (void*)r->step_respawn_pos})
         if (p) (void)hipFree(p);
 }
 
@@ -310,12 +365,21 @@ int rays_launch(geo_rays* r, float ox, float oy, float oz, const float* other_de
     a.orb_out = orbits ? r->orbits + (1u - r->orb_cur) * n : nullptr;
     a.rng_in = orbits ? r->rng + r->orb_cur * n : nullptr;
     a.rng_out = orbits ? r->rng + (1u - r->orb_cur) * n : nullptr;
+    a.step_respawn = r->step_respawn;
+    a.step_respawn_pos = r->step_respawn_pos;
     if (r->n_conn == 0) return GEO_OK;
     const dim3 grid((r->n_conn + kRaysBlock - 1) / kRaysBlock);
-    if (orbits)
-        hipLaunchKernelGGL(geo_rays_kernel<true>, grid, dim3(kRaysBlock), 0, s, a);
-    else
-        hipLaunchKernelGGL(geo_rays_kernel<false>, grid, dim3(kRaysBlock), 0, s, a);
+    if (!orbits) {
+        hipLaunchKernelGGL(geo_rays_kernel<kPlain>, grid, dim3(kRaysBlock), 0, s, a);
+    } else if (r->n_conn < kFusedMaxConnectors) {
+        hipLaunchKernelGGL(geo_rays_kernel<kOrbitsFused>, grid, dim3(kRaysBlock), 0, s, a);
+    } else {
+        hipLaunchKernelGGL(geo_orbits_kernel, dim3((r->n_points + kRaysBlock - 1) / kRaysBlock), dim3(kRaysBlock), 0,
+                           s, r->n_points, dt, r->rs, a.orb_in, a.orb_out, a.rng_in, a.rng_out, r->pos,
+                           r->step_respawn, r->step_respawn_pos);
+        if (hipGetLastError() != hipSuccess) return GEO_EHIP;
+        hipLaunchKernelGGL(geo_rays_kernel<kOrbitsStepped>, grid, dim3(kRaysBlock), 0, s, a);
+    }
     if (hipGetLastError() != hipSuccess) return GEO_EHIP;
     if (orbits) r->orb_cur ^= 1u;
     return GEO_OK;
@@ -434,7 +498,8 @@ int geo_points_create(geo_ctx* ctx, float schwarz_r, const float* model_xyz, uin
                 st = GEO_EINVAL;  // the reference unwraps: a vertex inside the horizon panics
             rng[i] = s;
         }
-        if (!st && ((st = dmalloc(&r->orbits, 2 * (size_t)n)) || (st = dmalloc(&r->rng, 2 * (size_t)n))))
+        if (!st && ((st = dmalloc(&r->orbits, 2 * (size_t)n)) || (st = dmalloc(&r->rng, 2 * (size_t)n)) ||
+                    (st = dmalloc(&r->step_respawn, n)) || (st = dmalloc(&r->step_respawn_pos, 3 * (size_t)n))))
             st = GEO_ENOMEM;
         if (!st && (hipMemcpy(r->orbits, orb.data(), sizeof(geo64::Orbit) * n, hipMemcpyHostToDevice) != hipSuccess ||
                     hipMemcpy(r->rng, rng.data(), sizeof(uint64_t) * n, hipMemcpyHostToDevice) != hipSuccess))

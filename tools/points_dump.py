@@ -29,7 +29,9 @@ def main():
     for name, rs, n, seed, obs, dts in (("disk", 1.0, 3000, 4, (25.0, 0.0, 1.0), [1 / 60] * 120),
                                         ("falling", 15.0, 1000, 5, (40.0, 0.0, 1.0), [0.5] * 200),
                                         ("dt_changes", 15.0, 1000, 6, (40.0, 0.0, 1.0),
-                                         [0.5 if f % 3 else 0.25 for f in range(60)] + [0.4] * 5 + [0.3] * 5)):
+                                         [0.5 if f % 3 else 0.25 for f in range(60)] + [0.4] * 5 + [0.3] * 5),
+                                        # a cloud past the fused update's size (geo_points.hip kFusedMaxConnectors)
+                                        ("large", 15.0, 70000, 7, (40.0, 0.0, 1.0), [0.5] * 12)):
         pc = g.PointCloud(ctx, accretion_disk(n, seed=seed), rs, obs, True, True, seed=seed + 90)
         for f, dt in enumerate(dts):
             pc.update((obs[0], obs[1] + 0.01 * f, obs[2]), dt)

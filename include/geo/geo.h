@@ -358,7 +358,8 @@ void geo_points_destroy(geo_points* pts);
 int geo_points_count(const geo_points* pts);
 /* PointCloud::update (point_cloud.rs:117-148): orbit step by dt seconds and
  * respawn (orbits), then update_ray(observer, 1) for every connector, in
- * one kernel launch.  Asynchronous on `stream`; it waits for the cloud's
+ * one kernel launch (two, orbit step then rays, from 131072 connectors on).
+ * Asynchronous on `stream`; it waits for the cloud's
  * previous update and for every geo_points_draw before it, whichever streams
  * they ran on. */
 int geo_points_update(geo_points* pts, const float* observer_xyz, double dt, void* stream);

@@ -67,7 +67,7 @@ def _run(tmp_path, n, plan=None, argv=("--steps", "3")):
     return r, time.monotonic() - t0
 
 
-@pytest.mark.parametrize("n", [2, 3])
+@pytest.mark.parametrize("n", [2, 3, 8])  # 8: the driver's scaling run (config 4)
 def test_fan_out_and_rank0_line(tmp_path, n):
     r, _ = _run(tmp_path, n)
     assert r.returncode == 0, r.stderr[-2000:]

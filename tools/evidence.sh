@@ -1,0 +1,110 @@
+#!/bin/bash
+# The one GPU evidence script (replaces the per-session tools/gpu_r0*.sh).
+# Every step runs under its own time limit; the first failing step ends the
+# call (no retries).  Output goes to gpurun_out/<TAG>/.
+#
+#   bash tools/evidence.sh TAG STEP [STEP ...]
+#
+# STEPs:
+#   suite            pytest -m gpu (one process) + smoke()
+#   tests:<k-expr>   pytest -m gpu -k <k-expr>
+#   gloo8            the driver's N = 8 form on this one GPU with gloo:
+#                    bench.py --gpus 8 --dist-backend gloo --steps 20 --warmup 5
+#                    (self-launcher, --rank0-lead auto, batched launches,
+#                    frame_check), its wall time recorded
+#   bench:<cfg>[:<mode>[:<steps>]]
+#                    bench.py under rocprofv3 --kernel-trace --stats, the
+#                    bench line and the trace's timed-window average from the
+#                    SAME invocation (tools/trace_window.py)
+#   plain:<cfg>[:<mode>[:<steps>]]   bench.py alone (default flags)
+#   pmc:<cfg>[:<mode>]  the PMC passes (each its own rocprofv3 run)
+#   motion:<kind>    bench.py --motion <kind> (orbit | fall), learned vs natural order
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+ROOT=$(pwd)
+TAG=$1; shift
+OUT=$ROOT/gpurun_out/$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+
+heartbeat() {  # keeps gpurun's 3-minute silence watchdog informed during long quiet steps
+  (while sleep 30; do date +%T >> "$OUT/heartbeat.txt"; done) &
+  HB=$!
+}
+stop_heartbeat() { kill $HB 2>/dev/null; wait $HB 2>/dev/null; }
+
+for step in "$@"; do
+  IFS=: read -r kind a1 a2 a3 <<< "$step"
+  echo "== $step ($(date +%T))"
+  case $kind in
+    suite)
+      timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread \
+        > "$OUT/gpu_suite.txt" 2>&1
+      rc=$?; tail -3 "$OUT/gpu_suite.txt"; [ $rc -eq 0 ] || exit $rc
+      timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.txt" 2>&1
+      rc=$?; tail -1 "$OUT/smoke.txt"; [ $rc -eq 0 ] || exit $rc ;;
+    tests)
+      timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "$a1" \
+        > "$OUT/tests_${a1//[^A-Za-z0-9_]/_}.txt" 2>&1
+      rc=$?; tail -3 "$OUT/tests_${a1//[^A-Za-z0-9_]/_}.txt"; [ $rc -eq 0 ] || exit $rc ;;
+    gloo8)
+      heartbeat
+      t0=$(date +%s.%N)
+      timeout -k 10 1000 python3 bench.py --gpus 8 --dist-backend gloo --steps 20 --warmup 5 \
+        > "$OUT/gloo8_bench.json" 2> "$OUT/gloo8_bench.err"
+      rc=$?
+      t1=$(date +%s.%N)
+      stop_heartbeat
+      python3 - "$OUT" "$t0" "$t1" "$rc" <<'EOF'
+import json, sys
+out, t0, t1, rc = sys.argv[1], float(sys.argv[2]), float(sys.argv[3]), int(sys.argv[4])
+rec = {"cmd": "python3 bench.py --gpus 8 --dist-backend gloo --steps 20 --warmup 5", "rc": rc,
+       "wall_s": round(t1 - t0, 2), "driver_timeout_s": 600}
+try:
+    d = json.loads(open(out + "/gloo8_bench.json").read().strip().splitlines()[-1])
+    rec.update({k: d[k] for k in ("n_gpus", "world_size", "dist_backend", "value", "ms_per_step", "frame_check")})
+    rec["config"] = d["config"]
+    rec["per_rank"] = d["per_rank"]
+except Exception as e:  # noqa: BLE001
+    rec["parse_error"] = repr(e)
+json.dump(rec, open(out + "/gloo8_summary.json", "w"), indent=1)
+print(json.dumps({k: rec.get(k) for k in ("rc", "wall_s", "frame_check")}))
+EOF
+      [ $rc -eq 0 ] || { tail -20 "$OUT/gloo8_bench.err"; exit $rc; } ;;
+    bench|plain)
+      cfg=${a1:-cfg3_4k}; mode=${a2:-}; steps=${a3:-20}
+      margs="--steps $steps --warmup 5"; [ -n "$mode" ] && margs="$margs --mode $mode"
+      name=${cfg}${mode:+_$mode}
+      if [ $kind = plain ]; then
+        timeout -k 10 400 python3 bench.py $margs > "$OUT/${name}_bench.json" 2> "$OUT/${name}_bench.err"
+        rc=$?; [ $rc -eq 0 ] || { tail -5 "$OUT/${name}_bench.err"; exit $rc; }
+        continue
+      fi
+      ( cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$name" \
+          -o run -- python3 "$ROOT/bench.py" $margs > "$OUT/${name}_bench.json" 2> "$OUT/${name}_bench.err" )
+      rc=$?; [ $rc -eq 0 ] || { tail -5 "$OUT/${name}_bench.err"; exit $rc; }
+      tr=$(find "$OUT/prof_$name" -name 'run_kernel_trace.csv' | head -n 1)
+      st=$(find "$OUT/prof_$name" -name 'run_kernel_stats.csv' | head -n 1)
+      cp "$st" "$OUT/${name}_kernel_stats.csv"
+      python3 tools/trace_window.py "$tr" --bench "$OUT/${name}_bench.json" > "$OUT/${name}_trace_window.txt"
+      rc=$?; cat "$OUT/${name}_trace_window.txt"; [ $rc -eq 0 ] || exit $rc
+      rm -rf "$OUT/prof_$name" ;;
+    pmc)
+      cfg=${a1:-cfg3_4k}; mode=${a2:-}
+      name=${cfg}${mode:+_$mode}
+      SETS=("GRBM_GUI_ACTIVE SQ_INSTS_SALU SQ_INSTS_VALU SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES"
+            "SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_MUL_F32"
+            "SQ_THREAD_CYCLES_VALU SQ_INSTS_VALU_FLOPS_FP32 SQ_ACTIVE_INST_VALU" "FETCH_SIZE" "WRITE_SIZE")
+      EXTRA_ARGS=${mode:+--mode $mode} CONFIG=$cfg bash tools/gpu_pmc.sh "$TAG/pmc_$name" "${SETS[@]}" || exit $?
+      python3 tools/pmc_to_profile.py "$TAG/pmc_$name" "$OUT/${name}_pmc.json" "$name" > /dev/null || exit $? ;;
+    motion)
+      kind2=${a1:-orbit}
+      for disp in learned natural; do
+        timeout -k 10 300 python3 bench.py --motion "$kind2" --dispatch $disp --steps 200 --warmup 20 \
+          --no-cpu-baseline > "$OUT/motion_${kind2}_$disp.json" 2> "$OUT/motion_${kind2}_$disp.err"
+        rc=$?; [ $rc -eq 0 ] || { tail -5 "$OUT/motion_${kind2}_$disp.err"; exit $rc; }
+      done ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
+echo "evidence $TAG: all steps ok"

@@ -104,7 +104,59 @@ def parse():
     p.add_argument("--check-frame", action="store_true", help=argparse.SUPPRESS)  # the default since round 3
     p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                    help="nccl (= RCCL over xGMI); gloo stages the gather through host memory (tests only)")
-    return p.parse_args()
+    p.add_argument("--motion", default="none", choices=list(MOTIONS),
+                   help="per-frame uniforms of a moving observer for the warmup and timed frames (the reference's "
+                        "present loop: Observer::update_position + calc_transformation_pipeline every frame, "
+                        "observer.rs:105-125, renderer.rs:208-264): orbit = start_orbit(1.8) from the config's "
+                        "position, fall = start_orbit(0) (the Fall button, lib.rs:180), pan = the camera turning "
+                        "(move_camera); dt = 1/60 s.  Not the metric's line (that is one pose, config 3)")
+    p.add_argument("--dispatch", default="learned", choices=["learned", "natural"],
+                   help="workgroup dispatch order: learned longest-first (geo_set_dispatch default) or natural "
+                        "row-major")
+    p.add_argument("--share", default=None, type=_share_spec,
+                   help="'r/n' (N = 1 only): render rank r's band set of an n-rank layout and nothing else (no "
+                        "gather, no reassembly): one rank's compute at N = n, on this GPU")
+    args = p.parse_args()
+    if args.share is not None and args.gpus != 1:
+        p.error("--share emulates one rank's share on one GPU: --gpus 1 only")
+    return args
+
+
+def _share_spec(v: str):
+    r, _, n = v.partition("/")
+    try:
+        rn = (int(r), int(n))
+    except ValueError:
+        raise argparse.ArgumentTypeError(f"--share: 'r/n', got {v!r}")
+    if not (rn[1] >= 2 and 0 <= rn[0] < rn[1]):
+        raise argparse.ArgumentTypeError("--share: 0 <= r < n, n >= 2")
+    return rn
+
+
+MOTIONS = ("none", "orbit", "fall", "pan")
+
+
+def motion_frames(g, cfg, kind: str, n: int, mode: int, flags: int, tol: float, dt: float = 1.0 / 60.0):
+    """n (uniform, scene) pairs of a moving observer, one per frame, starting
+    from the config's pose (see --motion).  The scene follows the observer's
+    radius (geo_scene.r_obs), as the reference's per-frame uniform does
+    (lib.rs:292)."""
+    obs = g.Observer(cfg.rs, cfg.fov, cfg.width, cfg.height)
+    obs.set_position(*cfg.position)
+    obs.set_camera(*cfg.camera)
+    obs.set_energy(cfg.energy)
+    if kind in ("orbit", "fall") and not obs.start_orbit(1.8 if kind == "orbit" else 0.0):
+        raise SystemExit(f"--motion {kind}: no orbit from {cfg.position}")
+    out = []
+    for _ in range(n):
+        if kind == "pan":
+            obs.move_camera(6.0, 0.0)  # pixels of mouse motion per frame (observer.rs:179-188)
+        else:
+            obs.update_position((0.0, 0.0, 0.0), dt)
+        out.append((obs.calc_transformation_pipeline(),
+                    g.make_scene(cfg.rs, cfg.sphere_r, obs.get_radial_position(), cfg.step, cfg.max_steps, mode,
+                                 flags=flags, tol=tol)))
+    return out
 
 
 # --rank0-lead auto: (rank 0's bands, each peer's bands) per cycle, in the
@@ -237,6 +289,8 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    # --share r/n: this one process renders rank r's share of an n-rank layout
+    lay_rank, lay_world = args.share if args.share else (rank, world)
     ndev = torch.cuda.device_count()
     if world > ndev and args.dist_backend == "nccl":
         # RCCL refuses two ranks on one GPU ("Duplicate GPU detected")
@@ -269,6 +323,8 @@ def main():
     frame = obs.calc_transformation_pipeline()
     args.mode = args.mode or cfg.mode
     mode = {"direct": g.GEO_MODE_DIRECT, "fan": g.GEO_MODE_FAN, "adaptive": g.GEO_MODE_ADAPTIVE}[args.mode]
+    if args.motion != "none" and mode == g.GEO_MODE_FAN:
+        raise SystemExit("--motion with --mode fan: the fan-mode draw needs a fan solved per radius (not benched)")
     tol = cfg.tol if mode == g.GEO_MODE_ADAPTIVE else 0.0
     sampler_flags = g._lib.GEO_FLAG_MIPS if args.mips else 0
     scene = g.make_scene(cfg.rs, cfg.sphere_r, obs.get_radial_position(), cfg.step, cfg.max_steps, mode,
@@ -276,6 +332,8 @@ def main():
     sky = make_sky(cfg.sky, cfg.sky_size)
     ctx = g.Context(local)
     ctx.set_sky(sky)
+    if args.dispatch == "natural":
+        ctx.set_dispatch(g._lib.GEO_DISPATCH_ROW_MAJOR)
     if mode == g.GEO_MODE_FAN:
         ctx.solve_ray_fan(cfg.sphere_r, cfg.rs, cfg.max_steps, cfg.step, 400, obs.get_radial_position())
 
@@ -289,8 +347,9 @@ def main():
 
     def make_sf(ld):
         lead, peer_bands = ld
-        return ShardedFrame(ctx, frame, scene, W, H, args.band_rows, rank, world, dev, dist if world > 1 else None,
-                            host_gather=args.dist_backend == "gloo", frames_per_gather=args.frames_per_gather,
+        return ShardedFrame(ctx, frame, scene, W, H, args.band_rows, lay_rank, lay_world, dev,
+                            dist if world > 1 else None, host_gather=args.dist_backend == "gloo",
+                            frames_per_gather=args.frames_per_gather,
                             render_streams=args.render_streams or (1 if world == 1 else 2), lead=lead,
                             peer_bands=peer_bands, batch_launch=args.batch_launch != "off")
 
@@ -339,14 +398,43 @@ def main():
             sf = make_sf(best)
     L = sf.layout
 
+    # --motion: the warmup's and the timed frames' own uniforms and scenes
+    # (plain, and with GEO_FLAG_DEFER_STEPS for the timed region)
+    scene_defer = g.make_scene(cfg.rs, cfg.sphere_r, obs.get_radial_position(), cfg.step, cfg.max_steps, mode,
+                               flags=g._lib.GEO_FLAG_DEFER_STEPS | sampler_flags, tol=tol)
+    moving = None
+    if args.motion != "none":
+        mv = motion_frames(g, cfg, args.motion, args.warmup + args.steps, mode, sampler_flags, tol)
+        moving = [(fr, sc, g.make_scene(cfg.rs, cfg.sphere_r, sc.r_obs, cfg.step, cfg.max_steps, mode,
+                                         flags=g._lib.GEO_FLAG_DEFER_STEPS | sampler_flags, tol=tol))
+                  for fr, sc in mv]
+
+    def pose(i):
+        """(uniform, scene) of warmup/timed frame i (i counts from the first warmup frame)."""
+        return (None, None) if moving is None else (moving[i][0], moving[i][2])
+
     # untimed diagnostic pass: per-pixel steps + mask give the RK4 evaluations
-    # per launch (main-loop steps + 3 Newton evaluations per sphere crossing)
+    # per launch (main-loop steps + 3 Newton evaluations per sphere crossing);
+    # with --motion, of every timed frame (per-frame totals on the device)
     n_loc = max(1, L.packed_rows()) * W
     diag_mask = torch.zeros(n_loc, dtype=torch.uint8, device=dev)
     diag_steps = torch.zeros(n_loc, dtype=torch.int32, device=dev)
     diag_ctr = torch.zeros(1, dtype=torch.int64, device=dev)
     diag_uv = torch.zeros(n_loc * 2, dtype=torch.float32, device=dev) if mode == g.GEO_MODE_FAN else None
     sf.render_local(sf.bufs[0], out_mask=diag_mask, out_uv=diag_uv, out_steps=diag_steps, steps_total=diag_ctr)
+    per_frame = None  # --motion: [(steps, hits)] of each timed frame
+    if moving is not None:
+        f_steps = torch.zeros(args.steps, dtype=torch.int64, device=dev)
+        f_hits = torch.zeros(args.steps, dtype=torch.int64, device=dev)
+        m_mask = torch.zeros_like(diag_mask)
+        m_steps = torch.zeros_like(diag_steps)
+        for i in range(args.steps):
+            fr, sc = moving[args.warmup + i][:2]
+            sf.render_local(sf.bufs[1], scene=sc, frame=fr, out_mask=m_mask, out_steps=m_steps,
+                            steps_total=f_steps[i:i + 1])
+            f_hits[i] = ((m_mask == 0) & (m_steps > 0)).sum()
+        per_frame = list(zip(f_steps.tolist(), f_hits.tolist()))
+        del m_mask, m_steps
     torch.cuda.synchronize()
     # the fan-mode draw is a memory-side kernel: its algorithmic bytes are the
     # RGBA8 it writes plus the distinct sky texels its rows sample (and the fan)
@@ -360,18 +448,24 @@ def main():
     hits = int(((diag_mask == 0) & (st > 0)).sum().item())  # unwritten (clipped) rows are 0
     rows_mine = L.rows_mine()
     steps_diag = int(diag_ctr.item())
-    evals_per_launch = steps_diag + NEWTON_EVALS * hits
-    if mode == g.GEO_MODE_ADAPTIVE:
-        flops_per_launch = FLOPS_PER_ATTEMPT * steps_diag + FLOPS_PER_NEWTON_DP5 * NEWTON_EVALS * hits
-    else:
-        flops_per_launch = FLOPS_PER_EVAL * evals_per_launch
+
+    def flops_of(steps, hits):
+        if mode == g.GEO_MODE_ADAPTIVE:
+            return FLOPS_PER_ATTEMPT * steps + FLOPS_PER_NEWTON_DP5 * NEWTON_EVALS * hits
+        return FLOPS_PER_EVAL * (steps + NEWTON_EVALS * hits)
+
+    if per_frame is None:
+        per_frame = [(steps_diag, hits)] * args.steps
+    frame_flops = [flops_of(st_, h_) for st_, h_ in per_frame]
+    steps_timed = sum(st_ for st_, _ in per_frame)  # what the timed region must count
+    # per-launch figures: the average timed frame (one pose: the diagnostic frame's)
+    evals_per_launch = round(sum(st_ + NEWTON_EVALS * h_ for st_, h_ in per_frame) / args.steps)
+    flops_per_launch = sum(frame_flops) / args.steps
 
     # timed region: K frames; steps counted in the context (GEO_FLAG_DEFER_STEPS)
     # and flushed once at the end; fence-free event pairs on every k-th frame
     from schwarzschild_raytracer_wgpu_amd.timing import HipEvent
 
-    scene_defer = g.make_scene(cfg.rs, cfg.sphere_r, obs.get_radial_position(), cfg.step, cfg.max_steps, mode,
-                               flags=g._lib.GEO_FLAG_DEFER_STEPS | sampler_flags, tol=tol)
     # per-launch kernel time: event pairs inside the timed region with one
     # render stream; with two (N > 1) launches overlap by design, so the
     # launch duration is measured on isolated launches after the timed region
@@ -392,7 +486,8 @@ def main():
     spin = args.spinup_frames * world
     spin_up(sf, spin)
     for i in range(args.warmup):
-        sf.step(i)
+        fr, sc = pose(i)
+        sf.step(i, frame=fr, scene=sc)
     sf.drain()
     torch.cuda.synchronize()
     if world > 1:
@@ -400,7 +495,8 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        sf.step(i, events=evs.get(i), scene=scene_defer)
+        fr, sc = pose(args.warmup + i)
+        sf.step(i, events=evs.get(i), scene=scene_defer if sc is None else sc, frame=fr)
     sf.drain()  # joins the render streams into the current one
     ctx.steps_flush(steps_ctr)
     torch.cuda.synchronize()
@@ -417,11 +513,17 @@ def main():
     c0 = time.perf_counter()
     if sf.batch:
         for i0 in range(0, args.steps, sf.K):
-            sf.render_batch((i0 // sf.K) % 2, [frame] * min(sf.K, args.steps - i0), scene=scene_defer)
+            n_b = min(sf.K, args.steps - i0)
+            if moving is None:
+                sf.render_batch((i0 // sf.K) % 2, [frame] * n_b, scene=scene_defer)
+            else:
+                mb = moving[args.warmup + i0:args.warmup + i0 + n_b]
+                sf.render_batch((i0 // sf.K) % 2, [m[0] for m in mb], scenes=[m[2] for m in mb])
     else:
         for i in range(args.steps):
+            fr, sc = pose(args.warmup + i)
             with torch.cuda.stream(sf._render_stream(i)):
-                sf.render_local(sf.local_view(i), scene=scene_defer)
+                sf.render_local(sf.local_view(i), scene=scene_defer if sc is None else sc, frame=fr)
     sf._join()
     torch.cuda.synchronize()
     if world > 1:
@@ -432,7 +534,7 @@ def main():
     # that frame i+1's waves fill frame i's tail (what a frame loop gains
     # from pipelining; not the metric's value, whose launches do not overlap)
     pipelined = None
-    if args.pipelined and world == 1 and sf.S == 1:
+    if args.pipelined and world == 1 and sf.S == 1 and moving is None and args.share is None:
         sf2 = ShardedFrame(ctx, frame, scene, W, H, args.band_rows, rank, world, dev, None, render_streams=2)
         spin_up(sf2, max(100, args.warmup))  # its buffers' allocation idled the GPU
         torch.cuda.synchronize()
@@ -456,22 +558,36 @@ def main():
         # per-frame figure the flops per frame divide
         iso = [(HipEvent(), HipEvent()) for _ in range(20)]
         cur = torch.cuda.current_stream().cuda_stream
+        # with --motion the isolated launches draw the first timed frames (a
+        # batch: the first K; one frame: the first), and their flops are those
+        # frames'
+        nb0 = sf.K if sf.batch else 1
+        if moving is not None:
+            flops_per_launch = sum(frame_flops[:nb0]) / nb0
         for a, b in iso:
             if sf.batch:
-                sf.render_batch(0, [frame] * sf.K, scene=scene_defer, events=(a, b), stream=cur)
+                if moving is None:
+                    sf.render_batch(0, [frame] * sf.K, scene=scene_defer, events=(a, b), stream=cur)
+                else:
+                    mb = moving[args.warmup:args.warmup + sf.K]
+                    sf.render_batch(0, [m[0] for m in mb], scenes=[m[2] for m in mb], events=(a, b), stream=cur)
             else:
+                fr, sc = pose(args.warmup)
                 ctx.time_next_render(a, b)
-                sf.render_local(sf.bufs[0], scene=scene_defer)
+                sf.render_local(sf.bufs[0], scene=scene_defer if sc is None else sc, frame=fr)
         torch.cuda.synchronize()
         ctx.steps_flush(torch.zeros(1, dtype=torch.int64, device=dev))  # discard the isolated launches' steps
         evs = {i: ab for i, ab in enumerate(iso)}
         per_launch = sf.K if sf.batch else 1
     kernel_ms = sorted(a.elapsed_time(b) / per_launch for a, b in evs.values())
     kernel_ms_avg = sum(kernel_ms) / len(kernel_ms)
+    if moving is not None and not (sf.S > 1 or sf.batch):
+        # the event-timed frames' own flops over their own times
+        flops_per_launch = sum(frame_flops[i] for i in evs) / len(evs)
 
     steps_done = int(steps_ctr.item())
-    if steps_done != steps_diag * args.steps:
-        raise SystemExit(f"step counter mismatch: {steps_done} vs {steps_diag} x {args.steps}")
+    if steps_done != steps_timed:
+        raise SystemExit(f"step counter mismatch: {steps_done} vs {steps_timed} counted by the diagnostic pass")
     stats = torch.tensor([elapsed, kernel_ms_avg, elapsed_compute], dtype=torch.float64, device=rdev)
     tot = torch.tensor([steps_done, rows_mine * W * args.steps, evals_per_launch], dtype=torch.int64, device=rdev)
     per_rank = None
@@ -495,12 +611,26 @@ def main():
     # batch, as assembled for present from every rank's bands (RCCL gather +
     # geo_assemble_lead at N > 1), against a single-launch render of the frame
     frame_check = None
-    if not args.no_frame_check and rank == 0:
+    if not args.no_frame_check and rank == 0 and args.share is None:
+        # the last timed frame's own pose (with --motion each frame has its own)
         ref = torch.empty(H * W * 4, dtype=torch.uint8, device=dev)
-        ctx.render_rows(frame, scene, W, H, 0, H, ref)
+        if moving is None:
+            ctx.render_rows(frame, scene, W, H, 0, H, ref)
+        else:
+            frames_ref = []
+            nbatch = sf.last[2] + 1
+            i_last = args.steps - 1
+            for k in range(nbatch):
+                fr, sc = moving[args.warmup + i_last - (nbatch - 1 - k)][:2]
+                r_k = torch.empty(H * W * 4, dtype=torch.uint8, device=dev)
+                ctx.render_rows(fr, sc, W, H, 0, H, r_k)
+                frames_ref.append(r_k)
+            ref = frames_ref[-1]
         torch.cuda.synchronize()
         nbatch = sf.last[2] + 1
-        same = [bool(torch.equal(sf.frame_rgba(k), ref)) for k in range(nbatch)] if world > 1 else [
+        if moving is None:
+            frames_ref = [ref] * nbatch
+        same = [bool(torch.equal(sf.frame_rgba(k), frames_ref[k])) for k in range(nbatch)] if world > 1 else [
             bool(torch.equal(sf.frame_rgba(), ref))]
         frame_check = {"ok": all(same), "frames": len(same), "ranks": world,
                        "what": "rank 0's assembled frames of the timed run's last batch == a single-launch "
@@ -543,6 +673,10 @@ def main():
                    f"{cfg.max_steps} max attempts"
     else:
         metric = f"geodesic-steps·pixels/sec at {W}x{H}, {cfg.max_steps} max steps (whole job; /GPU = value/n_gpus)"
+    if args.motion != "none":
+        metric += f" [moving observer: {args.motion}]"
+    if args.share:
+        metric += f" [rank {lay_rank}'s share of {lay_world}, alone]"
         unit = "geodesic-steps·pixels/s"
         stepping = f"step pi/100, {cfg.max_steps} max RK4 steps"
     out = {
@@ -563,7 +697,10 @@ def main():
                         f"FrozenFall E={cfg.energy}, camera {tuple(round(c, 4) for c in cfg.camera)}, fov pi/2, "
                         f"{stepping}, mode {args.mode}, sky {'mip-mapped trilinear' if args.mips else 'level-0 bilinear'}",
             "width": W, "height": H, "max_steps": cfg.max_steps,
-            "parallelism": f"rowbands{world}" if world > 1 else "single",
+            "parallelism": (f"rowbands{world}" if world > 1 else
+                            f"share {lay_rank}/{lay_world} alone (no gather)" if args.share else "single"),
+            "motion": args.motion,
+            "dispatch": args.dispatch,
             "band_rows": args.band_rows,
             "frames_per_gather": sf.K,
             "rank0_lead": "%d:%d" % (L.lead, L.peer_bands),
@@ -862,10 +999,11 @@ def cpu_baseline(frame, scene, sky, W, H, args, ctx, fan=None):
     """The same per-pixel integrator on the host cores: geo_render_cpu
     (libgeo_cpu.so, include/geo/geo_cpu.h), the product's geo_pixel.h built
     for the host (g++ -O2 -ffp-contract=off), scalar, std::thread row blocks
-    (BASELINE.md §3).  Threads = every core this process may run on
-    (sched_getaffinity, SURVEY.md §8d's hardware_concurrency); the 16-thread
-    figure (the GPU box's CPU share) beside it.  One warm-up, then the median
-    of 3 runs of the frame (every 4th row above 4K).
+    (BASELINE.md §3).  Threads = the CPUs this process may run on at once:
+    min(sched_getaffinity, ceil(cgroup quota)) (SURVEY.md §8d's
+    hardware_concurrency, without oversubscribing the quota); the
+    all-affinity figure beside it when it differs.  One warm-up, then the
+    median of 3 runs of the frame (every 4th row above 4K).
 
     North_star's comparator, outside the timed runs: the CPU's rows against
     the same rows of the GPU frame (geo_render_rows): RGBA bytes, the
@@ -908,11 +1046,18 @@ def cpu_baseline(frame, scene, sky, W, H, args, ctx, fan=None):
                 times.append(dt)
         return statistics.median(times), times, steps
 
-    med, times, steps = timed(all_cores)
-    fixed16 = None
-    if all_cores != 16:
-        m16, t16, _ = timed(16)
-        fixed16 = {"threads": 16, "seconds_per_run": t16, "value": None}
+    # the headline uses the CPUs this process may actually run on at once:
+    # its affinity mask capped by the cgroup quota (an oversubscribed pool of
+    # 256 threads on a 16-CPU quota ran ~8 % slower, BENCH_r04); the
+    # all-affinity figure is reported beside it
+    quota = cpu_quota()
+    threads = min(all_cores, math.ceil(quota)) if quota else all_cores
+    med, times, steps = timed(threads)
+    all_aff = None
+    if threads != all_cores:
+        _, t_all, _ = timed(all_cores)
+        all_aff = {"threads": all_cores, "seconds_per_run": t_all, "value": None,
+                   "what": "every core in the affinity mask (oversubscribes the cgroup quota)"}
     # GEO_FLAG_MIPS with k > 1: geo_render_cpu also traces each sampled row's
     # quad partner (row + 1) for the footprint; those rows' steps are work
     # done in the timed runs, counted here (the partner rows alone, untimed)
@@ -921,16 +1066,16 @@ def cpu_baseline(frame, scene, sky, W, H, args, ctx, fan=None):
         partner = np.empty(((H - 1 + k - 1) // k, W, 4), np.uint8)
         plain = type(scene).from_buffer_copy(scene)
         plain.flags = scene.flags & ~g_flag_mips()
-        partner_steps = run(all_cores, rgba=partner, row0=1, n=(H - 1 + k - 1) // k, flags_scene=plain)
+        partner_steps = run(threads, rgba=partner, row0=1, n=(H - 1 + k - 1) // k, flags_scene=plain)
     work = steps + partner_steps
-    if fixed16 is not None:
-        fixed16["value"] = work / statistics.median(fixed16["seconds_per_run"])
+    if all_aff is not None:
+        all_aff["value"] = work / statistics.median(all_aff["seconds_per_run"])
 
     # the comparator (untimed): CPU rows with mask and UV vs the GPU frame's rows
     mask_c = np.empty((nrows, W), np.uint8)
     uv_c = np.empty((nrows, W, 2), np.float32)
     rgba_c = np.empty_like(rgba)
-    run(all_cores, rgba=rgba_c, mask=mask_c, uv=uv_c)
+    run(threads, rgba=rgba_c, mask=mask_c, uv=uv_c)
     dev = torch.device("cuda", torch.cuda.current_device())
     g_rgba = torch.empty(H * W * 4, dtype=torch.uint8, device=dev)
     g_mask = torch.empty(H * W, dtype=torch.uint8, device=dev)
@@ -955,16 +1100,16 @@ def cpu_baseline(frame, scene, sky, W, H, args, ctx, fan=None):
     return {
         "value": value,
         "unit": unit,
-        "cores": all_cores,
+        "cores": threads,
         "kind": "port",
         "cpu_model": cpu_model(),
         "cgroup_cpu_quota": cpu_quota(),
         "sample": f"{what} {W}x{H} frame ({nrows * W} pixels, {steps} steps"
                   f"{f' + {partner_steps} in the traced quad-partner rows' if partner_steps else ''}): "
-                  f"median of 3 runs after one warm-up, {all_cores} threads (every core in this process's "
-                  f"affinity mask)",
+                  f"median of 3 runs after one warm-up, {threads} threads (min(affinity mask {all_cores}, "
+                  f"cgroup quota {quota}))",
         "seconds_per_run": times,
-        "threads_16": fixed16,
+        "all_affinity": all_aff,
         "matches_gpu": {
             "ok": ok, "rows_compared": nrows, "pixels_compared": nrows * W,
             "rgba_identical": rgba_same, "mask_mismatches": mask_diff, "uv_bit_mismatches": uv_bits_diff,

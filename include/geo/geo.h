@@ -43,7 +43,8 @@
 extern "C" {
 #endif
 
-#define GEO_ABI_VERSION 4  /* 4: geo_render_band_set_frames, geo_assemble_shares */
+#define GEO_ABI_VERSION 5  /* 4: geo_render_band_set_frames, geo_assemble_shares;
+                                5: geo_render_band_set_batch, geo_dispatch_stats */
 
 typedef enum geo_status {
     GEO_OK = 0,
@@ -224,9 +225,10 @@ int geo_render_band_set(geo_ctx* ctx, const geo_frame* frame, const geo_scene* s
  * launch: frame f's uniform is frames[f], its packed bands (the layout of
  * geo_render_band_set) go to out_rgba8 + f*out_frame_stride bytes
  * (out_frame_stride a multiple of 4, at least the packed bands' bytes).  The
- * frames share the scene (observer radius, step, budget, mode), so a batch is
- * frames of an observer at one radius (Unmoving, Orbiting, or the same pose
- * drawn again); fan mode reads the context's current fan for every frame.
+ * frames share the scene (observer radius, step, budget, mode): frames of an
+ * observer at one radius (a camera pan, or the same pose drawn again); a
+ * moving observer's frames go through geo_render_band_set_batch below.  Fan
+ * mode reads the context's current fan for every frame.
  * Colour only (no mask, UV or per-pixel steps; no GEO_FLAG_MIPS); the
  * executed steps of all frames go to steps_total or, with
  * GEO_FLAG_DEFER_STEPS, to the context's accumulator.  One launch pays the
@@ -238,6 +240,16 @@ int geo_render_band_set_frames(geo_ctx* ctx, const geo_frame* frames, uint32_t n
                                uint32_t width, uint32_t height, uint32_t band_rows, uint32_t row0,
                                uint32_t row_stride, uint32_t nbands, uint8_t* out_rgba8, size_t out_frame_stride,
                                unsigned long long* steps_total, void* stream);
+
+/* geo_render_band_set_frames with a scene per frame (scenes[f] for frames[f]):
+ * a moving observer's frames, whose radius r_obs changes every frame, in one
+ * launch.  The scenes may differ in r_obs only (every other field equal, the
+ * same integration kind: all outside or all inside the horizon; a fan-mode
+ * batch draws one fan, so r_obs must agree too), else GEO_EINVAL. */
+int geo_render_band_set_batch(geo_ctx* ctx, const geo_frame* frames, const geo_scene* scenes, uint32_t nframes,
+                              uint32_t width, uint32_t height, uint32_t band_rows, uint32_t row0,
+                              uint32_t row_stride, uint32_t nbands, uint8_t* out_rgba8, size_t out_frame_stride,
+                              unsigned long long* steps_total, void* stream);
 
 /* Rank 0's reassembly for the LEAD layout (multi-GPU present with rank 0
  * taking a larger share: it renders but never sends its rows, while the peers'
@@ -279,6 +291,7 @@ int geo_pack_rgb(geo_ctx* ctx, const uint8_t* rgba, uint64_t npixels, uint8_t* r
  * ring), and the hardware dispatches workgroups in launch order, so a long
  * tile dispatched late stretches the kernel's tail.
  *   GEO_DISPATCH_LONGEST_FIRST (the default): every period-th render of a grid
+ *     (period 1: every render; 16: renders 1, 17, 33, ...)
  *     (same width, height, rows, bands, mode and sampler) records each 32 x 8
  *     tile's cost on the device, and two small kernels after it build the
  *     order, most expensive tile first, for the renders that follow; the
@@ -293,12 +306,23 @@ int geo_pack_rgb(geo_ctx* ctx, const uint8_t* rgba, uint64_t npixels, uint8_t* r
 #define GEO_DISPATCH_EXPLICIT 2 /* set by geo_set_tile_order */
 int geo_set_dispatch(geo_ctx* ctx, int mode, uint32_t period);
 
+/* GEO_DISPATCH_LONGEST_FIRST's counters since the context was created: the
+ * renders that recorded tile costs, and the rebuilt orders renders have
+ * adopted.  A rebuild runs on the context's own stream after every render
+ * issued before it; renders adopt its order once the host sees it complete
+ * (an event query, never a wait), so a recording render due while the last
+ * rebuild is still running is deferred to the next render.  Either pointer
+ * may be NULL. */
+int geo_dispatch_stats(geo_ctx* ctx, unsigned long long* costs_recorded, unsigned long long* orders_adopted);
+
 /* Times the next render of this context (geo_render_rows/bands/band_set, on
  * any stream): its kernel dispatch carries start_event and stop_event
  * (hipEvent_t created with timing), so hipEventElapsedTime gives the
  * kernel's own execution time, as a profiler's dispatch timestamps do, with
  * no marker packets around it.  (A frame of more than 65 535 tile rows: from
- * the first launch's start to the last one's end.)  Consumed by that render. */
+ * the first launch's start to the last one's end.)  Consumed by the next
+ * render call whether it succeeds or not: a refused call (GEO_EINVAL,
+ * GEO_ESTATE, ...) records neither event and drops the pair. */
 int geo_time_next_render(geo_ctx* ctx, void* start_event, void* stop_event);
 
 /* An explicit dispatch order (GEO_DISPATCH_EXPLICIT): workgroup i draws tile

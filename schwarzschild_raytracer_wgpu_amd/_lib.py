@@ -102,9 +102,15 @@ SIGNATURES = {
         [_vp, ctypes.POINTER(GeoFrame), _u32, ctypes.POINTER(GeoScene), _u32, _u32, _u32, _u32, _u32, _u32, _vp,
          ctypes.c_size_t, _vp, _vp],
     ),
+    "geo_render_band_set_batch": (
+        _int,
+        [_vp, ctypes.POINTER(GeoFrame), ctypes.POINTER(GeoScene), _u32, _u32, _u32, _u32, _u32, _u32, _u32, _vp,
+         ctypes.c_size_t, _vp, _vp],
+    ),
     "geo_steps_flush": (_int, [_vp, _vp, _vp]),
     "geo_set_tile_order": (_int, [_vp, _u32, _u32, _vp]),
     "geo_set_dispatch": (_int, [_vp, _int, _u32]),
+    "geo_dispatch_stats": (_int, [_vp, _vp, _vp]),
     "geo_time_next_render": (_int, [_vp, _vp, _vp]),
     "geo_assemble_bands": (_int, [_vp, _vp, ctypes.c_size_t, ctypes.c_size_t, _u32, _u32, _u32, _u32, _u32, _u32,
                                   _vp, _vp]),

@@ -158,6 +158,12 @@ class Context:
         GEO_DISPATCH_ROW_MAJOR."""
         check("geo_set_dispatch", lib.geo_set_dispatch(self._h, mode, period))
 
+    def dispatch_stats(self) -> tuple[int, int]:
+        """geo_dispatch_stats: (renders that recorded tile costs, rebuilt orders adopted)."""
+        rec, adopted = ctypes.c_ulonglong(), ctypes.c_ulonglong()
+        check("geo_dispatch_stats", lib.geo_dispatch_stats(self._h, ctypes.byref(rec), ctypes.byref(adopted)))
+        return rec.value, adopted.value
+
     def set_tile_order(self, tiles_x: int, tiles_y: int, order=None) -> None:
         """geo_set_tile_order: workgroup dispatch order (packed y << 16 | x per
         tile, a permutation of the grid) for renders of a tiles_x x tiles_y grid;

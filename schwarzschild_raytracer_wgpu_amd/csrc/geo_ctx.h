@@ -71,14 +71,19 @@ struct geo_ctx {
     // added into tile_cost) and two small kernels after it rebuild the order
     // from those costs, most expensive tile first, into the order buffer the
     // current one is not in; later renders of the same grid (learn_key)
-    // dispatch in that order.  The rebuild waits, on the device, for every
-    // render of the context issued before it (render_done), so no render still
-    // reads the buffer it overwrites; a render on another stream waits once
-    // for the rebuild (order_written, order_epoch vs stream_epoch).
+    // dispatch in that order.  The rebuild runs on the context's own
+    // learn_stream, after every render of the context issued before it
+    // (render_done of every slot, waited for on learn_stream only), so no
+    // render still reads the buffer it overwrites and no render stream ever
+    // waits for another (such a wait can sit behind a collective).
+    // Renders adopt the new order only once the host has seen the rebuild
+    // complete (hipEventQuery, never a wait), so none waits for it either; a
+    // recording render is deferred while a rebuild is pending (the rebuild
+    // consumes and zeroes the costs).
     // GEO_DISPATCH_EXPLICIT: geo_set_tile_order's order for its grid.
     // Orders are packed (y << 16 | x) per workgroup.
     int dispatch_mode;
-    uint32_t dispatch_period, since_learn;
+    uint32_t dispatch_period, since_learn;  // renders of the grid since its last recording one
     uint32_t learn_key[9];
     bool learn_valid;   // learn_key names a grid
     int order_cur;      // order[order_cur] is the grid's order (-1: none yet)
@@ -87,9 +92,12 @@ struct geo_ctx {
     uint32_t* class_hist;
     uint32_t tile_cap;    // tiles the buffers hold
     uint32_t explicit_x, explicit_y;  // GEO_DISPATCH_EXPLICIT's grid
-    hipEvent_t order_written;
-    uint32_t order_epoch;
-    uint32_t stream_epoch[kRenderStreams];
+    hipEvent_t order_written;   // the last rebuild, on learn_stream
+    hipStream_t learn_stream;   // created by the first rebuild
+    bool rebuild_pending;       // issued, not yet seen complete by the host
+    bool rebuild_keep;          // its order is still wanted (same grid and mode since)
+    int rebuild_nb;             // the order buffer it writes
+    unsigned long long costs_recorded, orders_adopted;  // geo_dispatch_stats
     // geo_time_next_render: events for the next render's kernel dispatch
     hipEvent_t time_start, time_stop;
 };

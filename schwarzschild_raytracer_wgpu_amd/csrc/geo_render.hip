@@ -75,9 +75,18 @@ struct FrameK {
     float kt;               // geo::aberration_kt
 };
 constexpr uint32_t kMaxBatchFrames = GEO_MAX_BATCH_FRAMES;
+// A batch's frames may each have their own observer radius (their scenes
+// differ in r_obs only, geo_render_band_set_batch): the scene constants of
+// each frame ride along (the integration kind is shared); a single-frame
+// launch reads RenderArgs::k.
 template <uint32_t NF>
 struct FrameBatch {
     FrameK f[NF];
+    geo::PixelConsts k[NF];
+};
+template <>
+struct FrameBatch<1> {
+    FrameK f[1];
 };
 
 struct RenderArgs {
@@ -264,15 +273,26 @@ __device__ __forceinline__ void shade_pixel_mips(const RenderArgs& a, float lam,
 
 // The pixel's traveled-angle result lambda' (pi/2 - angle) by mode.
 template <int MODE, int KIND>
-__device__ __forceinline__ float pixel_lambda(const RenderArgs& a, float st, float ct, float rct, uint32_t* steps) {
+__device__ __forceinline__ float pixel_lambda(const RenderArgs& a, const geo::PixelConsts& k, float st, float ct,
+                                              float rct, uint32_t* steps) {
     if constexpr (MODE == GEO_MODE_FAN) {
         *steps = 0;
         return geo::fan_lerp(a.fan, a.n_fan, st);
     } else if constexpr (MODE == GEO_MODE_ADAPTIVE) {
-        return geo::kPi2 - geo::geodesic_angle_adaptive<KIND>(a.k, st, ct, rct, steps);
+        return geo::kPi2 - geo::geodesic_angle_adaptive<KIND>(k, st, ct, rct, steps);
     } else {
-        return geo::kPi2 - geo::geodesic_angle_v<KIND>(a.k, st, ct, rct, steps);
+        return geo::kPi2 - geo::geodesic_angle_v<KIND>(k, st, ct, rct, steps);
     }
+}
+
+// The scene constants of frame z of the launch.
+template <uint32_t NF>
+__device__ __forceinline__ const geo::PixelConsts& frame_consts(const RenderArgs& a, const FrameBatch<NF>& fb,
+                                                                uint32_t z) {
+    if constexpr (NF > 1)
+        return fb.k[z];
+    else
+        return a.k;
 }
 
 // Pixels per lane: a fan-mode lane (level-0 sampler) draws two, rows
@@ -404,7 +424,7 @@ __global__ __launch_bounds__(kBlock) void geo_render_kernel(const RenderArgs a, 
             const float st = geo::central_sin(c2z);
             const float ct = geo::central_rho(c2x, c2y);
             const float rct = geo::rcpf_(ct);  // shared by the ray's 1/b^2 and its sky direction
-            const float lam = pixel_lambda<MODE, KIND>(a, st, ct, rct, &steps);
+            const float lam = pixel_lambda<MODE, KIND>(a, frame_consts(a, fb, z), st, ct, rct, &steps);
             shade_pixel(a, f.frame.central_to_uv, c2x, c2y, ct, rct, lam, steps, obase + (size_t)ly * a.width + px);
         }
     } else {
@@ -419,7 +439,7 @@ __global__ __launch_bounds__(kBlock) void geo_render_kernel(const RenderArgs a, 
         const float st = geo::central_sin(c2z);
         const float ct = geo::central_rho(c2x, c2y);
         const float rct = geo::rcpf_(ct);
-        const float lam = pixel_lambda<MODE, KIND>(a, st, ct, rct, &steps);
+        const float lam = pixel_lambda<MODE, KIND>(a, frame_consts(a, fb, z), st, ct, rct, &steps);
         // A pixel's UV is read by its own sample and by its quad partners'
         // footprints, all in this wave: a wave wholly inside the shadow reads
         // none (unless the caller asks for UV) and skips the UV and the
@@ -943,7 +963,6 @@ static int render_slot(geo_ctx* c, hipStream_t s) {
             for (int b = 0; b < 2; ++b) c->fan_read_slots[b] &= ~(1u << i);
         }
         c->render_stream[i] = s;
-        c->stream_epoch[i] = 0;  // has not waited for any order rebuild
     }
     return i;
 }
@@ -972,6 +991,7 @@ void geo_ctx_destroy(geo_ctx* c) {
     for (int i = 0; i < geo_ctx::kRenderStreams; ++i) (void)hipEventDestroy(c->render_done[i]);
     if (c->step_slots) (void)hipFree(c->step_slots);
     if (c->learn_valid || c->tile_cap) (void)hipEventSynchronize(c->order_written);
+    if (c->learn_stream) (void)hipStreamDestroy(c->learn_stream);
     for (int b = 0; b < 2; ++b)
         if (c->order[b]) (void)hipFree(c->order[b]);
     if (c->tile_cost) (void)hipFree(c->tile_cost);
@@ -1180,9 +1200,11 @@ static int launch_tiles(RenderArgs a, const FrameBatch<NF>& fb, uint32_t nframes
 // One frame (FrameBatch<1>, the kernel arguments as before batching), or a
 // batch of 2 .. kMaxBatchFrames in one launch (FrameBatch<kMaxBatchFrames>,
 // the frame in blockIdx.z; no mip-mapped sampler).
+static_assert(sizeof(RenderArgs) + sizeof(FrameBatch<kMaxBatchFrames>) <= 4096, "kernel arguments fit 4 KiB");
 template <int MODE, int KIND>
-static int launch_frames(const RenderArgs& a, const FrameK* fk, uint32_t nframes, bool mips, uint32_t tiles_x,
-                         uint32_t tiles_y, hipStream_t s, hipEvent_t done, hipEvent_t t_start, hipEvent_t t_stop) {
+static int launch_frames(const RenderArgs& a, const FrameK* fk, const geo::PixelConsts* pk, uint32_t nframes,
+                         bool mips, uint32_t tiles_x, uint32_t tiles_y, hipStream_t s, hipEvent_t done,
+                         hipEvent_t t_start, hipEvent_t t_stop) {
     if (nframes == 1) {
         FrameBatch<1> fb;
         fb.f[0] = fk[0];
@@ -1190,7 +1212,10 @@ static int launch_frames(const RenderArgs& a, const FrameK* fk, uint32_t nframes
     }
     FrameBatch<kMaxBatchFrames> fb;
     std::memset(&fb, 0, sizeof(fb));
-    for (uint32_t i = 0; i < nframes; ++i) fb.f[i] = fk[i];
+    for (uint32_t i = 0; i < nframes; ++i) {
+        fb.f[i] = fk[i];
+        fb.k[i] = pk[i];
+    }
     return launch_tiles<MODE, KIND, kMaxBatchFrames>(a, fb, nframes, false, tiles_x, tiles_y, s, done, t_start,
                                                      t_stop);
 }
@@ -1212,6 +1237,7 @@ static int ensure_tiles(geo_ctx* c, uint32_t n) {
     c->tile_cap = 0;
     c->order_cur = -1;
     c->learn_valid = false;
+    c->rebuild_pending = false;  // order_written synchronised above
     const size_t chunks = (n + kOrderChunk - 1) / kOrderChunk;
     if (hipMalloc(&c->order[0], n * sizeof(uint32_t)) != hipSuccess ||
         hipMalloc(&c->order[1], n * sizeof(uint32_t)) != hipSuccess ||
@@ -1229,12 +1255,26 @@ static int ensure_tiles(geo_ctx* c, uint32_t n) {
     return GEO_OK;
 }
 
+// A render call refused before render_impl: the timing pair of
+// geo_time_next_render is dropped too (it belongs to that call alone).
+static int invalid_call(geo_ctx* c) {
+    if (c) c->time_start = c->time_stop = nullptr;
+    return GEO_EINVAL;
+}
+
 // frames: nframes uniforms (1 .. kMaxBatchFrames); frame f's output starts
 // out_frame_stride bytes after frame f - 1's (a batch draws colour only).
+// scene_per_frame: `scene` points at nframes scenes, frame f's at scene[f]
+// (they may differ in r_obs only); otherwise one scene for every frame.
 static int render_impl(geo_ctx* c, const geo_frame* frames, uint32_t nframes, size_t out_frame_stride,
-                       const geo_scene* scene, uint32_t width, uint32_t height, uint32_t row0, uint32_t nrows,
+                       const geo_scene* scene, bool scene_per_frame, uint32_t width, uint32_t height, uint32_t row0, uint32_t nrows,
                        uint32_t band_rows, uint32_t band_stride, uint8_t* out_rgba8, uint8_t* out_mask,
                        float* out_uv, uint32_t* out_steps, unsigned long long* steps_total, void* stream) {
+    // geo_time_next_render's events belong to this render alone, on every
+    // exit path: a call that fails validation drops them (a later render
+    // must not record the caller's pair)
+    const hipEvent_t t_start = c->time_start, t_stop = c->time_stop;
+    c->time_start = c->time_stop = nullptr;
     if (scene->mode != GEO_MODE_DIRECT && scene->mode != GEO_MODE_FAN && scene->mode != GEO_MODE_ADAPTIVE)
         return GEO_EINVAL;
     if ((scene->flags & ~(GEO_FLAG_DEFER_STEPS | GEO_FLAG_COMPOSITE | GEO_FLAG_MIPS)) != 0) return GEO_EINVAL;
@@ -1261,14 +1301,27 @@ static int render_impl(geo_ctx* c, const geo_frame* frames, uint32_t nframes, si
     if (!g.ok) return GEO_EHIP;
     RenderArgs a;
     FrameK fk[kMaxBatchFrames];
+    geo::PixelConsts pk[kMaxBatchFrames];
     for (uint32_t i = 0; i < nframes; ++i) {
         const geo_frame& fr = frames[i];
         std::memcpy(&fk[i].frame, &fr, sizeof(geo_frame));
         fk[i].cam = geo::camera_consts(fr.display_to_movement, fr.movement_to_central, width, height);
         fk[i].kt = geo::aberration_kt(fr.psi_factor_and_position[0]);
+        const geo_scene& si = scene_per_frame ? scene[i] : *scene;
+        if (i > 0 && scene_per_frame) {
+            // one launch, one sampler, one integration: every field but r_obs
+            // agrees with frame 0's (a fan-mode batch draws one fan: r_obs too)
+            if (si.rs != scene->rs || si.sphere_r != scene->sphere_r || si.step != scene->step ||
+                si.max_steps != scene->max_steps || si.mode != scene->mode || si.flags != scene->flags ||
+                si.tol != scene->tol || (scene->mode == GEO_MODE_FAN && si.r_obs != scene->r_obs) ||
+                !(si.r_obs > 0.0f))
+                return GEO_EINVAL;
+        }
+        pk[i] = geo::make_consts(si.rs, si.sphere_r, si.r_obs, si.step, si.max_steps, si.tol);
+        if (geo::geodesic_kind(pk[i]) != geo::geodesic_kind(pk[0])) return GEO_EINVAL;
     }
     a.out_frame_px = out_frame_stride / 4u;
-    a.k = geo::make_consts(scene->rs, scene->sphere_r, scene->r_obs, scene->step, scene->max_steps, scene->tol);
+    a.k = pk[0];
     a.width = width;
     a.height = height;
     a.row0 = row0;
@@ -1322,9 +1375,6 @@ static int render_impl(geo_ctx* c, const geo_frame* frames, uint32_t nframes, si
     const int slot = render_slot(c, s);
     if (slot < 0) return GEO_EHIP;
     const hipEvent_t done = c->render_done[slot];
-    // geo_time_next_render's events, for this render only
-    const hipEvent_t t_start = c->time_start, t_stop = c->time_stop;
-    c->time_start = c->time_stop = nullptr;
     // The dispatch order (geo_ctx): a learned or explicit order for exactly
     // this grid, one launch, not in fan mode (its tiles all cost the same).
     bool record = false;
@@ -1339,10 +1389,28 @@ static int render_impl(geo_ctx* c, const geo_frame* frames, uint32_t nframes, si
                 std::memcpy(c->learn_key, key, sizeof(key));
                 c->learn_valid = true;
                 c->order_cur = -1;
+                c->rebuild_keep = false;  // a rebuild still running learned another grid
                 c->since_learn = c->dispatch_period;
             }
-            record = c->since_learn >= c->dispatch_period;
-            c->since_learn = record ? 0u : c->since_learn + 1u;
+            // adopt a finished rebuild: a host query, never a wait
+            if (c->rebuild_pending) {
+                const hipError_t q = hipEventQuery(c->order_written);
+                if (q == hipSuccess) {
+                    c->rebuild_pending = false;
+                    if (c->rebuild_keep) {
+                        c->order_cur = c->rebuild_nb;
+                        ++c->orders_adopted;
+                    }
+                } else if (q != hipErrorNotReady) {
+                    return GEO_EHIP;
+                }
+            }
+            // every period-th render of the grid records (period 1: every
+            // render), or the first one after that whose predecessor's
+            // rebuild has been adopted
+            if (c->since_learn < c->dispatch_period) ++c->since_learn;
+            record = c->since_learn >= c->dispatch_period && !c->rebuild_pending;
+            if (record) c->since_learn = 0u;
             if (record) {
                 int est = ensure_tiles(c, tiles_x * tiles_y);
                 if (est) return est;
@@ -1353,12 +1421,6 @@ static int render_impl(geo_ctx* c, const geo_frame* frames, uint32_t nframes, si
                 a.tile_cost = c->tile_cost;
             }
             if (c->order_cur >= 0) a.tile_order = c->order[c->order_cur];
-        }
-        // the order and the costs this render reads or adds to were last
-        // written by a rebuild, maybe on another stream
-        if ((a.tile_order || a.tile_cost) && c->stream_epoch[slot] != c->order_epoch) {
-            if (hipStreamWaitEvent(s, c->order_written, 0) != hipSuccess) return GEO_EHIP;
-            c->stream_epoch[slot] = c->order_epoch;
         }
     }
     int st;
@@ -1372,7 +1434,7 @@ static int render_impl(geo_ctx* c, const geo_frame* frames, uint32_t nframes, si
         // writer waits for its readers on the host, so they need no event)
         const bool by_slot = !c->fan_written_rec[fb] || c->fan_writer[fb] == s;
         if (!by_slot && hipStreamWaitEvent(s, c->fan_written[fb], 0) != hipSuccess) return GEO_EHIP;
-        st = launch_frames<GEO_MODE_FAN, geo::kCurvedOut>(a, fk, nframes, mips, tiles_x, tiles_y, s, done, t_start, t_stop);
+        st = launch_frames<GEO_MODE_FAN, geo::kCurvedOut>(a, fk, pk, nframes, mips, tiles_x, tiles_y, s, done, t_start, t_stop);
         if (st) return st;
         if (by_slot) {
             c->fan_read_slots[fb] |= 1u << slot;
@@ -1386,34 +1448,42 @@ static int render_impl(geo_ctx* c, const geo_frame* frames, uint32_t nframes, si
         }
     } else if (adaptive) {
         switch (geo::geodesic_kind(a.k)) {
-            case geo::kCurvedOut: st = launch_frames<GEO_MODE_ADAPTIVE, geo::kCurvedOut>(a, fk, nframes, mips, tiles_x, tiles_y, s, done, t_start, t_stop); break;
-            case geo::kCurvedIn: st = launch_frames<GEO_MODE_ADAPTIVE, geo::kCurvedIn>(a, fk, nframes, mips, tiles_x, tiles_y, s, done, t_start, t_stop); break;
-            default: st = launch_frames<GEO_MODE_ADAPTIVE, geo::kFlat>(a, fk, nframes, mips, tiles_x, tiles_y, s, done, t_start, t_stop);
+            case geo::kCurvedOut: st = launch_frames<GEO_MODE_ADAPTIVE, geo::kCurvedOut>(a, fk, pk, nframes, mips, tiles_x, tiles_y, s, done, t_start, t_stop); break;
+            case geo::kCurvedIn: st = launch_frames<GEO_MODE_ADAPTIVE, geo::kCurvedIn>(a, fk, pk, nframes, mips, tiles_x, tiles_y, s, done, t_start, t_stop); break;
+            default: st = launch_frames<GEO_MODE_ADAPTIVE, geo::kFlat>(a, fk, pk, nframes, mips, tiles_x, tiles_y, s, done, t_start, t_stop);
         }
     } else {
         switch (geo::geodesic_kind(a.k)) {
-            case geo::kCurvedOut: st = launch_frames<GEO_MODE_DIRECT, geo::kCurvedOut>(a, fk, nframes, mips, tiles_x, tiles_y, s, done, t_start, t_stop); break;
-            case geo::kCurvedIn: st = launch_frames<GEO_MODE_DIRECT, geo::kCurvedIn>(a, fk, nframes, mips, tiles_x, tiles_y, s, done, t_start, t_stop); break;
-            default: st = launch_frames<GEO_MODE_DIRECT, geo::kFlat>(a, fk, nframes, mips, tiles_x, tiles_y, s, done, t_start, t_stop);
+            case geo::kCurvedOut: st = launch_frames<GEO_MODE_DIRECT, geo::kCurvedOut>(a, fk, pk, nframes, mips, tiles_x, tiles_y, s, done, t_start, t_stop); break;
+            case geo::kCurvedIn: st = launch_frames<GEO_MODE_DIRECT, geo::kCurvedIn>(a, fk, pk, nframes, mips, tiles_x, tiles_y, s, done, t_start, t_stop); break;
+            default: st = launch_frames<GEO_MODE_DIRECT, geo::kFlat>(a, fk, pk, nframes, mips, tiles_x, tiles_y, s, done, t_start, t_stop);
         }
     }
     if (st) return st;
     if (record) {
-        // rebuild the order into the buffer not in use, after every render of
-        // the context issued so far (renders on this stream are ordered
-        // already; the others may read that buffer)
+        // rebuild the order into the buffer not in use, on the context's
+        // learn stream, after every render of the context issued so far (this
+        // one included: its launch recorded render_done[slot]); earlier
+        // renders on any stream may still read that buffer
+        ++c->costs_recorded;
+        if (!c->learn_stream && hipStreamCreateWithFlags(&c->learn_stream, hipStreamNonBlocking) != hipSuccess) {
+            c->learn_stream = nullptr;
+            return GEO_EHIP;
+        }
+        hipStream_t ls = c->learn_stream;
         const int nb = c->order_cur < 0 ? 0 : 1 - c->order_cur;
         for (int i = 0; i < c->n_render_streams; ++i)
-            if (i != slot && hipStreamWaitEvent(s, c->render_done[i], 0) != hipSuccess) return GEO_EHIP;
+            if (hipStreamWaitEvent(ls, c->render_done[i], 0) != hipSuccess) return GEO_EHIP;
         const uint32_t n = tiles_x * tiles_y;
         const uint32_t chunks = (n + kOrderChunk - 1) / kOrderChunk;
-        hipLaunchKernelGGL(geo_order_hist, dim3(chunks), dim3(256), 0, s, c->tile_cost, n, c->class_hist);
-        hipLaunchKernelGGL(geo_order_scatter, dim3(chunks), dim3(256), 0, s, c->tile_cost, n, c->class_hist, tiles_x,
+        hipLaunchKernelGGL(geo_order_hist, dim3(chunks), dim3(256), 0, ls, c->tile_cost, n, c->class_hist);
+        hipLaunchKernelGGL(geo_order_scatter, dim3(chunks), dim3(256), 0, ls, c->tile_cost, n, c->class_hist, tiles_x,
                            c->order[nb]);
         if (hipGetLastError() != hipSuccess) return GEO_EHIP;
-        if (hipEventRecord(c->order_written, s) != hipSuccess) return GEO_EHIP;
-        c->stream_epoch[slot] = ++c->order_epoch;
-        c->order_cur = nb;
+        if (hipEventRecord(c->order_written, ls) != hipSuccess) return GEO_EHIP;
+        c->rebuild_pending = true;
+        c->rebuild_keep = true;
+        c->rebuild_nb = nb;
     }
     if (call_set >= 0) {
         hipLaunchKernelGGL(geo_steps_finalize, dim3(1), dim3(kStepSlots), 0, s, a.step_slots, steps_total);
@@ -1548,6 +1618,14 @@ int geo_set_dispatch(geo_ctx* c, int mode, uint32_t period) {
     c->dispatch_period = period;
     c->learn_valid = false;  // learn again from the next render
     c->order_cur = -1;
+    c->rebuild_keep = false;
+    return GEO_OK;
+}
+
+int geo_dispatch_stats(geo_ctx* c, unsigned long long* costs_recorded, unsigned long long* orders_adopted) {
+    if (!c) return GEO_EINVAL;
+    if (costs_recorded) *costs_recorded = c->costs_recorded;
+    if (orders_adopted) *orders_adopted = c->orders_adopted;
     return GEO_OK;
 }
 
@@ -1559,6 +1637,7 @@ int geo_set_tile_order(geo_ctx* c, uint32_t tiles_x, uint32_t tiles_y, const uin
         c->dispatch_mode = GEO_DISPATCH_ROW_MAJOR;
         c->learn_valid = false;
         c->order_cur = -1;
+        c->rebuild_keep = false;
         return GEO_OK;
     }
     if (tiles_x == 0 || tiles_y == 0 || tiles_x > 0xFFFFu || tiles_y > kMaxGridY) return GEO_EINVAL;
@@ -1574,6 +1653,7 @@ int geo_set_tile_order(geo_ctx* c, uint32_t tiles_x, uint32_t tiles_y, const uin
     if (st) return st;
     // renders in flight may read either buffer, a rebuild may write one
     if (wait_renders(c) != GEO_OK || hipEventSynchronize(c->order_written) != hipSuccess) return GEO_EHIP;
+    c->rebuild_pending = false;
     if (hipMemcpy(c->order[0], order, n * sizeof(uint32_t), hipMemcpyHostToDevice) != hipSuccess) {
         c->order_cur = -1;
         return GEO_EHIP;
@@ -1591,11 +1671,11 @@ int geo_render_rows(geo_ctx* c, const geo_frame* frame, const geo_scene* scene, 
                     uint8_t* out_mask, float* out_uv, uint32_t* out_steps,
                     unsigned long long* steps_total, void* stream) {
     if (!c || !frame || !scene || !out_rgba8 || width == 0 || height == 0 || nrows == 0)
-        return GEO_EINVAL;
+        return invalid_call(c);
     if ((uint64_t)row0 + nrows > height || width > (1u << 20) || height > (1u << 20))
-        return GEO_EINVAL;
+        return invalid_call(c);
     // one band covering every row (2^21 >= nrows)
-    return render_impl(c, frame, 1, 0, scene, width, height, row0, nrows, 1u << 21, 1u << 21, out_rgba8, out_mask,
+    return render_impl(c, frame, 1, 0, scene, false, width, height, row0, nrows, 1u << 21, 1u << 21, out_rgba8, out_mask,
                        out_uv, out_steps, steps_total, stream);
 }
 
@@ -1605,13 +1685,13 @@ int geo_render_bands(geo_ctx* c, const geo_frame* frame, const geo_scene* scene,
                      uint32_t* out_steps, unsigned long long* steps_total, void* stream) {
     if (!c || !frame || !scene || !out_rgba8 || width == 0 || height == 0 || band_rows == 0 ||
         nbands == 0 || band_step == 0 || band_rows < kBandRowAlign || (band_rows & (band_rows - 1)) != 0)
-        return GEO_EINVAL;
-    if (width > (1u << 20) || height > (1u << 20)) return GEO_EINVAL;
+        return invalid_call(c);
+    if (width > (1u << 20) || height > (1u << 20)) return invalid_call(c);
     const uint64_t first = (uint64_t)band0 * band_rows;
     const uint64_t last = first + (uint64_t)(nbands - 1) * band_step * band_rows;
     const uint64_t nrows = (uint64_t)nbands * band_rows;
-    if (first >= height || last >= height || nrows > (1u << 20)) return GEO_EINVAL;
-    return render_impl(c, frame, 1, 0, scene, width, height, (uint32_t)first, (uint32_t)nrows,
+    if (first >= height || last >= height || nrows > (1u << 20)) return invalid_call(c);
+    return render_impl(c, frame, 1, 0, scene, false, width, height, (uint32_t)first, (uint32_t)nrows,
                        band_rows, band_step * band_rows, out_rgba8, out_mask, out_uv,
                        out_steps, steps_total, stream);
 }
@@ -1634,8 +1714,8 @@ int geo_render_band_set(geo_ctx* c, const geo_frame* frame, const geo_scene* sce
                         uint8_t* out_rgba8, uint8_t* out_mask, float* out_uv, uint32_t* out_steps,
                         unsigned long long* steps_total, void* stream) {
     if (!c || !frame || !scene || !out_rgba8 || !band_set_ok(width, height, band_rows, row0, row_stride, nbands))
-        return GEO_EINVAL;
-    return render_impl(c, frame, 1, 0, scene, width, height, row0, nbands * band_rows, band_rows, row_stride,
+        return invalid_call(c);
+    return render_impl(c, frame, 1, 0, scene, false, width, height, row0, nbands * band_rows, band_rows, row_stride,
                        out_rgba8, out_mask, out_uv, out_steps, steps_total, stream);
 }
 
@@ -1645,8 +1725,19 @@ int geo_render_band_set_frames(geo_ctx* c, const geo_frame* frames, uint32_t nfr
                                unsigned long long* steps_total, void* stream) {
     if (!c || !frames || !scene || !out_rgba8 || nframes == 0 || nframes > kMaxBatchFrames ||
         !band_set_ok(width, height, band_rows, row0, row_stride, nbands))
-        return GEO_EINVAL;
-    return render_impl(c, frames, nframes, out_frame_stride, scene, width, height, row0, nbands * band_rows,
+        return invalid_call(c);
+    return render_impl(c, frames, nframes, out_frame_stride, scene, false, width, height, row0, nbands * band_rows,
+                       band_rows, row_stride, out_rgba8, nullptr, nullptr, nullptr, steps_total, stream);
+}
+
+int geo_render_band_set_batch(geo_ctx* c, const geo_frame* frames, const geo_scene* scenes, uint32_t nframes,
+                              uint32_t width, uint32_t height, uint32_t band_rows, uint32_t row0, uint32_t row_stride,
+                              uint32_t nbands, uint8_t* out_rgba8, size_t out_frame_stride,
+                              unsigned long long* steps_total, void* stream) {
+    if (!c || !frames || !scenes || !out_rgba8 || nframes == 0 || nframes > kMaxBatchFrames ||
+        !band_set_ok(width, height, band_rows, row0, row_stride, nbands))
+        return invalid_call(c);
+    return render_impl(c, frames, nframes, out_frame_stride, scenes, true, width, height, row0, nbands * band_rows,
                        band_rows, row_stride, out_rgba8, nullptr, nullptr, nullptr, steps_total, stream);
 }
 

@@ -166,6 +166,27 @@ class _RawEvent:
             self.h = None
 
 
+def _batch_key(scene) -> bytes:
+    """What the frames of one batched launch must share
+    (geo_render_band_set_batch): the scene bytes but the observer radius, and
+    the side of the horizon it is on (the integration kind); in fan mode the
+    radius too (one fan for the launch)."""
+    b = bytearray(bytes(scene))
+    if scene.mode != 1:
+        b[8:12] = b"\0\0\0\0"  # geo_scene.r_obs
+        b += b"o" if scene.r_obs > scene.rs else b"i"
+    return bytes(b)
+
+
+def _empty_timing(events, stream: int) -> None:
+    """A timed step of a rank with no rows renders nothing: record the
+    caller's pair back to back on the stream, so elapsed_time reads ~0
+    instead of failing on unrecorded events."""
+    if events is not None:
+        events[0].record(stream)
+        events[1].record(stream)
+
+
 class ShardedFrame:
     """Render-then-gather pipeline for one rank, K frames per gather.
 
@@ -227,8 +248,9 @@ class ShardedFrame:
         self.batch = bool(batch_launch) and self.K > 1
         if self.batch and self.K > GEO_MAX_BATCH_FRAMES:
             raise ValueError(f"batch_launch: at most {GEO_MAX_BATCH_FRAMES} frames per gather")
-        self.pending_frames = []     # batch mode: the open batch's uniforms not yet rendered,
-        self.pending_scene = None    # the scene their steps passed (None = the object's)
+        self.pending_frames = []     # batch mode: copies of the open batch's uniforms not yet rendered,
+        self.pending_scenes = []     # and copies of their scenes (they differ in r_obs at most)
+        self._pending_key = b""
         self.pending_first = 0       # and the slot of the first of them
         L = self.layout
         self.row_bytes = width * 4
@@ -291,12 +313,13 @@ class ShardedFrame:
         b, sub = (i // self.K) % 2, i % self.K
         return self.bufs[b][sub * self.slice:(sub + 1) * self.slice]
 
-    def render_local(self, buf, scene=None, **outs) -> None:
+    def render_local(self, buf, scene=None, frame=None, **outs) -> None:
         L = self.layout
         if L.nbands() == 0:  # a frame too small to give this rank a band
             return
-        self.ctx.render_band_set(self.frame, self.scene if scene is None else scene, self.width, self.height,
-                                 L.band_height(), L.row0(), L.cycle_rows, L.nbands(), buf, **outs)
+        self.ctx.render_band_set(self.frame if frame is None else frame, self.scene if scene is None else scene,
+                                 self.width, self.height, L.band_height(), L.row0(), L.cycle_rows, L.nbands(), buf,
+                                 **outs)
 
     def _assemble(self, b: int, src, n: int, stream=None) -> None:
         """Rank 0: frames of batch b from its own bands (bufs[b]) and the peers' gathered blocks."""
@@ -309,26 +332,33 @@ class ShardedFrame:
         k = (i // self.K) % 2 % self.S if self.batch else i % self.S
         return self.stream0 if k == 0 else self.extra[k - 1]
 
-    def render_batch(self, b: int, frames, scene=None, events=None, stream=None, first: int = 0) -> None:
+    def render_batch(self, b: int, frames, scene=None, events=None, stream=None, first: int = 0,
+                     scenes=None) -> None:
         """The frames of batch buffer b (slots first .. first + len(frames) - 1)
-        in one launch (geo_render_band_set_frames), on `stream` (a handle;
-        default the buffer's render stream)."""
-        import ctypes
-
-        from ._lib import GeoFrame, check
+        in one launch (geo_render_band_set_batch), on `stream` (a handle;
+        default the buffer's render stream).  scenes: one per frame (they may
+        differ in r_obs only); default `scene` (or the object's) for all."""
+        from ._lib import GeoFrame, GeoScene, check
 
         band_h, row0, cycle, nb = self._band
-        if not nb:
-            return
         sh = self._sh[b % self.S] if stream is None else stream
+        if not nb:
+            _empty_timing(events, sh)
+            return
         if events is not None:
-            self.lib.geo_time_next_render(self._ctx_h, events[0].h, events[1].h)
-        self._frame_arr = (GeoFrame * len(frames))(*frames)
-        st = self.lib.geo_render_band_set_frames(
-            self._ctx_h, self._frame_arr, len(frames), self._scene_ref if scene is None else ctypes.byref(scene),
-            self.width, self.height, band_h, row0, cycle, nb, self._lv[b][first], self.slice, None, sh)
+            st = self.lib.geo_time_next_render(self._ctx_h, events[0].h, events[1].h)
+            if st != 0:
+                check("geo_time_next_render", st)
+        n = len(frames)
+        if scenes is None:
+            scenes = [self.scene if scene is None else scene] * n
+        self._frame_arr = (GeoFrame * n)(*frames)
+        self._scene_arr = (GeoScene * n)(*scenes)
+        st = self.lib.geo_render_band_set_batch(
+            self._ctx_h, self._frame_arr, self._scene_arr, n, self.width, self.height, band_h, row0, cycle, nb,
+            self._lv[b][first], self.slice, None, sh)
         if st != 0:
-            check("geo_render_band_set_frames", st)
+            check("geo_render_band_set_batch", st)
 
     def _join(self) -> None:
         """The current stream waits for every render stream."""
@@ -344,7 +374,7 @@ class ShardedFrame:
         self.batches += 1
         rendered = [k for k in range(self.S) if self.rendered_in[b][k]]
         self.rendered_in[b] = [False] * self.S
-        if self.world == 1:
+        if self.world == 1 or self.dist is None:  # one rank, or one rank's share alone (no present)
             self.pending[b] = (None, n, self.batches, rendered)
             return
         torch = self.torch
@@ -396,32 +426,41 @@ class ShardedFrame:
     def _step_batch(self, b: int, sub: int, events, scene, frame) -> None:
         """Batch mode: record frame `sub` of the open batch; at its K-th frame
         render the batch in one launch, pack it (peers) and launch its gather.
-        A launch's frames share one scene (geo_render_band_set_frames): a step
-        whose scene differs from the pending frames' first renders those."""
-        if self.pending_frames and bytes(self.scene if scene is None else scene) != bytes(
-                self.scene if self.pending_scene is None else self.pending_scene):
+        A launch's frames may differ in the observer radius only
+        (geo_render_band_set_batch: a moving observer): a step whose scene
+        differs otherwise from the pending frames' renders those first.  The
+        uniform and the scene are copied when the step is recorded (the launch
+        reads them later): a caller may update its objects in place between
+        steps, as the per-frame path allows."""
+        from ._lib import GeoFrame, GeoScene
+
+        sc = GeoScene.from_buffer_copy(self.scene if scene is None else scene)
+        key = _batch_key(sc)
+        if self.pending_frames and key != self._pending_key:
             self._flush_batch(b)
         if not self.pending_frames:
             self.pending_first = sub
-        self.pending_frames.append(self.frame if frame is None else frame)
-        self.pending_scene = scene  # a partial batch flushed by drain() keeps the steps' scene
+            self._pending_key = key
+        self.pending_scenes.append(sc)
+        self.pending_frames.append(GeoFrame.from_buffer_copy(self.frame if frame is None else frame))
         self.rendered = sub + 1
         self.open = b
         if sub == self.K - 1:
-            self._flush_batch(b, events, scene)
+            self._flush_batch(b, events)
             self._launch(b, self.K)
             self.rendered = 0
 
-    def _flush_batch(self, b: int, events=None, scene=None) -> None:
+    def _flush_batch(self, b: int, events=None) -> None:
+        """Render the pending frames (their snapshots and their scenes') in one launch."""
         n, first = len(self.pending_frames), self.pending_first
         if not n:
             return
-        scene = self.pending_scene if scene is None else scene
         k = b % self.S
         sh = self._sh[k]
         self.ev_free[b].wait(sh)
-        self.render_batch(b, self.pending_frames, scene=scene, events=events, stream=sh, first=first)
+        self.render_batch(b, self.pending_frames, events=events, stream=sh, first=first, scenes=self.pending_scenes)
         self.pending_frames = []
+        self.pending_scenes = []
         if self.bpp == 3 and self.rank != 0:
             st = self.lib.geo_pack_rgb(self._ctx_h, self._lv[b][first], n * self.slice // 4, self._sv[b][first], sh)
             if st != 0:
@@ -451,9 +490,15 @@ class ShardedFrame:
             self.ev_free[b].wait(sh)  # first render of this stream into the batch buffer
         band_h, row0, cycle, nb = self._band
         lib = self.lib
-        if events is not None:
+        if not nb:
+            _empty_timing(events, sh)  # a rank with no rows: a zero-length pair
+        elif events is not None:
             # the render's kernel dispatch carries the pair (no marker packets)
-            lib.geo_time_next_render(self._ctx_h, events[0].h, events[1].h)
+            st = lib.geo_time_next_render(self._ctx_h, events[0].h, events[1].h)
+            if st != 0:
+                from ._lib import check
+
+                check("geo_time_next_render", st)
         if nb:
             st = lib.geo_render_band_set(
                 self._ctx_h, self._frame_ref if frame is None else ctypes.byref(frame),

@@ -83,3 +83,49 @@ def test_rank0_lead_specs_and_trials():
             owned = sorted(x for lay in L for x in lay.local_to_frame_rows() if x >= 0)
             assert owned == list(range(2160)), (n, a, b)
             assert all(lay.band_height() % 8 == 0 for lay in L)  # a wave's rows lie in one band
+
+
+def test_share_spec_and_motion_frames():
+    """--share r/n and --motion: the per-frame uniforms of a moving observer
+    follow the reference's Observer (the scene's radius is the observer's)."""
+    import argparse
+
+    import schwarzschild_raytracer_wgpu_amd as g
+    from schwarzschild_raytracer_wgpu_amd.scenes import CONFIGS
+
+    assert bench._share_spec("1/8") == (1, 8)
+    for bad in ("8/8", "1/1", "x/8", "1"):
+        with pytest.raises(argparse.ArgumentTypeError):
+            bench._share_spec(bad)
+    cfg = CONFIGS["cfg3_4k"]
+    for kind in ("orbit", "fall", "pan"):
+        mv = bench.motion_frames(g, cfg, kind, 30, g.GEO_MODE_DIRECT, 0, 0.0)
+        assert len(mv) == 30
+        frames = {bytes(f) for f, _ in mv}
+        assert len(frames) == 30, kind  # every frame its own uniform
+        radii = [sc.r_obs for _, sc in mv]
+        if kind == "pan":
+            assert len(set(radii)) == 1
+        else:
+            assert len(set(radii)) == 30 and all(r > cfg.rs for r in radii)
+        for fr, sc in mv:  # the uniform's position is the scene's radius
+            x, y, z = fr.psi_factor_and_position[1:]
+            assert abs((x * x + y * y + z * z) ** 0.5 - sc.r_obs) < 1e-5
+    fall = [sc.r_obs for _, sc in bench.motion_frames(g, cfg, "fall", 60, g.GEO_MODE_DIRECT, 0, 0.0)]
+    assert all(b < a for a, b in zip(fall, fall[1:]))  # falling in
+
+
+def test_batch_key_groups_a_moving_observer():
+    """dist._batch_key: frames that differ in the radius only share a batched
+    launch (on one side of the horizon; fan mode: one fan, one radius)."""
+    import schwarzschild_raytracer_wgpu_amd as g
+    from schwarzschild_raytracer_wgpu_amd.dist import _batch_key
+
+    def sc(r, budget=512, mode=g.GEO_MODE_DIRECT):
+        return g.make_scene(1.0, 50.0, r, 0.0314, budget, mode)
+
+    assert _batch_key(sc(2.5)) == _batch_key(sc(2.4))
+    assert _batch_key(sc(2.5)) != _batch_key(sc(2.5, budget=256))
+    assert _batch_key(sc(2.5)) != _batch_key(sc(0.9))       # across the horizon: another integration
+    assert _batch_key(sc(0.8)) == _batch_key(sc(0.9))
+    assert _batch_key(sc(2.5, mode=g.GEO_MODE_FAN)) != _batch_key(sc(2.4, mode=g.GEO_MODE_FAN))

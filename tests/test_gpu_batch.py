@@ -110,3 +110,93 @@ def test_batch_rejects_what_it_does_not_draw(geo, torch_mod):
     assert call(plain, fb + 2) == _lib.GEO_EINVAL
     torch_mod.cuda.synchronize()
     ctx.close()
+
+
+def _moving(geo, w, h, n, kind):
+    """n uniforms and scenes of a moving observer (the reference's present
+    loop: Observer::update_position then calc_transformation_pipeline per
+    frame, observer.rs:105-125, renderer.rs:208-264): 'orbit' =
+    start_orbit(1.8) from (2.5, 0, 0.1), 'fall' = start_orbit(0) (the Fall
+    button, lib.rs:180), dt = 1/20 s per frame (large steps: the radius moves
+    visibly within a batch)."""
+    obs = geo.Observer(1.0, math.pi / 2, w, h)
+    obs.set_position(2.5, 0.0, 0.1)
+    assert obs.start_orbit(1.8 if kind == "orbit" else 0.0)
+    frames, scenes = [], []
+    for _ in range(n):
+        obs.update_position((0.0, 0.0, 0.0), 0.05)
+        frames.append(obs.calc_transformation_pipeline())
+        scenes.append(geo.make_scene(1.0, 50.0, obs.get_radial_position(), math.pi / 100, 1024, geo.GEO_MODE_DIRECT))
+    return frames, scenes
+
+
+@pytest.mark.parametrize("kind", ["orbit", "fall"])
+@pytest.mark.parametrize("mode_name", ["direct", "adaptive"])
+def test_batch_of_a_moving_observer(geo, torch_mod, kind, mode_name):
+    """geo_render_band_set_batch: frames whose scenes differ in r_obs (each
+    frame's own radius) in one launch == each frame rendered alone with its
+    own scene, bytes and step totals."""
+    from schwarzschild_raytracer_wgpu_amd import _lib
+    from schwarzschild_raytracer_wgpu_amd.scenes import make_sky
+
+    w, h, band_rows, row0, row_stride = 160, 96, 8, 8, 24
+    dev = torch_mod.device("cuda:0")
+    ctx = geo.Context(0)
+    ctx.set_sky(make_sky("equirect", (256, 128)))
+    n = _lib.GEO_MAX_BATCH_FRAMES
+    frames, scenes = _moving(geo, w, h, n, kind)
+    if mode_name == "adaptive":
+        scenes = [geo.make_scene(s.rs, s.sphere_r, s.r_obs, s.step, s.max_steps, geo.GEO_MODE_ADAPTIVE)
+                  for s in scenes]
+    assert len({s.r_obs for s in scenes}) == n  # every frame its own radius
+    nbands = (h - row0 + row_stride - 1) // row_stride
+    packed = nbands * band_rows * w * 4
+    out = torch_mod.full((n * packed,), 7, dtype=torch_mod.uint8, device=dev)
+    tot = torch_mod.zeros(1, dtype=torch_mod.int64, device=dev)
+    fa, sa = (geo.GeoFrame * n)(*frames), (geo.GeoScene * n)(*scenes)
+    _lib.check("geo_render_band_set_batch", _lib.lib.geo_render_band_set_batch(
+        ctx._h, fa, sa, n, w, h, band_rows, row0, row_stride, nbands, out.data_ptr(), packed, tot.data_ptr(),
+        torch_mod.cuda.current_stream().cuda_stream))
+    ref_tot = torch_mod.zeros(1, dtype=torch_mod.int64, device=dev)
+    for f in range(n):
+        ref = torch_mod.full((packed,), 7, dtype=torch_mod.uint8, device=dev)
+        ctx.render_band_set(frames[f], scenes[f], w, h, band_rows, row0, row_stride, nbands, ref, steps_total=ref_tot)
+        assert torch_mod.equal(out[f * packed:(f + 1) * packed], ref), (kind, f)
+    torch_mod.cuda.synchronize()
+    assert int(tot.item()) == int(ref_tot.item()) > 0
+    ctx.close()
+
+
+def test_batch_scenes_must_agree_but_for_the_radius(geo, torch_mod):
+    import ctypes
+
+    from schwarzschild_raytracer_wgpu_amd import _lib
+    from schwarzschild_raytracer_wgpu_amd.scenes import make_sky
+
+    dev = torch_mod.device("cuda:0")
+    ctx = geo.Context(0)
+    ctx.set_sky(make_sky("equirect", (64, 32)))
+    frames, r = _frames(geo, 64, 32, 2)
+    fa = (geo.GeoFrame * 2)(*frames)
+    out = torch_mod.empty(2 * 64 * 32 * 4, dtype=torch_mod.uint8, device=dev)
+
+    def call(s0, s1):
+        sa = (geo.GeoScene * 2)(s0, s1)
+        return _lib.lib.geo_render_band_set_batch(ctx._h, fa, sa, 2, 64, 32, 8, 0, 8, 4, out.data_ptr(),
+                                                  64 * 32 * 4, None, torch_mod.cuda.current_stream().cuda_stream)
+
+    def sc(r_obs=r, budget=64, mode=geo.GEO_MODE_DIRECT, step=math.pi / 100):
+        return geo.make_scene(1.0, 50.0, r_obs, step, budget, mode)
+
+    assert call(sc(), sc(r * 1.01)) == _lib.GEO_OK
+    assert call(sc(), sc(budget=65)) == _lib.GEO_EINVAL             # another budget
+    assert call(sc(), sc(step=math.pi / 99)) == _lib.GEO_EINVAL     # another step
+    assert call(sc(), sc(mode=geo.GEO_MODE_ADAPTIVE)) == _lib.GEO_EINVAL
+    assert call(sc(), sc(r_obs=0.9)) == _lib.GEO_EINVAL             # inside the horizon: another kind
+    assert call(sc(), sc(r_obs=-1.0)) == _lib.GEO_EINVAL
+    assert call(sc(r_obs=0.8), sc(r_obs=0.9)) == _lib.GEO_OK        # both inside
+    ctx.solve_ray_fan(50.0, 1.0, 1000, math.pi / 100, 400, r, host=False)
+    assert call(sc(mode=geo.GEO_MODE_FAN), sc(mode=geo.GEO_MODE_FAN)) == _lib.GEO_OK
+    assert call(sc(mode=geo.GEO_MODE_FAN), sc(r * 1.01, mode=geo.GEO_MODE_FAN)) == _lib.GEO_EINVAL  # one fan
+    torch_mod.cuda.synchronize()
+    ctx.close()

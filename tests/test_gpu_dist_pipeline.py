@@ -219,10 +219,12 @@ def test_assemble_lead_matches_host_assembly(W, H, B, world, lead, bpp, nframes)
 
 @pytest.mark.parametrize("S", [1, 2])
 def test_batch_splits_on_scene_change(S):
-    """Batch mode, a peer rank: a launch's frames share one scene, so a step
-    whose scene differs from the pending frames' renders those first (into
-    their slots), and the batch's gather still sends all K frames; every sent
-    frame equals that frame's own render with its own scene."""
+    """Batch mode, a peer rank: a launch's frames may differ in the observer
+    radius (one geo_render_band_set_batch launch), but a step whose scene
+    differs otherwise (here the step budget) renders the pending frames
+    first (into their slots), and the batch's gather still sends all K
+    frames; every sent frame equals that frame's own render with its own
+    scene."""
     import torch
 
     if not torch.cuda.is_available():
@@ -251,13 +253,14 @@ def test_batch_splits_on_scene_change(S):
     ctx = g.Context(0)
     ctx.set_sky(make_sky("equirect", (128, 64)))
     poses = []
-    for r in (2.5, 3.4):
+    for r, budget in ((2.5, 256), (3.4, 256), (2.9, 200)):
         obs = g.Observer(1.0, math.pi / 2, W, H)
         obs.set_position(r, 0.0, 0.1)
         rr = obs.get_radial_position()
         poses.append((obs.calc_transformation_pipeline(),
-                      g.make_scene(1.0, 50.0, rr, math.pi / 100, 256, g.GEO_MODE_DIRECT)))
-    which = [0, 0, 1, 0, 1, 1, 1, 1, 0, 0]  # scene changes inside batches 0 and 2, none in batch 1
+                      g.make_scene(1.0, 50.0, rr, math.pi / 100, budget, g.GEO_MODE_DIRECT)))
+    # radius changes inside every batch; budget changes inside batches 0 and 2 (splits), none in batch 1
+    which = [0, 2, 1, 0, 1, 0, 1, 1, 0, 2]
     pg = PeerGather()
     sf = ShardedFrame(ctx, poses[0][0], poses[0][1], W, H, B, rank, world, dev, dist=pg, frames_per_gather=K,
                       render_streams=S, batch_launch=True)
@@ -269,6 +272,7 @@ def test_batch_splits_on_scene_change(S):
     assert len(pg.sent) == 3 and sf.frames_done == len(which)
     L = sf.layout
     ref = []
+    assert len({bytes(p[1]) for p in poses}) == 3
     for frame, scene in poses:
         one = torch.zeros(sf.slice, dtype=torch.uint8, device=dev)
         ctx.render_band_set(frame, scene, W, H, L.band_height(), L.row0(), L.cycle_rows, L.nbands(), one)
@@ -276,8 +280,103 @@ def test_batch_splits_on_scene_change(S):
         ctx.pack_rgb(one, sf.slice // 4, packed)
         ref.append(packed)
     torch.cuda.synchronize()
-    assert not torch.equal(ref[0], ref[1])
+    assert not torch.equal(ref[0], ref[1]) and not torch.equal(ref[0], ref[2])
     for i, p in enumerate(which):
         batch = pg.sent[i // K]
         got = batch[(i % K) * sf.tslice:(i % K + 1) * sf.tslice]
         assert torch.equal(got, ref[p]), i
+
+
+@pytest.mark.parametrize("S", [1, 2])
+def test_batch_snapshots_uniforms_mutated_in_place(S):
+    """Batch mode reads a batch's uniforms when it launches, K steps after
+    the first was recorded: ShardedFrame must copy them at each step.  One
+    GeoFrame object and one GeoScene object are updated in place before every
+    step (the pose alternates; the scene's step budget changes once, inside a
+    batch); every frame sent equals that step's own render."""
+    import ctypes
+
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    import schwarzschild_raytracer_wgpu_amd as g
+    from schwarzschild_raytracer_wgpu_amd.dist import ShardedFrame
+    from schwarzschild_raytracer_wgpu_amd.scenes import make_sky
+
+    class PeerGather:
+        def __init__(self):
+            self.stream = torch.cuda.Stream()
+            self.sent = []
+
+        def gather(self, src, gather_list=None, dst=0, async_op=True):
+            ready = torch.cuda.Event()
+            ready.record(torch.cuda.current_stream())
+            with torch.cuda.stream(self.stream):
+                self.stream.wait_event(ready)
+                self.sent.append(src.clone())
+                done = torch.cuda.Event()
+                done.record(self.stream)
+            return _Work(torch, done)
+
+    W, H, B, world, rank, K = 256, 144, 8, 2, 1, 4
+    dev = torch.device("cuda:0")
+    ctx = g.Context(0)
+    ctx.set_sky(make_sky("equirect", (128, 64)))
+    poses = [default_frame(W, H, pos=p) for p in ((2.5, 0.0, 0.1), (3.4, 0.2, 0.0))]
+    scenes = [default_scene(256), default_scene(200)]
+    fr = g.GeoFrame.from_buffer_copy(poses[0])
+    sc = g.GeoScene.from_buffer_copy(scenes[0])
+    plan = [(0, 0), (1, 0), (0, 0), (1, 0), (1, 0), (0, 1), (1, 1), (0, 1), (1, 1), (0, 0)]
+    pg = PeerGather()
+    sf = ShardedFrame(ctx, fr, sc, W, H, B, rank, world, dev, dist=pg, frames_per_gather=K, render_streams=S,
+                      batch_launch=True)
+    assert sf.batch
+    for i, (p, s) in enumerate(plan):
+        ctypes.memmove(ctypes.addressof(fr), ctypes.addressof(poses[p]), ctypes.sizeof(fr))
+        ctypes.memmove(ctypes.addressof(sc), ctypes.addressof(scenes[s]), ctypes.sizeof(sc))
+        sf.step(i, frame=fr if i % 2 else None, scene=sc if i % 3 else None)  # explicit and the object's own
+    sf.drain()
+    torch.cuda.synchronize()
+    assert len(pg.sent) == 3 and sf.frames_done == len(plan)
+    L = sf.layout
+    for i, (p, s) in enumerate(plan):
+        one = torch.zeros(sf.slice, dtype=torch.uint8, device=dev)
+        ctx.render_band_set(poses[p], scenes[s], W, H, L.band_height(), L.row0(), L.cycle_rows, L.nbands(), one)
+        ref = torch.empty(sf.tslice, dtype=torch.uint8, device=dev)
+        ctx.pack_rgb(one, sf.slice // 4, ref)
+        torch.cuda.synchronize()
+        got = pg.sent[i // K][(i % K) * sf.tslice:(i % K + 1) * sf.tslice]
+        assert torch.equal(got, ref), i
+
+
+def test_timed_step_of_a_rank_without_rows():
+    """A rank whose share of a tiny frame is empty still records the caller's
+    timing pair (zero length), per frame and batched."""
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    import schwarzschild_raytracer_wgpu_amd as g
+    from schwarzschild_raytracer_wgpu_amd.dist import ShardedFrame
+    from schwarzschild_raytracer_wgpu_amd.scenes import make_sky
+    from schwarzschild_raytracer_wgpu_amd.timing import HipEvent
+
+    class Sink:
+        def gather(self, src, gather_list=None, dst=0, async_op=True):
+            return _Work(torch, torch.cuda.Event())
+
+    W, H = 64, 16  # two 8-row bands: ranks 2 and 3 of 4 own none
+    dev = torch.device("cuda:0")
+    ctx = g.Context(0)
+    ctx.set_sky(make_sky("equirect", (128, 64)))
+    for batch in (False, True):
+        sf = ShardedFrame(ctx, default_frame(W, H), default_scene(64), W, H, 8, 3, 4, dev, dist=Sink(),
+                          frames_per_gather=2, batch_launch=batch)
+        assert sf.layout.nbands() == 0
+        ev = (HipEvent(), HipEvent())
+        sf.step(0)
+        sf.step(1, events=ev)
+        sf.drain()
+        torch.cuda.synchronize()
+        assert 0.0 <= ev[0].elapsed_time(ev[1]) < 1.0

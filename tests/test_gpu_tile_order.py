@@ -145,3 +145,56 @@ def test_time_next_render(dev):
     assert torch.equal(out, ref) and 0.0 < ms < 50.0
     ctx.set_sky(make_sky("equirect", (128, 64)))  # waits on the context's event: must not hang
     ctx.close()
+
+
+@pytest.mark.parametrize("period", [1, 3, 16])
+def test_learning_period_counts(dev, period):
+    """GEO_DISPATCH_LONGEST_FIRST records every period-th render of a grid
+    (renders 1, period + 1, ...) and the next render adopts the order built
+    from it; with a sync after each render every rebuild completes in time."""
+    w, h = 200, 117
+    frame = default_frame(w, h)
+    scene = default_scene(256)
+    ctx = Context(0)
+    ctx.set_sky(make_sky("equirect", (256, 128)))
+    ctx.set_dispatch(GEO_DISPATCH_LONGEST_FIRST, period)
+    rec0, ad0 = ctx.dispatch_stats()
+    n = 2 * period + 2
+    out = torch.zeros(h * w * 4, dtype=torch.uint8, device=dev)
+    for _ in range(n):
+        ctx.render_rows(frame, scene, w, h, 0, h, out)
+        torch.cuda.synchronize()
+    rec, ad = ctx.dispatch_stats()
+    assert rec - rec0 == len([i for i in range(n) if i % period == 0])
+    assert ad - ad0 == len([i for i in range(n - 1) if i % period == 0])
+    ctx.close()
+
+
+def test_refused_render_drops_the_timing_pair(dev):
+    """geo_time_next_render's pair belongs to the next render call: a call
+    refused before launching records neither event, and the render after it
+    does not record them either."""
+    from schwarzschild_raytracer_wgpu_amd import _lib
+    from schwarzschild_raytracer_wgpu_amd.timing import HipEvent
+
+    w, h = 64, 32
+    frame = default_frame(w, h)
+    scene = default_scene(256)
+    ctx = Context(0)
+    ctx.set_sky(make_sky("equirect", (128, 64)))
+    out = torch.zeros(h * w * 4, dtype=torch.uint8, device=dev)
+    a, b = HipEvent(), HipEvent()
+    for bad in ("args", "state"):
+        ctx.time_next_render(a, b)
+        if bad == "args":  # rows past the frame: refused by the entry point
+            st = _lib.lib.geo_render_rows(ctx._h, frame, scene, w, h, h - 1, 2, out.data_ptr(), None, None, None,
+                                          None, None)
+        else:  # fan mode without a fan: refused inside
+            fs = make_scene(1.0, 50.0, scene.r_obs, scene.step, 256, GEO_MODE_FAN)
+            st = _lib.lib.geo_render_rows(ctx._h, frame, fs, w, h, 0, h, out.data_ptr(), None, None, None, None, None)
+        assert st < 0
+        ctx.render_rows(frame, scene, w, h, 0, h, out)
+        torch.cuda.synchronize()
+        with pytest.raises(RuntimeError):
+            a.elapsed_time(b)  # never recorded
+    ctx.close()

@@ -86,23 +86,38 @@ EOF
       tr=$(find "$OUT/prof_$name" -name 'run_kernel_trace.csv' | head -n 1)
       st=$(find "$OUT/prof_$name" -name 'run_kernel_stats.csv' | head -n 1)
       cp "$st" "$OUT/${name}_kernel_stats.csv"
-      python3 tools/trace_window.py "$tr" --bench "$OUT/${name}_bench.json" > "$OUT/${name}_trace_window.txt"
+      python3 tools/trace_window.py "$tr" --bench "$OUT/${name}_bench.json" --json "$OUT/${name}_trace_window.json" > "$OUT/${name}_trace_window.txt"
       rc=$?; cat "$OUT/${name}_trace_window.txt"; [ $rc -eq 0 ] || exit $rc
       rm -rf "$OUT/prof_$name" ;;
     pmc)
       cfg=${a1:-cfg3_4k}; mode=${a2:-}
       name=${cfg}${mode:+_$mode}
-      SETS=("GRBM_GUI_ACTIVE SQ_INSTS_SALU SQ_INSTS_VALU SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES"
-            "SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_MUL_F32"
-            "SQ_THREAD_CYCLES_VALU SQ_INSTS_VALU_FLOPS_FP32 SQ_ACTIVE_INST_VALU" "FETCH_SIZE" "WRITE_SIZE")
+      # the round-4 sets (tools/gpu_pmc.sh limits: <= 8 SQ, 4 TCC, 2 GRBM per pass)
+      SETS=("GRBM_GUI_ACTIVE SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_VALU"
+            "SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_FMA_F32 SQ_THREAD_CYCLES_VALU SQ_INSTS_VALU_FLOPS_FP32"
+            "FETCH_SIZE" "WRITE_SIZE" "TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum"
+            "GRBM_GUI_ACTIVE SQ_BUSY_CU_CYCLES MeanOccupancyPerCU")
       EXTRA_ARGS=${mode:+--mode $mode} CONFIG=$cfg bash tools/gpu_pmc.sh "$TAG/pmc_$name" "${SETS[@]}" || exit $?
       python3 tools/pmc_to_profile.py "$TAG/pmc_$name" "$OUT/${name}_pmc.json" "$name" > /dev/null || exit $? ;;
     motion)
-      kind2=${a1:-orbit}
-      for disp in learned natural; do
-        timeout -k 10 300 python3 bench.py --motion "$kind2" --dispatch $disp --steps 200 --warmup 20 \
-          --no-cpu-baseline > "$OUT/motion_${kind2}_$disp.json" 2> "$OUT/motion_${kind2}_$disp.err"
-        rc=$?; [ $rc -eq 0 ] || { tail -5 "$OUT/motion_${kind2}_$disp.err"; exit $rc; }
+      # learned vs natural dispatch order on moving frames: N = 1 (one launch
+      # per frame) and one 8-rank share alone in batched launches of 8 frames
+      # (K distinct uniforms share one learned order); 3 interleaved reps
+      : > "$OUT/motion_runs.txt"
+      for rep in 1 2 3; do
+        for shr in none 1/8; do
+          for mot in none orbit fall; do
+            for disp in learned natural; do
+              sargs=""; [ $shr != none ] && sargs="--share $shr --frames-per-gather 8 --batch-launch on"
+              f="$OUT/motion_${mot}_${disp}_${shr/\//of}_$rep.json"
+              timeout -k 10 200 python3 bench.py --motion $mot --dispatch $disp --steps 200 --warmup 20 \
+                --no-cpu-baseline $sargs > "$f" 2> "$f.err"
+              rc=$?; [ $rc -eq 0 ] || { tail -5 "$f.err"; exit $rc; }
+              echo "$rep $shr $mot $disp $(python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().splitlines()[-1]); print(d['ms_per_step'], d['kernel_ms']['avg'], d['value'])" "$f")" \
+                | tee -a "$OUT/motion_runs.txt"
+            done
+          done
+        done
       done ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac

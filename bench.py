@@ -409,9 +409,11 @@ def main():
                                          flags=g._lib.GEO_FLAG_DEFER_STEPS | sampler_flags, tol=tol))
                   for fr, sc in mv]
 
-    def pose(i):
-        """(uniform, scene) of warmup/timed frame i (i counts from the first warmup frame)."""
-        return (None, None) if moving is None else (moving[i][0], moving[i][2])
+    def pose(i, defer=True):
+        """(uniform, scene) of warmup/timed frame i (i counts from the first
+        warmup frame); the scene with GEO_FLAG_DEFER_STEPS (the timed region
+        counts its steps in the context) or without (the warmup)."""
+        return (None, None) if moving is None else (moving[i][0], moving[i][2 if defer else 1])
 
     # untimed diagnostic pass: per-pixel steps + mask give the RK4 evaluations
     # per launch (main-loop steps + 3 Newton evaluations per sphere crossing);
@@ -460,7 +462,7 @@ def main():
     steps_timed = sum(st_ for st_, _ in per_frame)  # what the timed region must count
     # per-launch figures: the average timed frame (one pose: the diagnostic frame's)
     evals_per_launch = round(sum(st_ + NEWTON_EVALS * h_ for st_, h_ in per_frame) / args.steps)
-    flops_per_launch = sum(frame_flops) / args.steps
+    flops_per_launch = flops_mean = sum(frame_flops) / args.steps
 
     # timed region: K frames; steps counted in the context (GEO_FLAG_DEFER_STEPS)
     # and flushed once at the end; fence-free event pairs on every k-th frame
@@ -486,7 +488,7 @@ def main():
     spin = args.spinup_frames * world
     spin_up(sf, spin)
     for i in range(args.warmup):
-        fr, sc = pose(i)
+        fr, sc = pose(i, defer=False)
         sf.step(i, frame=fr, scene=sc)
     sf.drain()
     torch.cuda.synchronize()
@@ -658,7 +660,7 @@ def main():
     # frame of the compute-only pass's wall time (no events; launch gaps
     # included)
     achieved_tflops = flops_per_launch / (kernel_ms_avg * 1e-3) / 1e12
-    wall_tflops = flops_per_launch / (compute_max / args.steps) / 1e12
+    wall_tflops = flops_mean / (compute_max / args.steps) / 1e12
     pmc_file, pmc = pmc_profile(args.config, args.mode, world) if not args.mips else (None, {})
     if mode == g.GEO_MODE_FAN:
         metric = (f"pixels/sec at {W}x{H}, fan-mode draw (the reference's display path: 400-node fan lerp, "
@@ -673,12 +675,12 @@ def main():
                    f"{cfg.max_steps} max attempts"
     else:
         metric = f"geodesic-steps·pixels/sec at {W}x{H}, {cfg.max_steps} max steps (whole job; /GPU = value/n_gpus)"
+        unit = "geodesic-steps·pixels/s"
+        stepping = f"step pi/100, {cfg.max_steps} max RK4 steps"
     if args.motion != "none":
         metric += f" [moving observer: {args.motion}]"
     if args.share:
         metric += f" [rank {lay_rank}'s share of {lay_world}, alone]"
-        unit = "geodesic-steps·pixels/s"
-        stepping = f"step pi/100, {cfg.max_steps} max RK4 steps"
     out = {
         "metric": metric,
         "value": value,

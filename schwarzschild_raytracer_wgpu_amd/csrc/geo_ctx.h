@@ -102,11 +102,16 @@ struct geo_ctx {
     hipEvent_t time_start, time_stop;
 };
 
-// Makes `dev` current for the scope of a C-ABI call, restoring the caller's device.
+// Makes `dev` current for the scope of a C-ABI call, restoring the caller's
+// device.  It also clears the thread's last-error state first: the call's
+// launches are checked with hipGetLastError, which would otherwise report an
+// error left by an unrelated earlier HIP call of the caller (e.g. an elapsed
+// time asked of an unrecorded event) as this call's failure.
 struct DeviceGuard {
     int prev = -1;
     bool ok = false;
     explicit DeviceGuard(int dev) {
+        (void)hipGetLastError();
         if (hipGetDevice(&prev) != hipSuccess) prev = -1;
         ok = hipSetDevice(dev) == hipSuccess;
     }

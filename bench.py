@@ -760,6 +760,7 @@ def main():
             "pmc_profile": pmc_file,
         },
     }
+    out["roofline"]["trace_check"] = trace_profile(out["config"]["workload"], world) if not args.share else None
     if mode == g.GEO_MODE_FAN:
         out["roofline"] = fan_roofline(sky_touch, rows_mine * W, kernel_ms_avg, compute_max / args.steps * 1e3, pmc,
                                        pmc_file, mode)
@@ -903,6 +904,30 @@ def pmc_profile(config, mode, world):
         if d.get("workload", "").startswith(config) and d["workload"].endswith(f", {mode})"):
             return os.path.basename(path), d["derived"]
     return None, {}
+
+
+def trace_profile(workload: str, world: int):
+    """The committed same-invocation capture of this workload
+    (profiles/*_trace_window.json, tools/evidence.sh bench step: the bench
+    line and a rocprofv3 kernel trace of the SAME run, tools/trace_window.py):
+    the profiler's timed-window launch average and the frac it gives beside
+    the line's event-timed one, or None.  N = 1 only (a full-frame launch)."""
+    import glob
+
+    if world != 1:
+        return None
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_trace_window.json")), reverse=True):
+        with open(path) as f:
+            d = json.load(f)
+        if d.get("workload") == workload and d.get("n_gpus") == 1:
+            return {"profile": os.path.basename(path), "window_avg_ms": d["window_avg_ms"],
+                    "events_avg_ms": d["line_kernel_ms_avg"], "frac_events": d["line_frac"],
+                    "frac_trace": d["trace_frac"], "trace_over_events": d["trace_over_line"],
+                    "what": "one earlier run of this workload under rocprofv3 --kernel-trace: its timed window's "
+                            "average launch (profiler timestamps) against the same run's event pairs; the event "
+                            "pair on a dispatch reads a few us longer than the profiler's kernel span, and a "
+                            "box reads +-3 % from another (DESIGN.md §4, measurement)"}
+    return None
 
 
 def reference_fan_cost(ctx, cfg, r):

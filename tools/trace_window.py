@@ -50,7 +50,7 @@ def main():
         a.spinup, a.warmup, a.steps = line["spinup_frames"], line["warmup"], line["steps"]
         mode = line["roofline"]["kernel"].split("<", 1)[1].split(">", 1)[0].split(",")[0].strip()
         names = collections.Counter(r["Kernel_Name"] for r in rows
-                                    if r["Kernel_Name"].startswith(f"geo_render_kernel<{mode},"))
+                                    if f"geo_render_kernel<{mode}," in r["Kernel_Name"])
         if not names:
             raise SystemExit(f"no geo_render_kernel<{mode}, ...> launches in {a.trace}")
         a.kernel = names.most_common(1)[0][0]
@@ -79,7 +79,8 @@ def main():
            "all_launches_avg_ms": statistics.fmean(dur),
            "line_kernel_ms_avg": line["kernel_ms"]["avg"], "line_frac": rf["frac"], "trace_frac": frac_trace,
            "trace_over_line": frac_trace / rf["frac"], "work_per_launch": work, "unit": rf["unit"],
-           "peak": rf["peak"], "line_value": line["value"]}
+           "peak": rf["peak"], "line_value": line["value"], "workload": line["config"]["workload"],
+           "n_gpus": line["n_gpus"], "source": a.trace.split("gpurun_out/")[-1]}
     print(f"roofline: line frac {rf['frac']:.4f} (events avg {line['kernel_ms']['avg']:.4f} ms), trace frac "
           f"{frac_trace:.4f} (window avg {win_ms:.4f} ms): trace/line {frac_trace / rf['frac']:.4f}")
     if a.json:

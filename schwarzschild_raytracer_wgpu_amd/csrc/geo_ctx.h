@@ -100,6 +100,9 @@ struct geo_ctx {
     unsigned long long costs_recorded, orders_adopted;  // geo_dispatch_stats
     // geo_time_next_render: events for the next render's kernel dispatch
     hipEvent_t time_start, time_stop;
+#if defined(GEO_WAVE_LOG)
+    unsigned long long* wave_log;  // diagnostic build only (geo_debug_set_wave_log)
+#endif
 };
 
 // Makes `dev` current for the scope of a C-ABI call, restoring the caller's

@@ -123,6 +123,12 @@ struct RenderArgs {
     uint32_t* out_steps;
     unsigned long long* step_slots;
     uint64_t out_frame_px;  // batched launch: pixels from one frame's output to the next (colour only)
+#if defined(GEO_WAVE_LOG)
+    // diagnostic build only (tools/wave_timeline.py): per wave, in launch
+    // order, {start, end} (s_memrealtime, 100 MHz), {HW_ID, XCC_ID}, {tile,
+    // the wave's largest step count}
+    unsigned long long* wave_log;
+#endif
 };
 
 // MODE: GEO_MODE_DIRECT / GEO_MODE_FAN / GEO_MODE_ADAPTIVE; KIND: geo::kCurvedOut/kCurvedIn/kFlat
@@ -392,6 +398,9 @@ __device__ __forceinline__ void fan_tile(const RenderArgs& a, const FrameK& f, s
 // frame in blockIdx.z and its output a.out_frame_px pixels after the last's).
 template <int MODE, int KIND, bool MIPS, uint32_t NF>
 __global__ __launch_bounds__(kBlock) void geo_render_kernel(const RenderArgs a, const FrameBatch<NF> fb) {
+#if defined(GEO_WAVE_LOG)
+    const unsigned long long t_wave0 = __builtin_amdgcn_s_memrealtime();
+#endif
     constexpr uint32_t LR = lane_rows(MODE, MIPS);
     const uint32_t z = NF > 1 ? blockIdx.z : 0u;
     const FrameK& f = fb.f[z];
@@ -475,6 +484,22 @@ __global__ __launch_bounds__(kBlock) void geo_render_kernel(const RenderArgs a, 
                 atomicAdd(&a.tile_cost[tile.y * gridDim.x + tile.x], wmax + a.cost_overhead);
         }
     }
+#if defined(GEO_WAVE_LOG)
+    if (a.wave_log) {
+        const uint32_t wmax = wave_max_u32(steps);
+        const unsigned long long t_wave1 = __builtin_amdgcn_s_memrealtime();
+        if ((threadIdx.x & 63) == 0) {
+            const size_t wg = ((size_t)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+            unsigned long long* p = a.wave_log + (wg * (kBlock / 64) + wave) * 4;
+            const uint32_t hw_id = __builtin_amdgcn_s_getreg((31 << 11) | 4);  // HW_REG_HW_ID
+            const uint32_t xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20);    // HW_REG_XCC_ID[3:0]
+            p[0] = t_wave0;
+            p[1] = t_wave1;
+            p[2] = hw_id | ((unsigned long long)xcc << 32);
+            p[3] = (tile.x | (tile.y << 16)) | ((unsigned long long)wmax << 32);
+        }
+    }
+#endif
 }
 
 // ---- longest-first dispatch: the order from recorded tile costs ---------
@@ -1321,6 +1346,9 @@ static int render_impl(geo_ctx* c, const geo_frame* frames, uint32_t nframes, si
         if (geo::geodesic_kind(pk[i]) != geo::geodesic_kind(pk[0])) return GEO_EINVAL;
     }
     a.out_frame_px = out_frame_stride / 4u;
+#if defined(GEO_WAVE_LOG)
+    a.wave_log = c->wave_log;
+#endif
     a.k = pk[0];
     a.width = width;
     a.height = height;
@@ -1621,6 +1649,16 @@ int geo_set_dispatch(geo_ctx* c, int mode, uint32_t period) {
     c->rebuild_keep = false;
     return GEO_OK;
 }
+
+#if defined(GEO_WAVE_LOG)
+// Diagnostic build only: renders log every wave's span into `log` (4 u64 per
+// wave of the launch's grid, device memory; NULL stops logging).
+int geo_debug_set_wave_log(geo_ctx* c, void* log) {
+    if (!c) return GEO_EINVAL;
+    c->wave_log = (unsigned long long*)log;
+    return GEO_OK;
+}
+#endif
 
 int geo_dispatch_stats(geo_ctx* c, unsigned long long* costs_recorded, unsigned long long* orders_adopted) {
     if (!c) return GEO_EINVAL;

@@ -18,7 +18,8 @@
 #                    SAME invocation (tools/trace_window.py)
 #   plain:<cfg>[:<mode>[:<steps>]]   bench.py alone (default flags)
 #   pmc:<cfg>[:<mode>]  the PMC passes (each its own rocprofv3 run)
-#   motion:<kind>    bench.py --motion <kind> (orbit | fall), learned vs natural order
+#   motion           bench.py --motion none|orbit|fall x --dispatch learned|natural, N = 1 and --share 1/8
+#   timeline[:cases] tools/wave_timeline.py: every wave's span in a launch (diagnostic build)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOT=$(pwd)
@@ -119,6 +120,12 @@ EOF
           done
         done
       done ;;
+    timeline)
+      # per-wave start/end of render launches (diagnostic build, built on the CPU side beforehand:
+      # python tools/build_variant.py tools/ab/libgeo_wavelog.so -DGEO_WAVE_LOG=1)
+      timeout -k 10 400 python3 tools/wave_timeline.py --out "$OUT/wave_timeline.json" ${a1:+--cases $a1} \
+        > "$OUT/wave_timeline.txt" 2> "$OUT/wave_timeline.err"
+      rc=$?; cat "$OUT/wave_timeline.txt"; [ $rc -eq 0 ] || { tail -5 "$OUT/wave_timeline.err"; exit $rc; } ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

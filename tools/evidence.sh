@@ -20,6 +20,8 @@
 #   pmc:<cfg>[:<mode>]  the PMC passes (each its own rocprofv3 run)
 #   motion           bench.py --motion none|orbit|fall x --dispatch learned|natural, N = 1 and --share 1/8
 #   timeline[:cases] tools/wave_timeline.py: every wave's span in a launch (diagnostic build)
+#   ab:<cfgs>[:reps] interleaved A/B of LIBS="a.so b.so" (bench lines; configs comma-separated)
+#   fuzz[:n[:base]]  long GPU fuzz sweeps (direct, adversarial, fan, mips) on new seeds
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOT=$(pwd)
@@ -119,6 +121,37 @@ EOF
             done
           done
         done
+      done ;;
+    ab)
+      # interleaved A/B of prebuilt libraries (LIBS="a.so b.so ...", e.g. from
+      # tools/build_variant.py) on one box: ab:<cfg>[,<cfg>...][:reps]; a cfg
+      # ending in _fan runs --mode fan; the in-tree library is restored after
+      cfgs=${a1:-cfg3_4k}; reps=${a2:-3}
+      LIB=schwarzschild_raytracer_wgpu_amd/libgeo.so
+      cp "$LIB" "$OUT/.orig.so"
+      : > "$OUT/ab.txt"
+      for rep in $(seq 1 $reps); do
+        for c in ${cfgs//,/ }; do
+          cargs="--config ${c%_fan}"; [ "$c" != "${c%_fan}" ] && cargs="$cargs --mode fan"
+          for v in ${LIBS:?LIBS=\"a.so b.so\"}; do
+            cp "$v" "$LIB"
+            timeout -k 10 300 python3 bench.py $cargs --no-cpu-baseline --steps 200 > "$OUT/ab.json" 2> "$OUT/ab.err"
+            rc=$?; [ $rc -eq 0 ] || { tail -5 "$OUT/ab.err"; cp "$OUT/.orig.so" "$LIB"; exit $rc; }
+            python3 -c "
+import json,sys; d=json.loads(open(sys.argv[1]).read().splitlines()[-1])
+print('%-14s %-32s rep%s  ms/frame %.5f  kernel %.5f  frac %.4f' % (sys.argv[2], sys.argv[3].split('/')[-1], sys.argv[4], d['ms_per_step'], d['kernel_ms']['avg'], d['roofline']['frac']))" \
+              "$OUT/ab.json" "$c" "$v" "$rep" | tee -a "$OUT/ab.txt"
+          done
+        done
+      done
+      cp "$OUT/.orig.so" "$LIB" ;;
+    fuzz)
+      # long GPU fuzz sweeps on seeds beyond the committed ones: fuzz:<n>:<base>
+      for t in test_gpu_fuzz_bitexact test_gpu_fuzz_adversarial_bitexact test_gpu_fuzz_fan_mode_bitexact \
+               test_gpu_fuzz_mips_bitexact; do
+        GEO_FUZZ_N=${a1:-2000} GEO_FUZZ_BASE=${a2:-500000} timeout -k 10 900 python -u -m pytest tests/test_gpu_fuzz.py \
+          -m gpu -q -s -k "$t" --timeout 850 --timeout-method thread > "$OUT/fuzz_$t.txt" 2>&1
+        rc=$?; grep -h "^fuzz" "$OUT/fuzz_$t.txt"; tail -1 "$OUT/fuzz_$t.txt"; [ $rc -eq 0 ] || exit $rc
       done ;;
     timeline)
       # per-wave start/end of render launches (diagnostic build, built on the CPU side beforehand:

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Dumps an accretion disk's state after a run of PointCloud updates with
 orbits (respawns included: rs = 15 makes every particle fall) and a point
-draw, so two builds of libgeo can be compared byte for byte (tools/gpu_r04u.sh).
+draw, so two builds of libgeo can be compared byte for byte (an A/B of two libraries).
 
   python tools/points_dump.py OUT.npz
 """

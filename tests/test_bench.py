@@ -129,3 +129,28 @@ def test_batch_key_groups_a_moving_observer():
     assert _batch_key(sc(2.5)) != _batch_key(sc(0.9))       # across the horizon: another integration
     assert _batch_key(sc(0.8)) == _batch_key(sc(0.9))
     assert _batch_key(sc(2.5, mode=g.GEO_MODE_FAN)) != _batch_key(sc(2.4, mode=g.GEO_MODE_FAN))
+
+
+@pytest.mark.gpu
+def test_bench_two_ranks_gloo_frame_check():
+    """The N > 1 bench path on one GPU (two ranks share it over gloo, as the
+    rehearsals do): the self-launcher, the lead trials, batched launches and
+    rank 0's assembled frames equal to the single-launch frame."""
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dist-backend", "gloo",
+                        "--config", "cfg2_1080p", "--steps", "8", "--warmup", "2", "--spinup-frames", "4",
+                        "--lead-trial-frames", "8", "--frames-per-gather", "2"],
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["world_size"] == 2 and d["dist_backend"] == "gloo"
+    assert d["config"]["frames_per_launch"] == 2 and len(d["config"]["lead_trials_ms_per_frame"]) == 8
+    assert d["frame_check"]["ok"] is True and d["frame_check"]["ranks"] == 2
+    assert sum(d["per_rank"]["rows"]) == 1080

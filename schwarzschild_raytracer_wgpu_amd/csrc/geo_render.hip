@@ -100,9 +100,6 @@ struct RenderArgs {
     // cost_overhead (its out-of-loop work, in steps) into its tile's entry
     unsigned int* tile_cost;
     uint32_t cost_overhead;
-#if defined(GEO_PRIO_PERMILLE) && GEO_PRIO_PERMILLE > 0
-    uint32_t prio_tiles;  // experiment: workgroups of a learned order that raise their priority
-#endif
     // local row lr -> row0 + b*band_stride + (lr - b*band_rows), b = lr / band_rows
     // = umulhi(lr, band_magic) (band_rows_magic)
     uint32_t band_rows, band_magic, band_stride;
@@ -412,11 +409,6 @@ __global__ __launch_bounds__(kBlock) void geo_render_kernel(const RenderArgs a, 
     if (a.tile_order) {
         const uint32_t t = a.tile_order[blockIdx.y * gridDim.x + blockIdx.x];  // one scalar load
         tile = make_uint2(t & 0xFFFFu, t >> 16);
-#if defined(GEO_PRIO_PERMILLE) && GEO_PRIO_PERMILLE > 0
-        // experiment: the first GEO_PRIO_PERMILLE per mille of a learned
-        // order (its costliest tiles) issue at raised priority from the start
-        if (blockIdx.y * gridDim.x + blockIdx.x < a.prio_tiles) __builtin_amdgcn_s_setprio(2);
-#endif
     }
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x) >> 6;
     const uint32_t lane = threadIdx.x & 63u;
@@ -1388,9 +1380,6 @@ static int render_impl(geo_ctx* c, const geo_frame* frames, uint32_t nframes, si
     a.sky_total_bytes = c->sky_total_bytes;
     a.tile_order = nullptr;
     a.tile_cost = nullptr;
-#if defined(GEO_PRIO_PERMILLE) && GEO_PRIO_PERMILLE > 0
-    a.prio_tiles = (uint32_t)(((uint64_t)tiles_x * tiles_y * GEO_PRIO_PERMILLE) / 1000u);
-#endif
     a.cost_overhead = adaptive ? kCostOverheadAdaptive : kCostOverheadDirect;
     const int fb = c->fan_cur;
     a.fan = fb < 0 ? nullptr : c->fan[fb];

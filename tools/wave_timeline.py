@@ -168,13 +168,20 @@ def main():
 
             for _ in range(a.warm):
                 render()
+            # the clock falls within ~1 ms of an idle queue and takes ~25 ms of
+            # work to come back (bench.py): every logged launch follows >= 30 ms
+            # of plain ones, queued behind it with no sync in between
+            ev0 = (HipEvent(), HipEvent())
+            render(ev0)
+            torch.cuda.synchronize()
+            pre = max(8, math.ceil(30.0 / max(ev0[0].elapsed_time(ev0[1]), 1e-3)))
             per = []
             for _ in range(a.frames):
-                check(lib.geo_debug_set_wave_log(h, ctypes.c_void_p(log.data_ptr())), "log")
                 log.zero_()
                 ev = (HipEvent(), HipEvent())
-                for _ in range(3):  # keep the clock up: the logged launch follows two plain ones
+                for _ in range(pre):
                     render()
+                check(lib.geo_debug_set_wave_log(h, ctypes.c_void_p(log.data_ptr())), "log")
                 render(ev)
                 check(lib.geo_debug_set_wave_log(h, None), "log off")
                 torch.cuda.synchronize()

@@ -73,6 +73,9 @@ def parse():
                         "clamped to [1, 8]: the timed region ends with the last batch's gather and reassembly, "
                         "and its first batch's renders run before any gather starts, so a short run wants "
                         "shallow batches (20 steps: 2) and a long one amortises the host cost (200 steps: 8)")
+    p.add_argument("--frames-per-launch", type=int, default=1,
+                   help="N = 1: render this many consecutive frames in one launch (geo_render_band_set_batch), as "
+                        "the ranks at N > 1 do per gather batch; 1 (default) = one launch per frame")
     p.add_argument("--batch-launch", default="auto", choices=["auto", "on", "off"],
                    help="N > 1: render each gather batch's frames in ONE launch (geo_render_band_set_frames), "
                         "paying a launch's fixed cost (~12.6 us: dispatch, ramp, drain) once per batch instead of per "
@@ -347,11 +350,13 @@ def main():
 
     def make_sf(ld):
         lead, peer_bands = ld
+        one = lay_world == 1
         return ShardedFrame(ctx, frame, scene, W, H, args.band_rows, lay_rank, lay_world, dev,
                             dist if world > 1 else None, host_gather=args.dist_backend == "gloo",
-                            frames_per_gather=args.frames_per_gather,
+                            frames_per_gather=args.frames_per_launch if one else args.frames_per_gather,
                             render_streams=args.render_streams or (1 if world == 1 else 2), lead=lead,
-                            peer_bands=peer_bands, batch_launch=args.batch_launch != "off")
+                            peer_bands=peer_bands,
+                            batch_launch=(args.frames_per_launch > 1) if one else args.batch_launch != "off")
 
     # everything that syncs or reads back (lead trials, the diagnostic pass)
     # runs before the clock spin-up below, which flows straight into the

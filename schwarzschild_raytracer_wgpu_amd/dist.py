@@ -241,7 +241,8 @@ class ShardedFrame:
         self.layout = BandLayout(height, band_rows, world, rank, lead if world > 1 else 1,
                                  peer_bands if world > 1 else 1)
         self.rank, self.world, self.dist = rank, world, dist
-        self.K = max(1, int(frames_per_gather)) if world > 1 else 1
+        # one rank alone batches frames only to render them in one launch
+        self.K = max(1, int(frames_per_gather)) if world > 1 or batch_launch else 1
         self.S = min(2, max(1, int(render_streams)))
         from ._lib import GEO_MAX_BATCH_FRAMES
 

@@ -53,7 +53,7 @@ def _worker(rank, world, port, W, H, B, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,W,H,B", [(2, 48, 40, 8), (2, 33, 27, 8), (3, 40, 50, 16)])
+@pytest.mark.parametrize("world,W,H,B", [(2, 48, 40, 8), (2, 33, 27, 8), (3, 40, 50, 16), (8, 24, 88, 8)])
 def test_gloo_band_gather_reassembles_frame(world, W, H, B):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -227,7 +227,8 @@ def _worker_lead(rank, world, port, W, H, B, lead, K, q, peer_bands=1):
 
 @pytest.mark.parametrize("world,W,H,B,lead,K,pb", [(2, 40, 52, 8, 2, 2, 1), (3, 28, 72, 8, 4, 1, 1),
                                                    (3, 33, 40, 8, 2, 2, 1), (2, 40, 60, 8, 3, 2, 1),
-                                                   (3, 28, 88, 8, 3, 1, 2), (2, 36, 70, 8, 5, 2, 2)])
+                                                   (3, 28, 88, 8, 3, 1, 2), (2, 36, 70, 8, 5, 2, 2),
+                                                   (8, 20, 96, 8, 3, 2, 2)])  # 8: config 4's world, a 3:2 share
 def test_gloo_lead_layout_reassembles_frames(world, W, H, B, lead, K, pb):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()

@@ -76,7 +76,7 @@ EOF
       [ $rc -eq 0 ] || { tail -20 "$OUT/gloo8_bench.err"; exit $rc; } ;;
     bench|plain)
       cfg=${a1:-cfg3_4k}; mode=${a2:-}; steps=${a3:-20}
-      margs="--steps $steps --warmup 5"; [ -n "$mode" ] && margs="$margs --mode $mode"
+      margs="--config $cfg --steps $steps --warmup 5"; [ -n "$mode" ] && margs="$margs --mode $mode"
       name=${cfg}${mode:+_$mode}
       if [ $kind = plain ]; then
         timeout -k 10 400 python3 bench.py $margs > "$OUT/${name}_bench.json" 2> "$OUT/${name}_bench.err"

@@ -295,14 +295,10 @@ __device__ __forceinline__ float pixel_lambda(const RenderArgs& a, const geo::Pi
 template <uint32_t NF>
 __device__ __forceinline__ const geo::PixelConsts& frame_consts(const RenderArgs& a, const FrameBatch<NF>& fb,
                                                                 uint32_t z) {
-#if defined(GEO_BATCH_SHARED_K)  // experiment: every frame of a batch reads frame 0's constants
-    return a.k;
-#else
     if constexpr (NF > 1)
         return fb.k[z];
     else
         return a.k;
-#endif
 }
 
 // Pixels per lane: a fan-mode lane (level-0 sampler) draws two, rows

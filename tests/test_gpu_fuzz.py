@@ -1,6 +1,7 @@
 """Fuzz parity on the GPU: the HIP kernels (through the C-ABI) equal the
 oracle's f32 restatement bit for bit (mask, UV bits, steps, RGBA) on seeded
-random scenes (tests/fuzz_scenes.py), direct and adaptive, 64x36 each."""
+random scenes (tests/fuzz_scenes.py), direct and adaptive, 64x36 each; the
+batched band-set launch on random batches and layouts (test_gpu_fuzz_batch_bitexact)."""
 import os
 
 import numpy as np
@@ -133,3 +134,90 @@ def test_gpu_fuzz_mips_bitexact(geo, torch_mod):  # noqa: F811
             bad.append((desc, (sw, sh)))
     print(f"fuzz mips: {n} scenes at {w}x{h}, {len(bad)} differ")
     assert not bad, f"{len(bad)} of {n} scenes differ: {bad[:5]}"
+
+
+def test_gpu_fuzz_batch_bitexact(geo, torch_mod):  # noqa: F811
+    """geo_render_band_set_batch on seeded random batches: ragged frames,
+    1..8 frames per launch, each frame's own uniform and observer radius
+    (same side of the horizon; one radius in fan mode), random band layouts
+    (world 1..8, any rank, rank 0's taller bands), a gap between frames.
+    Every frame's packed bands == geo_render_band_set of that frame alone
+    (bytes, the gap untouched, step totals), and one frame per batch ==
+    the oracle's f32 restatement on its rows."""
+    from schwarzschild_raytracer_wgpu_amd import _lib
+    from schwarzschild_raytracer_wgpu_amd.scenes import make_sky
+
+    torch = torch_mod
+    dev = torch.device("cuda:0")
+    sky = make_sky("equirect", (256, 128))
+    ctx = make_ctx(geo, sky)
+    stream = torch.cuda.current_stream().cuda_stream
+    n_seeds = int(os.environ.get("GEO_FUZZ_N", 400))
+    base = int(os.environ.get("GEO_FUZZ_BASE", 30_000))
+    bad = []
+    for seed in range(base, base + n_seeds):
+        rng = np.random.default_rng(seed)
+        w, h = int(rng.integers(20, 130)), int(rng.integers(9, 90))
+        mode = (_lib.GEO_MODE_DIRECT, _lib.GEO_MODE_ADAPTIVE, _lib.GEO_MODE_FAN)[seed % 3]
+        frame0, scene0, desc = random_scene(seed, w, h, adaptive=mode == _lib.GEO_MODE_ADAPTIVE)
+        scene0.mode = mode
+        n = int(rng.integers(1, _lib.GEO_MAX_BATCH_FRAMES + 1))
+        frames, scenes = [frame0], [scene0]
+        for f in range(1, n):
+            frames.append(random_scene(seed * 16 + f + 1_000_000, w, h)[0])
+            s = geo.GeoScene.from_buffer_copy(bytes(scene0))
+            if mode != _lib.GEO_MODE_FAN:
+                r = scene0.r_obs * float(rng.uniform(0.9, 1.1))
+                if scene0.r_obs < scene0.rs:  # stay inside the horizon
+                    r = min(r, 0.995 * scene0.rs)
+                elif scene0.r_obs > scene0.rs:
+                    r = max(r, 1.005 * scene0.rs)
+                s.r_obs = r
+            scenes.append(s)
+        fan = None
+        if mode == _lib.GEO_MODE_FAN:
+            fan = ctx.solve_ray_fan(scene0.sphere_r, scene0.rs, 1000, scene0.step, 400, scene0.r_obs)
+        world = int(rng.integers(1, 9))
+        band = 8 * int(rng.choice([1, 2, 3]))  # band heights: multiples of 8 (geo.h)
+        lead = band * int(rng.integers(1, 3)) if rng.random() < 0.7 else 8 * int(rng.integers(1, band // 4 + 1))
+        rank = int(rng.integers(0, world))
+        row_stride = lead + (world - 1) * band
+        row0, band_h = (0, lead) if rank == 0 else (lead + (rank - 1) * band, band)
+        if row0 >= h:
+            row0, band_h, rank = 0, lead, 0
+        nbands = (h - row0 + row_stride - 1) // row_stride
+        packed = nbands * band_h * w * 4
+        stride = packed + 4 * int(rng.integers(0, 10))
+        out = torch.full((n * stride,), 7, dtype=torch.uint8, device=dev)
+        tot = torch.zeros(1, dtype=torch.int64, device=dev)
+        fa, sa = (geo.GeoFrame * n)(*frames), (geo.GeoScene * n)(*scenes)
+        st = _lib.lib.geo_render_band_set_batch(ctx._h, fa, sa, n, w, h, band_h, row0, row_stride, nbands,
+                                                out.data_ptr(), stride, tot.data_ptr(), stream)
+        layout = f"n={n} world={world} rank={rank} band={band_h} row0={row0} stride={row_stride} nbands={nbands}"
+        if st != _lib.GEO_OK:
+            bad.append((desc, layout, f"status {st}"))
+            continue
+        ref_tot = torch.zeros(1, dtype=torch.int64, device=dev)
+        same = True
+        for f in range(n):
+            ref = torch.full((packed,), 7, dtype=torch.uint8, device=dev)
+            ctx.render_band_set(frames[f], scenes[f], w, h, band_h, row0, row_stride, nbands, ref,
+                                steps_total=ref_tot)
+            got = out[f * stride:(f + 1) * stride]
+            same = same and torch.equal(got[:packed], ref) and bool((got[packed:] == 7).all())
+        torch.cuda.synchronize()
+        if mode != _lib.GEO_MODE_FAN:
+            same = same and int(tot.item()) == int(ref_tot.item())
+        # one frame of the batch against the oracle, on the rows its bands hold
+        f = int(rng.integers(0, n))
+        o = O.render_f32(frames[f], scenes[f], sky, w, h, fan=fan, threads=4)["rgba"]
+        got = out[f * stride:f * stride + packed].cpu().numpy().reshape(-1, w, 4)
+        for k, y in enumerate(y for j in range(nbands) for y in range(row0 + j * row_stride,
+                                                                        row0 + j * row_stride + band_h)):
+            if y < h and not np.array_equal(got[k], o[y]):
+                same = False
+                break
+        if not same:
+            bad.append((desc, layout))
+    print(f"fuzz batch: {n_seeds} batches, {len(bad)} differ")
+    assert not bad, f"{len(bad)} of {n_seeds} batches differ: {bad[:3]}"

@@ -148,7 +148,7 @@ print('%-14s %-32s rep%s  ms/frame %.5f  kernel %.5f  frac %.4f' % (sys.argv[2],
     fuzz)
       # long GPU fuzz sweeps on seeds beyond the committed ones: fuzz:<n>:<base>
       for t in test_gpu_fuzz_bitexact test_gpu_fuzz_adversarial_bitexact test_gpu_fuzz_fan_mode_bitexact \
-               test_gpu_fuzz_mips_bitexact; do
+               test_gpu_fuzz_mips_bitexact test_gpu_fuzz_batch_bitexact; do
         GEO_FUZZ_N=${a1:-2000} GEO_FUZZ_BASE=${a2:-500000} timeout -k 10 900 python -u -m pytest tests/test_gpu_fuzz.py \
           -m gpu -q -s -k "$t" --timeout 850 --timeout-method thread > "$OUT/fuzz_$t.txt" 2>&1
         rc=$?; grep -h "^fuzz" "$OUT/fuzz_$t.txt"; tail -1 "$OUT/fuzz_$t.txt"; [ $rc -eq 0 ] || exit $rc

@@ -20,8 +20,9 @@
 #   pmc:<cfg>[:<mode>]  the PMC passes (each its own rocprofv3 run)
 #   motion           bench.py --motion none|orbit|fall x --dispatch learned|natural, N = 1 and --share 1/8
 #   timeline[:cases] tools/wave_timeline.py: every wave's span in a launch (diagnostic build)
-#   ab:<cfgs>[:reps] interleaved A/B of LIBS="a.so b.so" (bench lines; configs comma-separated)
-#   fuzz[:n[:base]]  long GPU fuzz sweeps (direct, adversarial, fan, mips) on new seeds
+#   ab:<cfgs>[:reps] interleaved A/B of LIBS="a.so b.so" and/or ABARGS="args;args" (bench lines;
+#                    configs comma-separated; replaces the round-5 fpl_ab.sh / batch_ab.sh)
+#   fuzz[:n[:base]]  long GPU fuzz sweeps (direct, adversarial, fan, mips, batched launches) on new seeds
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOT=$(pwd)
@@ -123,24 +124,32 @@ EOF
         done
       done ;;
     ab)
-      # interleaved A/B of prebuilt libraries (LIBS="a.so b.so ...", e.g. from
-      # tools/build_variant.py) on one box: ab:<cfg>[,<cfg>...][:reps]; a cfg
-      # ending in _fan runs --mode fan; the in-tree library is restored after
+      # interleaved A/B on one box: ab:<cfg>[,<cfg>...][:reps]; a cfg ending
+      # in _fan runs --mode fan.  LIBS="a.so b.so ..." (prebuilt libraries,
+      # e.g. from tools/build_variant.py or tools/build_rev.sh; the in-tree
+      # library is restored after) and/or ABARGS="args;args;..." (bench.py
+      # argument sets, e.g. "--frames-per-launch 1;--frames-per-launch 8" or
+      # "--share 1/8 --frames-per-gather 8 --batch-launch on"); each
+      # (cfg, args, lib) is one line per rep
       cfgs=${a1:-cfg3_4k}; reps=${a2:-3}
       LIB=schwarzschild_raytracer_wgpu_amd/libgeo.so
       cp "$LIB" "$OUT/.orig.so"
+      libs=${LIBS:-$OUT/.orig.so}
+      IFS=';' read -r -a argsets <<< "${ABARGS:-}"; [ ${#argsets[@]} -eq 0 ] && argsets=("")
       : > "$OUT/ab.txt"
       for rep in $(seq 1 $reps); do
         for c in ${cfgs//,/ }; do
           cargs="--config ${c%_fan}"; [ "$c" != "${c%_fan}" ] && cargs="$cargs --mode fan"
-          for v in ${LIBS:?LIBS=\"a.so b.so\"}; do
-            cp "$v" "$LIB"
-            timeout -k 10 300 python3 bench.py $cargs --no-cpu-baseline --steps 200 > "$OUT/ab.json" 2> "$OUT/ab.err"
-            rc=$?; [ $rc -eq 0 ] || { tail -5 "$OUT/ab.err"; cp "$OUT/.orig.so" "$LIB"; exit $rc; }
-            python3 -c "
+          for xa in "${argsets[@]}"; do
+            for v in $libs; do
+              cp "$v" "$LIB"
+              timeout -k 10 300 python3 bench.py $cargs $xa --no-cpu-baseline --steps 200 > "$OUT/ab.json" 2> "$OUT/ab.err"
+              rc=$?; [ $rc -eq 0 ] || { tail -5 "$OUT/ab.err"; cp "$OUT/.orig.so" "$LIB"; exit $rc; }
+              python3 -c "
 import json,sys; d=json.loads(open(sys.argv[1]).read().splitlines()[-1])
-print('%-14s %-32s rep%s  ms/frame %.5f  kernel %.5f  frac %.4f' % (sys.argv[2], sys.argv[3].split('/')[-1], sys.argv[4], d['ms_per_step'], d['kernel_ms']['avg'], d['roofline']['frac']))" \
-              "$OUT/ab.json" "$c" "$v" "$rep" | tee -a "$OUT/ab.txt"
+print('%-14s %-44s %-28s rep%s  ms/frame %.5f  kernel %.5f  frac %.4f  frame_check %s' % (sys.argv[2], sys.argv[5], sys.argv[3].split('/')[-1], sys.argv[4], d['ms_per_step'], d['kernel_ms']['avg'], d['roofline']['frac'], (d.get('frame_check') or {}).get('ok')))" \
+                "$OUT/ab.json" "$c" "$v" "$rep" "${xa:--}" | tee -a "$OUT/ab.txt"
+            done
           done
         done
       done

@@ -1,5 +1,10 @@
+#!/bin/bash
+# gloo rehearsals of the multi-rank present path on one GPU (world 2 and 3,
+# both launchers, several gather batch sizes and rank-0 leads): every run's
+# frame_check must pass.  The driver's N = 8 form is tools/evidence.sh gloo8.
+#   TAG=r05 bash tools/gpu_dist_rehearse.sh
 set -u
-cd $GRAFT_REPO_ROOT
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 TAG=${TAG:-r03}
 # spec: world, frames per gather ("d": bench.py's default for the run length), steps, lead, launcher

@@ -102,7 +102,22 @@ EOF
             "FETCH_SIZE" "WRITE_SIZE" "TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum"
             "GRBM_GUI_ACTIVE SQ_BUSY_CU_CYCLES MeanOccupancyPerCU")
       EXTRA_ARGS=${mode:+--mode $mode} CONFIG=$cfg bash tools/gpu_pmc.sh "$TAG/pmc_$name" "${SETS[@]}" || exit $?
-      python3 tools/pmc_to_profile.py "$TAG/pmc_$name" "$OUT/${name}_pmc.json" "$name" > /dev/null || exit $? ;;
+      # the labels bench.py's pmc_profile() matches: "<cfg> (WxH, ..., <mode>)"
+      labels=$(python3 - "$cfg" "$mode" <<'PY'
+import sys
+from schwarzschild_raytracer_wgpu_amd.scenes import CONFIGS
+cfg, mode = sys.argv[1], sys.argv[2]
+c = CONFIGS[cfg]
+m = mode or c.mode
+what = {"direct": f"{c.max_steps} steps", "adaptive": f"RK5(4) tol {c.tol:g}", "fan": None}[m]
+print(f"{cfg} ({c.width}x{c.height}{', ' + what if what else ''}, {m})")
+print({"direct": "geo_render_kernel<GEO_MODE_DIRECT, kCurvedOut>",
+       "adaptive": "geo_render_kernel<GEO_MODE_ADAPTIVE, kCurvedOut>",
+       "fan": "geo_render_kernel<GEO_MODE_FAN> (two pixels per lane)"}[m])
+PY
+) || exit $?
+      python3 tools/pmc_to_profile.py "$TAG/pmc_$name" "$OUT/${name}_pmc.json" "$(sed -n 1p <<< "$labels")" \
+        "$(sed -n 2p <<< "$labels")" > /dev/null || exit $? ;;
     motion)
       # learned vs natural dispatch order on moving frames: N = 1 (one launch
       # per frame) and one 8-rank share alone in batched launches of 8 frames

@@ -12,6 +12,8 @@ event pairs around each of N back-to-back launches after a spin-up:
            (block i on XCD i % 8), so XCD k gets the k-th eighth of the tiles
            in row-major order, whose sky lines then meet in one L2
   xcd_lpt  the same regions, each in longest-first order
+  xcd_blk  XCD regions as a 2 x 4 grid of blocks of tiles (fan mode: every
+           tile costs the same, so regions of equal size finish together)
   auto     the product default: GEO_DISPATCH_LONGEST_FIRST, the order learned
            on the device every 16 renders (its recording renders and
            rebuild kernels inside the timed launches)
@@ -36,11 +38,12 @@ from schwarzschild_raytracer_wgpu_amd.timing import HipEvent  # noqa: E402
 TW, TH, WW, WH = 32, 8, 16, 4  # tile and wave shapes (geo_render.hip)
 
 
-def xcd_order(packed, rank=None):
+def xcd_order(packed, rank=None, parts=None):
     """Block i -> XCD i % 8: XCD k's blocks take the k-th eighth of `packed`
-    (row-major tiles), in `rank` order within the eighth if given."""
+    (row-major tiles; or parts[k], indices into packed), in `rank` order
+    within the eighth if given."""
     n = packed.size
-    parts = np.array_split(np.arange(n), 8)
+    parts = np.array_split(np.arange(n), 8) if parts is None else parts
     if rank is not None:
         parts = [p[np.argsort(rank[p], kind="stable")] for p in parts]
     out = np.empty(n, np.uint32)
@@ -110,6 +113,10 @@ def main():
         packed = (np.arange(ty)[:, None] << 16 | np.arange(tx)[None, :]).astype(np.uint32).ravel()
         by_cost = np.argsort(-cost.ravel(), kind="stable")
         orders = {"natural": None, "xcd": xcd_order(packed)}
+        if fan:
+            idx = np.arange(tx * ty).reshape(ty, tx)
+            orders["xcd_blk"] = xcd_order(packed, parts=[b.ravel() for rb in np.array_split(idx, 4, axis=0)
+                                                         for b in np.array_split(rb, 2, axis=1)])
         if not fan:
             orders["auto"] = "auto"
         if not fan:  # fan-mode pixels have no steps: every tile costs the same

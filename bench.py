@@ -100,6 +100,9 @@ def parse():
     p.add_argument("--mips", action="store_true",
                    help="sample the sky through its mip chain (GEO_FLAG_MIPS, the reference's textureSample); "
                         "the metric's line is the level-0 path")
+    p.add_argument("--ring-f64", action="store_true",
+                   help="GEO_FLAG_RING_F64: redraw the capture band's pixels in f64 beside the f32 draw (N = 1, "
+                        "direct mode, one frame per launch; off on the metric's line)")
     p.add_argument("--no-frame-check", action="store_true",
                    help="skip rank 0's check, after the timed region, that every frame of the timed run's last "
                         "batch (the frames as assembled for present) equals a single-launch render of the frame; "
@@ -330,6 +333,10 @@ def main():
         raise SystemExit("--motion with --mode fan: the fan-mode draw needs a fan solved per radius (not benched)")
     tol = cfg.tol if mode == g.GEO_MODE_ADAPTIVE else 0.0
     sampler_flags = g._lib.GEO_FLAG_MIPS if args.mips else 0
+    if args.ring_f64:
+        if mode != g.GEO_MODE_DIRECT or args.mips or world > 1 or args.frames_per_launch > 1:
+            raise SystemExit("--ring-f64: direct mode, level-0 sampler, N = 1, one frame per launch (geo.h)")
+        sampler_flags |= g._lib.GEO_FLAG_RING_F64
     scene = g.make_scene(cfg.rs, cfg.sphere_r, obs.get_radial_position(), cfg.step, cfg.max_steps, mode,
                          flags=sampler_flags, tol=tol)
     sky = make_sky(cfg.sky, cfg.sky_size)
@@ -684,6 +691,8 @@ def main():
         stepping = f"step pi/100, {cfg.max_steps} max RK4 steps"
     if args.motion != "none":
         metric += f" [moving observer: {args.motion}]"
+    if args.ring_f64:
+        metric += " [GEO_FLAG_RING_F64: the capture band redrawn in f64]"
     if args.share:
         metric += f" [rank {lay_rank}'s share of {lay_world}, alone]"
     out = {
@@ -714,6 +723,7 @@ def main():
             "lead_trials_ms_per_frame": lead_trials,
             "render_streams": sf.S,
             "frames_per_launch": sf.K if sf.batch else 1,
+            "ring_f64": bool(args.ring_f64),
         },
         "per_gpu": value / world,
         "world_size": dist.get_world_size() if world > 1 else 1,
@@ -774,7 +784,12 @@ def main():
         fan = None
         if mode == g.GEO_MODE_FAN:  # the fan the draws read, as the host's copy
             fan = ctx.solve_ray_fan(cfg.sphere_r, cfg.rs, cfg.max_steps, cfg.step, 400, obs.get_radial_position())
-        out["cpu_baseline"] = cpu_baseline(frame, scene, sky, W, H, args, ctx, fan)
+        # (with --ring-f64 the CPU path is the f32 draw's, compared with the f32 draw)
+        cpu_scene = scene
+        if args.ring_f64:
+            cpu_scene = g.GeoScene.from_buffer_copy(bytes(scene))
+            cpu_scene.flags &= ~g._lib.GEO_FLAG_RING_F64
+        out["cpu_baseline"] = cpu_baseline(frame, cpu_scene, sky, W, H, args, ctx, fan)
         cpu_ok = out["cpu_baseline"]["matches_gpu"]["ok"]
         if mode != g.GEO_MODE_FAN:
             out["reference_equivalent"] = reference_fan_cost(ctx, cfg, obs.get_radial_position())

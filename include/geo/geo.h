@@ -43,8 +43,9 @@
 extern "C" {
 #endif
 
-#define GEO_ABI_VERSION 5  /* 4: geo_render_band_set_frames, geo_assemble_shares;
-                                5: geo_render_band_set_batch, geo_dispatch_stats */
+#define GEO_ABI_VERSION 6  /* 4: geo_render_band_set_frames, geo_assemble_shares;
+                                5: geo_render_band_set_batch, geo_dispatch_stats;
+                                6: GEO_FLAG_RING_F64 */
 
 typedef enum geo_status {
     GEO_OK = 0,
@@ -83,6 +84,21 @@ typedef enum geo_status {
                                    level-0 bilinear sample otherwise).  Quads are frame-
                                    aligned, so row0 must be even (GEO_EINVAL otherwise);
                                    band layouts keep bands 8-row aligned. */
+#define GEO_FLAG_RING_F64 8u    /* (off on the benchmarked path) GEO_MODE_DIRECT only: the
+                                   pixels next to the capture orbit, |b/b_c - 1| <
+                                   GEO_RING_X by the f32 ray (b = r_obs cos(theta) /
+                                   sqrt(1 - rs/r_obs), b_c = 3 sqrt(3) rs / 2; rs > 0,
+                                   r_obs > rs), are drawn again in f64 -- the camera ray,
+                                   solve_geodesic and the sky direction, as the literal
+                                   f64 restatement does -- on a context side stream
+                                   concurrently with the f32 draw, and written over it
+                                   (RGBA, mask, UV, per-pixel steps) after both.  There
+                                   the orbit amplifies the f32 roundings past the 1e-4 UV
+                                   bar.  steps_total keeps counting the f32
+                                   draw's steps.  Not with GEO_FLAG_COMPOSITE,
+                                   GEO_FLAG_MIPS, more than one frame or 2^31 pixels
+                                   (GEO_EINVAL). */
+#define GEO_RING_X 8e-3f
 
 /* Observer motion states, ObserverState (SR/simulation/observer.rs:12-16). */
 #define GEO_OBSERVER_UNMOVING 0

@@ -88,6 +88,8 @@ def _load() -> ctypes.CDLL:
         "geo_oracle_lod_q8_n": (None, [vp, u32, vp]),
         "geo_oracle_render_mips_f32": (i, [vp, vp, vp, u32, vp, u32, u32, u32, u32, u32, u32, i, vp, vp, vp, vp,
                                            vp]),
+        "geo_oracle_ring_kx": (ctypes.c_float, [vp]),
+        "geo_oracle_ring_band": (i, [vp, vp, u32, u32, u32, u32, u32, vp]),
     }
     for n, (r, a) in sig.items():
         fn = getattr(lib, n)
@@ -182,6 +184,18 @@ def render_f64(frame, scene, width, height, row0=0, nrows=None, fan=None, thread
     if rc != 0:
         raise ValueError(f"geo_oracle_render_f64: {rc}")
     return dict(mask=mask, uv=uv, steps=steps, lam=lam, theta=theta)
+
+
+def ring_band(frame, scene, width, height, row0=0, nrows=None, row_step=1):
+    """GEO_FLAG_RING_F64's band (geo.h) on rows row0 + i row_step: 1 where the
+    f32 ray's |b/b_c - 1| < GEO_RING_X (all 0 when the flag does not apply)."""
+    nrows = (height - row0 + row_step - 1) // row_step if nrows is None else nrows
+    band = np.empty((nrows, width), np.uint8)
+    fr, sc = as_frame(frame), as_scene(scene)  # alive across the call
+    rc = lib.geo_oracle_ring_band(_addr(fr), _addr(sc), width, height, row0, nrows, row_step, _np(band))
+    if rc != 0:
+        raise ValueError(f"geo_oracle_ring_band: {rc}")
+    return band
 
 
 def render_f32(frame, scene, sky, width, height, row0=0, nrows=None, row_step=1, fan=None, threads=8,

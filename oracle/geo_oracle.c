@@ -628,10 +628,8 @@ static uint32_t blend_over(uint32_t s, uint32_t dst) {
     return out;
 }
 
-static void pixel_f32(const geo_frame* f, const cam_f32* cam, const fconsts* k, int mode, const float* fan, uint32_t n_fan,
-                      const uint32_t* sky, uint32_t sw, uint32_t sh, int opaque, int composite, uint32_t width,
-                      uint32_t height, uint32_t px, uint32_t py, uint32_t* rgba, uint8_t* bh_out, float* uv,
-                      uint32_t* steps) {
+/* The pixel's unit ray in the central frame, c2 (shader.wgsl:58-75). */
+static void camera_c2(const geo_frame* f, const cam_f32* cam, uint32_t px, uint32_t py, float* c2) {
     /* camera ray (shader.wgsl:60-64): d = M0 (-ny M0[12], -nx M0[13], M0[14]) with the pixel-centre NDC
      * nx = (2 px + 1 - W)/W, ny = (H - 2 py - 1)/H, affine in (px, py): d = py A + px B + C, the frame
      * constants in f64 rounded once to f32 (cam_f32) */
@@ -644,17 +642,25 @@ static void pixel_f32(const geo_frame* f, const cam_f32* cam, const fconsts* k, 
     float len = sqrtf(fmaf(d[2], d[2], fmaf(d[1], d[1], d[0] * d[0])));
     float id = 1.0f / fmaf(-kk, d[2], len);
     float g = kt * id;
-    float c2[3];
     float e[3] = {d[0] * g, d[1] * g, fmaf(-kk, len, d[2]) * id};
     if (cc->m1_identity) { /* movement_to_central = I (observer.rs:243-246): skipped, -0 stays -0 */
         c2[0] = e[0]; c2[1] = e[1]; c2[2] = e[2];
     } else {
         m3vf(f->movement_to_central, e[0], e[1], e[2], c2);
     }
+}
+
+static void pixel_f32(const geo_frame* f, const cam_f32* cam, const fconsts* k, int mode, const float* fan, uint32_t n_fan,
+                      const uint32_t* sky, uint32_t sw, uint32_t sh, int opaque, int composite, uint32_t width,
+                      uint32_t height, uint32_t px, uint32_t py, uint32_t* rgba, uint8_t* bh_out, float* uv,
+                      uint32_t* steps, float* ct_out) {
+    float c2[3];
+    camera_c2(f, cam, px, py, c2);
     float st = c2[2] > -1.0f ? c2[2] : -1.0f; /* med3(c2z, -1, 1): NaN -> -1 */
     st = st < 1.0f ? st : 1.0f;
     float rho2 = sqrtf(fmaf(c2[1], c2[1], c2[0] * c2[0])); /* cos theta */
     float rrho = 1.0f / rho2;
+    if (ct_out) *ct_out = rho2;
     float lam;
     *steps = 0;
     if (mode == (int)GEO_MODE_FAN) {
@@ -718,7 +724,45 @@ typedef struct {
     double* lam;
     double* theta;
     uint64_t total;
+    int ring;      /* GEO_FLAG_RING_F64 applies (ring_kx) */
+    float ring_kx; /* r_obs / (sqrt(1 - rs/r_obs) 3 sqrt(3)/2 rs), rounded once to f32 */
 } job_t;
+
+/* GEO_FLAG_RING_F64 (geo.h): the f32 ray's |b/b_c - 1| = |kx cos(theta) - 1|,
+ * kx from the scene in f64 rounded once (the library computes the same
+ * expression on its host). */
+float geo_oracle_ring_kx(const geo_scene* s) {
+    double rs = (double)s->rs, r = (double)s->r_obs;
+    double e = sqrt(1.0 - rs / r);
+    return (float)(r / (e * (1.5 * sqrt(3.0) * rs)));
+}
+
+static int ring_applies(const geo_scene* s) {
+    return (s->flags & GEO_FLAG_RING_F64) != 0 && s->rs > 0.0f && s->r_obs > s->rs;
+}
+
+/* the band test on the f32 ray's cos(theta) */
+static int in_ring(float kx, float ct) { return fabsf(kx * ct - 1.0f) < GEO_RING_X; }
+
+int geo_oracle_ring_band(const geo_frame* f, const geo_scene* s, uint32_t width, uint32_t height, uint32_t row0,
+                         uint32_t nrows, uint32_t row_step, uint8_t* band) {
+    if (!f || !s || !band || width == 0 || height == 0 || row_step == 0) return -1;
+    if ((uint64_t)row0 + (uint64_t)(nrows ? nrows - 1 : 0) * row_step >= height) return -1;
+    int ring = ring_applies(s) && s->mode == GEO_MODE_DIRECT;
+    float kx = ring ? geo_oracle_ring_kx(s) : 0.0f;
+    cam_f32 cam = camera_f32(f, width, height);
+    for (uint32_t r = 0; r < nrows; ++r)
+        for (uint32_t px = 0; px < width; ++px) {
+            uint8_t b = 0;
+            if (ring) {
+                float c2[3];
+                camera_c2(f, &cam, px, row0 + r * row_step, c2);
+                b = (uint8_t)in_ring(kx, sqrtf(fmaf(c2[1], c2[1], c2[0] * c2[0])));
+            }
+            band[(size_t)r * width + px] = b;
+        }
+    return 0;
+}
 
 static void* job_f32(void* arg) {
     job_t* j = (job_t*)arg;
@@ -729,10 +773,25 @@ static void* job_f32(void* arg) {
             size_t o = (size_t)r * j->width + px;
             uint32_t rgba, st;
             uint8_t bh;
-            float uv[2];
+            float uv[2], ct;
             memcpy(&rgba, j->rgba + 4 * o, 4); /* the target, for GEO_FLAG_COMPOSITE */
             pixel_f32(j->f, &j->cam, &j->k, (int)j->s->mode, j->fan, j->n_fan, j->sky, j->sw, j->sh, j->opaque,
-                      (j->s->flags & GEO_FLAG_COMPOSITE) != 0, j->width, j->height, px, py, &rgba, &bh, uv, &st);
+                      (j->s->flags & GEO_FLAG_COMPOSITE) != 0, j->width, j->height, px, py, &rgba, &bh, uv, &st, &ct);
+            total += st; /* steps_total counts the f32 draw's steps (geo.h GEO_FLAG_RING_F64) */
+            if (j->ring && in_ring(j->ring_kx, ct)) {
+                /* the capture-orbit band: the pixel again in f64 (the literal
+                 * restatement), sampled at its UV rounded to f32 */
+                geo_oracle_px p;
+                geo_oracle_pixel_f64(j->f, j->s, NULL, 0, j->width, j->height, px, py, &p);
+                float U = (float)p.u, V = (float)p.v;
+                if (!(U == U)) U = 0.0f;
+                if (!(V == V)) V = 0.0f;
+                uv[0] = clampf(U, 0.0f, 1.0f);
+                uv[1] = clampf(V, 0.0f, 1.0f);
+                bh = (uint8_t)p.bh;
+                st = p.steps;
+                rgba = bh ? 0xFF000000u : blend_over(bilinear_level(j->sky, j->sw, j->sh, uv[0], uv[1]), 0xFF000000u);
+            }
             memcpy(j->rgba + 4 * o, &rgba, 4);
             if (j->mask) j->mask[o] = bh;
             if (j->uv) {
@@ -740,7 +799,6 @@ static void* job_f32(void* arg) {
                 j->uv[2 * o + 1] = uv[1];
             }
             if (j->steps) j->steps[o] = st;
-            total += st;
         }
     }
     j->total = total;
@@ -811,10 +869,15 @@ int geo_oracle_render_f32(const geo_frame* f, const geo_scene* s, const float* f
     if (!f || !s || !sky || !rgba || width == 0 || height == 0 || row_step == 0) return -1;
     if ((uint64_t)row0 + (uint64_t)(nrows ? nrows - 1 : 0) * row_step >= height) return -1;
     if (s->mode == GEO_MODE_FAN && (!fan || n_fan < 2)) return -1;
+    if ((s->flags & GEO_FLAG_RING_F64) &&
+        (s->mode != GEO_MODE_DIRECT || (s->flags & (GEO_FLAG_COMPOSITE | GEO_FLAG_MIPS))))
+        return -1; /* the library's GEO_EINVAL */
     job_t j;
     memset(&j, 0, sizeof(j));
     j.f = f;
     j.s = s;
+    j.ring = ring_applies(s);
+    j.ring_kx = j.ring ? geo_oracle_ring_kx(s) : 0.0f;
     j.k = make_fconsts(s);
     j.cam = camera_f32(f, width, height);
     j.fan = fan;
@@ -942,7 +1005,7 @@ static void* job_grid(void* arg) {
             size_t o = (size_t)r * g->gw + x;
             uint32_t rgba = 0;
             pixel_f32(g->f, g->cam, g->k, g->mode, g->fan, g->n_fan, g->sky, g->sw, g->sh, 1, 0, g->width, g->height,
-                      x, g->r_lo + r, &rgba, &g->bh[o], &g->uv[2 * o], &g->steps[o]);
+                      x, g->r_lo + r, &rgba, &g->bh[o], &g->uv[2 * o], &g->steps[o], NULL);
         }
     return NULL;
 }
@@ -954,6 +1017,7 @@ int geo_oracle_render_mips_f32(const geo_frame* f, const geo_scene* s, const flo
     if (!f || !s || !sky || !rgba || width == 0 || height == 0 || nrows == 0 || (row0 & 1u)) return -1;
     if ((uint64_t)row0 + nrows > height) return -1;
     if (s->mode == GEO_MODE_FAN && (!fan || n_fan < 2)) return -1;
+    if (s->flags & GEO_FLAG_RING_F64) return -1; /* not with GEO_FLAG_MIPS (geo.h) */
     if (threads < 1) threads = 1;
     if (threads > 64) threads = 64;
     uint32_t* chain = (uint32_t*)malloc(geo_oracle_mip_chain_texels(sky_w, sky_h) * 4);

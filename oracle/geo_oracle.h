@@ -75,6 +75,14 @@ int geo_oracle_render_f32(const geo_frame* f, const geo_scene* s, const float* f
                           int threads, uint8_t* rgba, uint8_t* mask, float* uv, uint32_t* steps,
                           uint64_t* steps_total);
 
+/* GEO_FLAG_RING_F64 (geo.h): render_f32 draws the band's pixels with
+ * geo_oracle_pixel_f64 (UV rounded to f32, the f32 sampler); the band is
+ * |kx cos(theta) - 1| < GEO_RING_X on the f32 ray.  ring_band: that band
+ * (1/0 per pixel) on rows row0 + i row_step. */
+float geo_oracle_ring_kx(const geo_scene* s);
+int geo_oracle_ring_band(const geo_frame* f, const geo_scene* s, uint32_t width, uint32_t height, uint32_t row0,
+                         uint32_t nrows, uint32_t row_step, uint8_t* band);
+
 /* GEO_FLAG_MIPS mirror (geo_pixel.h): the 4-level box-filtered mip chain
  * (levels one after another, geo_oracle_mip_chain_texels(w, h) texels), and
  * rows [row0, row0 + nrows) (row0 even) sampled trilinearly with the level of

@@ -858,6 +858,268 @@ __global__ void geo_fan_kernel(double sphere_r, double schwarz_r, uint32_t max_i
     fan[i] = (float)(FRAC_PI_2 - angle);
 }
 
+// ---- GEO_FLAG_RING_F64 (geo.h; DESIGN.md §2, "The capture band in f64") ----
+// Next to the capture orbit the orbit's instability amplifies the f32 draw's
+// roundings past the UV bar; these pixels are drawn again in f64 by a kernel
+// on a side stream, concurrently with the f32 draw, and written over its
+// output afterwards (geo_ring_scatter).  The band is decided on the f32 ray,
+// exactly as the oracle decides it (the same f32 operations), so which
+// pixels are redrawn is part of the specification.
+
+// One pixel of the band: its column, local (output) row and frame row
+// (geo_ring_scan), then what the f64 redraw gives it (geo_ring_kernel).
+struct RingPixel {
+    uint32_t px, lr, py;
+};
+struct RingEntry {
+    uint64_t o;
+    uint32_t rgba;
+    uint32_t steps_bh;  // steps; bit 31: black hole
+    float u, v;
+};
+
+struct RingArgs {
+    FrameK f;
+    uint32_t width, height, row0, nrows, band_rows, band_magic, band_stride;
+    uint32_t tiles_y;  // 16-row blocks of the launch's rows
+    float kx;          // r_obs / (sqrt(1 - rs/r_obs) 3 sqrt(3)/2 rs), rounded once (geo_oracle_ring_kx)
+    double rs, sphere_r, r_obs, step;
+    uint32_t max_steps;
+    const uint32_t* sky;
+    uint32_t sky_bytes, sky_pitch_b, sky_opaque;
+    float sky_w256, sky_h256;
+    RingPixel* pix;
+    RingEntry* list;
+    uint32_t* count;
+    uint32_t cap;  // entries the lists hold (a pixel is listed once: >= the launch's pixels)
+};
+
+// The literal loop's exits with its step count (sphere_ray_tracer.rs:134-191:
+// `steps = iteration + 1` once a step is taken; the loop test on the state
+// before it ends the loop without one), on fan_integrate's scaled f64 RK4
+// and its groups of steps per exit branch.
+template <bool FLAT>
+__device__ __attribute__((noinline)) double ring_integrate(double sphere_r, double schwarz_r, uint32_t max_iter, double step, double r,
+                                 double u_bar0, uint32_t* steps) {
+    const double NO_VALUE = GEO_NO_VALUE;
+    const double r3_2 = 3. * schwarz_r / 2.;
+    const double c = FLAT ? 1. : r3_2;
+    const double u0 = 1. / r;
+    const double SU = c / sphere_r;
+    const double BD = c * (0.9 * fmin(u0, 1. / fmax(sphere_r, r3_2)));
+    const double HU = FLAT ? __builtin_inf() : c / schwarz_r;
+    const double h = step, hh = step / 2., hh2 = step * step / 4., hhh = step * step / 2., h6 = step / 6.,
+                 h2_6 = step * step / 6.;
+    double U = c * u0, V = c * u_bar0;
+    *steps = 0;
+    if (!(U > 0.)) return NO_VALUE;
+    double angle = 0.;
+    uint32_t it = 0;
+    // fan_integrate's groups: one exit branch per kFanGroup steps, a stopping
+    // group replayed step by step below (the same arithmetic, the literal
+    // loop's step count)
+    while (it + kFanGroup <= max_iter) {
+        double su[kFanGroup + 1], sv[kFanGroup + 1];
+        su[0] = U;
+        sv[0] = V;
+        bool stop = false;
+#pragma unroll
+        for (int j = 0; j < kFanGroup; ++j) {
+            fan_rk4<FLAT>(su[j], sv[j], h, hh, hh2, hhh, h6, h2_6, &su[j + 1], &sv[j + 1]);
+            stop |= fan_test<FLAT>(su[j], sv[j], su[j + 1], SU, BD, HU) != 0;
+        }
+        if (stop) break;
+        U = su[kFanGroup];
+        V = sv[kFanGroup];
+#pragma unroll
+        for (int j = 0; j < kFanGroup; ++j) angle += step;
+        it += kFanGroup;
+        *steps = it;
+    }
+    for (; it < max_iter; ++it) {
+        if (!FLAT && U > HU && V > 0.) return NO_VALUE;
+        double NU, NV;
+        fan_rk4<FLAT>(U, V, h, hh, hh2, hhh, h6, h2_6, &NU, &NV);
+        *steps = it + 1;
+        if ((NU > SU) != (U > SU)) {
+            double ns, wu, wv;
+            if (fabs(V) > fabs(NV)) {
+                ns = 0.;
+                wu = U;
+                wv = V;
+            } else {
+                ns = h;
+                wu = NU;
+                wv = NV;
+            }
+            for (int n = 0; n < 3; ++n) {
+                ns -= (wu - SU) / wv;
+                const double n2 = ns * ns;
+                fan_rk4<FLAT>(U, V, ns, ns / 2., n2 / 4., n2 / 2., ns / 6., n2 / 6., &wu, &wv);
+            }
+            return angle + ns;
+        }
+        if (NU < BD) return NO_VALUE;
+        U = NU;
+        V = NV;
+        angle += step;
+    }
+    return NO_VALUE;
+}
+
+// ocml's f64 atan2, asin, sin, cos as calls: inlined, they take the
+// kernel's registers past 200 VGPRs (2 waves per SIMD beside the f32 draw)
+__device__ __attribute__((noinline)) double ring_atan2(double y, double x) { return atan2(y, x); }
+__device__ __attribute__((noinline)) double ring_asin(double x) { return asin(x); }
+__device__ __attribute__((noinline)) double ring_sin(double x) { return sin(x); }
+__device__ __attribute__((noinline)) double ring_cos(double x) { return cos(x); }
+
+__device__ __forceinline__ void ring_m3v(const float* m, const double* v, double* o) {
+    for (int i = 0; i < 3; ++i) o[i] = (double)m[i] * v[0] + (double)m[4 + i] * v[1] + (double)m[8 + i] * v[2];
+}
+__device__ __attribute__((noinline)) void ring_to_cart(double phi, double lam, double* c) {
+    c[0] = ring_cos(phi) * ring_cos(lam);
+    c[1] = ring_sin(phi) * ring_cos(lam);
+    c[2] = ring_sin(lam);
+}
+
+// The pixel as the literal f64 restatement draws it (shader.wgsl:57-106 with
+// the geodesic at theta = the pixel's lambda, geo_oracle_pixel_f64): UV, the
+// black-hole test and the steps.  Direct mode, rs > 0, r_obs > rs.
+__device__ void ring_pixel_f64(const RingArgs& a, uint32_t px, uint32_t py, double* u, double* v, bool* bh,
+                               uint32_t* steps) {
+    const double PI = 3.14159265358979323846, FRAC_PI_2 = 1.57079632679489661923;
+    const geo_frame& f = a.f.frame;
+    const float* m0 = f.display_to_movement;
+    const double ndc_x = ((double)px + 0.5) / (double)a.width * 2. - 1.;
+    const double ndc_y = 1. - ((double)py + 0.5) / (double)a.height * 2.;
+    double c[3] = {-ndc_y * (double)m0[12], -ndc_x * (double)m0[13], 1. * (double)m0[14]};
+    double d[3];
+    ring_m3v(m0, c, d);
+    const double len = sqrt(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]);
+    d[0] /= len;
+    d[1] /= len;
+    d[2] /= len;
+    double phi = ring_atan2(d[1], d[0]);
+    double lam = ring_asin(d[2]);
+    const double k = (double)f.psi_factor_and_position[0];
+    const double sin_result = ring_sin(lam);
+    lam = ring_asin((sin_result - k) / (1. - sin_result * k));
+    ring_to_cart(phi, lam, c);
+    ring_m3v(f.movement_to_central, c, d);
+    phi = ring_atan2(d[1], d[0]);
+    const double theta = ring_asin(d[2]);
+    // sphere_ray_tracer.rs:38-49 at theta (r_obs > rs: the outside branch)
+    const double r = a.r_obs;
+    const double rotation = r * ring_cos(theta);
+    const bool r_falling = theta > 0.;
+    const double energy = sqrt(1. - a.rs / r);
+    double angle, u_bar0;
+    *steps = 0;
+    if (solve_geodesic_f64_init(a.sphere_r, a.rs, r, energy, rotation, r_falling, &angle, &u_bar0))
+        angle = ring_integrate<false>(a.sphere_r, a.rs, a.max_steps, a.step, r, u_bar0, steps);
+    const double lam2 = FRAC_PI_2 - angle;
+    *bh = lam2 < -7.;
+    ring_to_cart(phi, lam2, c);
+    ring_m3v(f.central_to_uv, c, d);
+    phi = ring_atan2(d[1], d[0]);
+    lam = ring_asin(d[2]);
+    double uu = phi / (FRAC_PI_2 * 4.);
+    if (uu < 0.) uu += 1.;
+    *u = uu;
+    *v = 0.5 - lam / (FRAC_PI_2 * 2.);
+    (void)PI;
+}
+
+// The band test, kRingScanRows pixels per lane (a column of them 16 rows
+// apart: 16 x 256 pixels per workgroup, few long waves, as the wave launch
+// rate bounds a grid of short ones; geo_render_kernel's band mapping): the
+// band's pixels go to a dense list, a wave's pixels of one row with one
+// atomic (the lanes' ranks in its ballot).
+constexpr uint32_t kRingScanRows = 16;
+__global__ __launch_bounds__(256) void geo_ring_scan(const RingArgs a) {
+    __builtin_amdgcn_s_setprio(2);  // beside the f32 draw (ring_fork): it gates the f64 redraw
+    const uint32_t lane = threadIdx.x & 63u;
+    for (uint32_t by = blockIdx.y; by < a.tiles_y; by += gridDim.y) {
+        const uint32_t px = blockIdx.x * 16u + (threadIdx.x & 15u);
+        for (uint32_t k = 0; k < kRingScanRows; ++k) {
+            const uint32_t lr = by * (16u * kRingScanRows) + k * 16u + (threadIdx.x >> 4);
+            bool in = px < a.width && lr < a.nrows;
+            uint32_t py = 0;
+            if (in) {
+                const uint32_t band = __umulhi(lr, a.band_magic);
+                py = a.row0 + band * a.band_stride + (lr - band * a.band_rows);
+                in = py < a.height;
+            }
+            bool ring = false;
+            if (in) {
+                float c2x, c2y, c2z;
+                geo::pixel_central_dir(a.f.cam, a.f.frame.movement_to_central, a.f.frame.psi_factor_and_position[0],
+                                       a.f.kt, px, py, &c2x, &c2y, &c2z);
+                const float ct = geo::central_rho(c2x, c2y);
+                ring = fabsf(a.kx * ct - 1.0f) < GEO_RING_X;
+            }
+            const uint64_t m = __ballot(ring);
+            if (m == 0) continue;
+            const uint32_t first = (uint32_t)__ffsll((unsigned long long)m) - 1u;
+            uint32_t base = 0;
+            if (lane == first) base = atomicAdd(a.count, (uint32_t)__popcll(m));
+            base = (uint32_t)__shfl((int)base, (int)first);
+            const uint32_t slot = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+            if (ring && slot < a.cap) a.pix[slot] = RingPixel{px, lr, py};
+        }
+    }
+}
+
+// The f64 redraw of the listed pixels, one lane each (a dense list: the
+// long f64 chains run on full waves).
+constexpr uint32_t kRingBlocks = 2048, kRingThreads = 64;
+__global__ __launch_bounds__(kRingThreads) void geo_ring_kernel(const RingArgs a) {
+    // its few waves are long f64 chains beside the f32 draw's waves: they
+    // issue first (the draw keeps the rest of each SIMD's issue)
+    __builtin_amdgcn_s_setprio(3);
+    const uint32_t n = min(*a.count, a.cap);
+    for (uint32_t i = blockIdx.x * kRingThreads + threadIdx.x; i < n; i += kRingBlocks * kRingThreads) {
+        const RingPixel p = a.pix[i];
+        double u, v;
+        bool bh;
+        uint32_t steps;
+        ring_pixel_f64(a, p.px, p.py, &u, &v, &bh, &steps);
+        float U = (float)u, V = (float)v;
+        if (!(U == U)) U = 0.0f;
+        if (!(V == V)) V = 0.0f;
+        U = fminf(fmaxf(U, 0.0f), 1.0f);
+        V = fminf(fmaxf(V, 0.0f), 1.0f);
+        const PaddedSkyQuad quad{__builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(a.sky), 0, (int)a.sky_bytes,
+                                                                   kBufferRsrcWord3),
+                                 a.sky_pitch_b};
+        RingEntry e;
+        e.o = (uint64_t)p.lr * a.width + p.px;
+        e.rgba = bh ? geo::kBlackRGBA : geo::sample_sky_qf(quad, a.sky_w256, a.sky_h256, a.sky_opaque != 0, U, V);
+        e.steps_bh = (steps & 0x7FFFFFFFu) | (bh ? 0x80000000u : 0u);
+        e.u = U;
+        e.v = V;
+        a.list[i] = e;
+    }
+}
+
+// After the f32 draw and geo_ring_kernel: the redrawn pixels over the output.
+// (The count is read after both: the list's entries < count are written.)
+__global__ __launch_bounds__(256) void geo_ring_scatter(const RingEntry* list, const uint32_t* count, uint32_t cap,
+                                                        uint32_t* next, uint32_t* rgba, uint8_t* mask, float2* uv,
+                                                        uint32_t* steps) {
+    const uint32_t n = min(*count, cap);
+    // the next render's counter (the other of the pair; nothing reads it now)
+    if (blockIdx.x == 0 && threadIdx.x == 0) *next = 0u;
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u) {
+        const RingEntry e = list[i];
+        rgba[e.o] = e.rgba;
+        if (mask) mask[e.o] = (uint8_t)(e.steps_bh >> 31);
+        if (uv) uv[e.o] = make_float2(e.u, e.v);
+        if (steps) steps[e.o] = e.steps_bh & 0x7FFFFFFFu;
+    }
+}
+
 }  // namespace
 
 
@@ -1017,6 +1279,15 @@ void geo_ctx_destroy(geo_ctx* c) {
     if (c->step_slots) (void)hipFree(c->step_slots);
     if (c->learn_valid || c->tile_cap) (void)hipEventSynchronize(c->order_written);
     if (c->learn_stream) (void)hipStreamDestroy(c->learn_stream);
+    if (c->ring_free_rec) (void)hipEventSynchronize(c->ring_free);
+    if (c->ring_stream) (void)hipStreamSynchronize(c->ring_stream);
+    if (c->ring_list) (void)hipFree(c->ring_list);
+    if (c->ring_pix) (void)hipFree(c->ring_pix);
+    if (c->ring_count) (void)hipFree(c->ring_count);
+    if (c->ring_fork) (void)hipEventDestroy(c->ring_fork);
+    if (c->ring_join) (void)hipEventDestroy(c->ring_join);
+    if (c->ring_free) (void)hipEventDestroy(c->ring_free);
+    if (c->ring_stream) (void)hipStreamDestroy(c->ring_stream);
     for (int b = 0; b < 2; ++b)
         if (c->order[b]) (void)hipFree(c->order[b]);
     if (c->tile_cost) (void)hipFree(c->tile_cost);
@@ -1291,6 +1562,94 @@ static int invalid_call(geo_ctx* c) {
 // out_frame_stride bytes after frame f - 1's (a batch draws colour only).
 // scene_per_frame: `scene` points at nframes scenes, frame f's at scene[f]
 // (they may differ in r_obs only); otherwise one scene for every frame.
+// GEO_FLAG_RING_F64: the list holds one entry per pixel of the launch at
+// most (the band may cover a whole frame); growing it waits for the last
+// scatter, which read the old one.  The side stream and its events are
+// made on first use.
+constexpr uint32_t kRingScatterBlocks = 512;
+static int ensure_ring(geo_ctx* c, size_t n) {
+    if (!c->ring_stream) {
+        if (hipStreamCreateWithFlags(&c->ring_stream, hipStreamNonBlocking) != hipSuccess) {
+            c->ring_stream = nullptr;
+            return GEO_EHIP;
+        }
+        if (hipEventCreateWithFlags(&c->ring_fork, kCtxEventFlags) != hipSuccess ||
+            hipEventCreateWithFlags(&c->ring_join, kCtxEventFlags) != hipSuccess ||
+            hipEventCreateWithFlags(&c->ring_free, kCtxEventFlags) != hipSuccess)
+            return GEO_EHIP;
+        if (hipMalloc(&c->ring_count, 256) != hipSuccess) {
+            c->ring_count = nullptr;
+            return GEO_ENOMEM;
+        }
+        // the pair of counters: render k counts into ring_count[k % 2], and
+        // its scatter zeroes the other one for render k + 1
+        if (hipMemset(c->ring_count, 0, 256) != hipSuccess) return GEO_EHIP;
+        c->ring_parity = 0;
+    }
+    if (c->ring_cap >= n) return GEO_OK;
+    if (c->ring_free_rec && hipEventSynchronize(c->ring_free) != hipSuccess) return GEO_EHIP;
+    if (c->ring_list) (void)hipFree(c->ring_list);
+    if (c->ring_pix) (void)hipFree(c->ring_pix);
+    c->ring_list = c->ring_pix = nullptr;
+    c->ring_cap = 0;
+    if (hipMalloc(&c->ring_list, n * sizeof(RingEntry)) != hipSuccess ||
+        hipMalloc(&c->ring_pix, n * sizeof(RingPixel)) != hipSuccess) {
+        if (c->ring_list) (void)hipFree(c->ring_list);
+        c->ring_list = c->ring_pix = nullptr;
+        return GEO_ENOMEM;
+    }
+    c->ring_cap = n;
+    return GEO_OK;
+}
+
+// The band test (geo_ring_scan) and the f64 redraw (geo_ring_kernel) forked
+// onto the ring stream before the f32 draw; ring_join marks their end.
+static int ring_fork(geo_ctx* c, const RenderArgs& a, const FrameK& fk, const geo_scene& sc, hipStream_t s) {
+    const int est = ensure_ring(c, (size_t)a.nrows * a.width);
+    if (est) return est;
+    RingArgs r;
+    r.f = fk;
+    r.width = a.width;
+    r.height = a.height;
+    r.row0 = a.row0;
+    r.nrows = a.nrows;
+    r.band_rows = a.band_rows;
+    r.band_magic = a.band_magic;
+    r.band_stride = a.band_stride;
+    r.tiles_y = (a.nrows + 16u * kRingScanRows - 1u) / (16u * kRingScanRows);
+    const double rs = (double)sc.rs, ro = (double)sc.r_obs;
+    r.kx = (float)(ro / (std::sqrt(1.0 - rs / ro) * (1.5 * std::sqrt(3.0) * rs)));  // geo_oracle_ring_kx
+    r.rs = rs;
+    r.sphere_r = (double)sc.sphere_r;
+    r.r_obs = ro;
+    r.step = (double)sc.step;
+    r.max_steps = sc.max_steps;
+    r.sky = a.sky;
+    r.sky_bytes = a.sky_bytes;
+    r.sky_pitch_b = a.sky_pitch_b;
+    r.sky_opaque = a.sky_opaque;
+    r.sky_w256 = a.sky_w256;
+    r.sky_h256 = a.sky_h256;
+    r.pix = static_cast<RingPixel*>(c->ring_pix);
+    r.list = static_cast<RingEntry*>(c->ring_list);
+    r.count = c->ring_count + c->ring_parity;  // zeroed by the previous scatter (or at allocation)
+    r.cap = (uint32_t)((size_t)a.nrows * a.width);
+    // the band test and the f64 redraw on the ring stream, beside the f32
+    // draw: after the caller's stream so far, and after the previous
+    // scatter (which read the lists) if that ran on another stream
+    hipStream_t rs_ = c->ring_stream;
+    if (hipEventRecord(c->ring_fork, s) != hipSuccess || hipStreamWaitEvent(rs_, c->ring_fork, 0) != hipSuccess)
+        return GEO_EHIP;
+    if (c->ring_free_rec && c->ring_free_stream != s && hipStreamWaitEvent(rs_, c->ring_free, 0) != hipSuccess)
+        return GEO_EHIP;
+    const uint32_t gy = r.tiles_y < kMaxGridY ? r.tiles_y : kMaxGridY;
+    hipLaunchKernelGGL(geo_ring_scan, dim3((a.width + 15u) / 16u, gy), dim3(256), 0, rs_, r);
+    hipLaunchKernelGGL(geo_ring_kernel, dim3(kRingBlocks), dim3(kRingThreads), 0, rs_, r);
+    if (hipGetLastError() != hipSuccess) return GEO_EHIP;
+    if (hipEventRecord(c->ring_join, rs_) != hipSuccess) return GEO_EHIP;
+    return GEO_OK;
+}
+
 static int render_impl(geo_ctx* c, const geo_frame* frames, uint32_t nframes, size_t out_frame_stride,
                        const geo_scene* scene, bool scene_per_frame, uint32_t width, uint32_t height, uint32_t row0, uint32_t nrows,
                        uint32_t band_rows, uint32_t band_stride, uint8_t* out_rgba8, uint8_t* out_mask,
@@ -1302,7 +1661,13 @@ static int render_impl(geo_ctx* c, const geo_frame* frames, uint32_t nframes, si
     c->time_start = c->time_stop = nullptr;
     if (scene->mode != GEO_MODE_DIRECT && scene->mode != GEO_MODE_FAN && scene->mode != GEO_MODE_ADAPTIVE)
         return GEO_EINVAL;
-    if ((scene->flags & ~(GEO_FLAG_DEFER_STEPS | GEO_FLAG_COMPOSITE | GEO_FLAG_MIPS)) != 0) return GEO_EINVAL;
+    if ((scene->flags & ~(GEO_FLAG_DEFER_STEPS | GEO_FLAG_COMPOSITE | GEO_FLAG_MIPS | GEO_FLAG_RING_F64)) != 0)
+        return GEO_EINVAL;
+    const bool ring_flag = (scene->flags & GEO_FLAG_RING_F64) != 0;
+    if (ring_flag && (scene->mode != GEO_MODE_DIRECT || nframes != 1 ||
+                      (scene->flags & (GEO_FLAG_COMPOSITE | GEO_FLAG_MIPS)) != 0 ||
+                      (uint64_t)nrows * width >= (1ull << 31)))  // the lists' 32-bit counts
+        return GEO_EINVAL;
     // frame-aligned 2 x 2 quads: the rows a wave covers start on even frame rows
     const bool mips = (scene->flags & GEO_FLAG_MIPS) != 0;
     if (mips && ((row0 | band_stride) & 1u) != 0) return GEO_EINVAL;
@@ -1451,6 +1816,13 @@ static int render_impl(geo_ctx* c, const geo_frame* frames, uint32_t nframes, si
             if (c->order_cur >= 0) a.tile_order = c->order[c->order_cur];
         }
     }
+    // GEO_FLAG_RING_F64: the band's f64 redraw forks onto the context's ring
+    // stream before the f32 draw, so that its long f64 chains run beside it
+    const bool ring = ring_flag && scene->rs > 0.0f && scene->r_obs > scene->rs;
+    if (ring) {
+        const int rs = ring_fork(c, a, fk[0], *scene, s);
+        if (rs) return rs;
+    }
     int st;
     if (scene->mode == GEO_MODE_FAN) {
         // after the solve that wrote the buffer (geo_ctx: on the solve's own
@@ -1488,6 +1860,21 @@ static int render_impl(geo_ctx* c, const geo_frame* frames, uint32_t nframes, si
         }
     }
     if (st) return st;
+    if (ring) {
+        // the redrawn pixels over the f32 draw; `done` then covers the ring
+        // kernel too (its sky reads), for geo_set_sky and the context's waits
+        if (hipStreamWaitEvent(s, c->ring_join, 0) != hipSuccess) return GEO_EHIP;
+        hipExtLaunchKernelGGL(geo_ring_scatter, dim3(kRingScatterBlocks), dim3(256), 0, s, nullptr, done, 0,
+                              static_cast<const RingEntry*>(c->ring_list), c->ring_count + c->ring_parity,
+                              (uint32_t)((size_t)a.nrows * a.width), c->ring_count + (1 - c->ring_parity), a.out_rgba,
+                              a.out_mask,
+                              a.out_uv, a.out_steps);
+        if (hipGetLastError() != hipSuccess) return GEO_EHIP;
+        if (hipEventRecord(c->ring_free, s) != hipSuccess) return GEO_EHIP;
+        c->ring_free_rec = true;
+        c->ring_free_stream = s;
+        c->ring_parity = 1 - c->ring_parity;
+    }
     if (record) {
         // rebuild the order into the buffer not in use, on the context's
         // learn stream, after every render of the context issued so far (this

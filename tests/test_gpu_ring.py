@@ -1,0 +1,235 @@
+"""GEO_FLAG_RING_F64 (geo.h; DESIGN.md §2, "The capture band in f64"): the
+pixels next to the capture orbit drawn again in f64 on a side stream and
+written over the f32 draw.
+
+Against the oracle (its f32 mirror with the same band drawn by the f64
+literal restatement, oracle render_f32 + GEO_FLAG_RING_F64): outside the
+band every output bit for bit (the f32 draw is untouched); the band itself
+the same pixels (decided on the f32 ray by the same f32 operations), each
+with the f64 literal's mask and steps and its UV to RING_UV_TOL (the GPU's
+f64 solve is the scaled RK4 of geo_fan_kernel and its atan2/asin/sin/cos
+are ocml's: f64 roundings apart, amplified near the orbit), RGBA within
+one level where the UV differ.  Against the f64 literal on whole config
+frames: every pixel inside north_star's bar, the capture band included.
+"""
+import math
+
+import numpy as np
+import pytest
+
+import f64_bar as B
+import oracle as O
+from fuzz_scenes import random_scene
+from helpers import default_frame, default_scene
+
+pytestmark = pytest.mark.gpu
+
+RING_UV_TOL = 1e-6  # band pixels, GPU f64 vs oracle f64 (both far inside the 1e-4 bar)
+
+
+@pytest.fixture(scope="module")
+def torch_mod():
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    return torch
+
+
+@pytest.fixture(scope="module")
+def geo():
+    import schwarzschild_raytracer_wgpu_amd as g
+
+    return g
+
+
+def _render(geo, torch, ctx, frame, scene, w, h):
+    dev = torch.device("cuda:0")
+    rgba = torch.empty(h * w * 4, dtype=torch.uint8, device=dev)
+    mask = torch.empty(h * w, dtype=torch.uint8, device=dev)
+    uv = torch.empty(h * w * 2, dtype=torch.float32, device=dev)
+    steps = torch.empty(h * w, dtype=torch.int32, device=dev)
+    tot = torch.zeros(1, dtype=torch.int64, device=dev)
+    ctx.render_rows(frame, scene, w, h, 0, h, rgba, mask, uv, steps, tot)
+    torch.cuda.synchronize()
+    return dict(rgba=rgba.cpu().numpy().reshape(h, w, 4), mask=mask.cpu().numpy().reshape(h, w),
+                uv=uv.cpu().numpy().reshape(h, w, 2), steps=steps.cpu().numpy().view(np.uint32).reshape(h, w),
+                total=int(tot.item()))
+
+
+def _ring(geo, scene):
+    s = geo.GeoScene.from_buffer_copy(bytes(scene))
+    s.flags |= geo._lib.GEO_FLAG_RING_F64
+    return s
+
+
+def _compare(hip, ref, band):
+    out = ~band
+    for f in ("mask", "steps", "rgba"):
+        assert np.array_equal(hip[f][out], ref[f][out]), f"{f} differs outside the band"
+    assert np.array_equal(hip["uv"][out].view(np.uint32), ref["uv"][out].view(np.uint32)), "uv outside the band"
+    assert np.array_equal(hip["mask"][band], ref["mask"][band]), "mask in the band"
+    du = np.abs(hip["uv"][band].astype(np.float64) - ref["uv"][band].astype(np.float64))
+    du = np.minimum(du, 1.0 - du)  # U wraps
+    assert (du.max() if du.size else 0.0) <= RING_UV_TOL, f"band uv {du.max()}"
+    same_uv = (hip["uv"][band].view(np.uint32) == ref["uv"][band].view(np.uint32)).all(axis=-1)
+    d_rgba = np.abs(hip["rgba"][band].astype(np.int32) - ref["rgba"][band].astype(np.int32)).max(axis=-1)
+    assert (d_rgba[same_uv] == 0).all(), "band rgba differs at identical UV"
+    assert (d_rgba <= 1).all(), "band rgba"
+    steps_bad = int((hip["steps"][band] != ref["steps"][band]).sum())
+    return {"band": int(band.sum()), "uv_max": float(du.max()) if du.size else 0.0,
+            "uv_bits_differ": int((~same_uv).sum()), "steps_differ": steps_bad}
+
+
+def test_ring_default_pose_against_the_oracle(geo, torch_mod):
+    from schwarzschild_raytracer_wgpu_amd.scenes import make_sky
+
+    w, h = 480, 270
+    sky = make_sky("equirect", (512, 256))
+    ctx = geo.Context(0)
+    ctx.set_sky(sky)
+    for cam in [(math.pi, 0.0), (math.pi + 0.3, 0.2), (math.pi - 0.5, -0.4)]:
+        frame = default_frame(w, h, camera=cam)
+        scene = _ring(geo, default_scene(2048))
+        hip = _render(geo, torch_mod, ctx, frame, scene, w, h)
+        ref = O.render_f32(frame, scene, sky, w, h, threads=8)
+        band = O.ring_band(frame, scene, w, h).astype(bool)
+        assert band.sum() > 100  # the frame crosses the orbit's band
+        st = _compare(hip, ref, band)
+        assert st["steps_differ"] == 0, st
+        # steps_total is the f32 draw's (geo.h): the flag does not change it
+        plain = _render(geo, torch_mod, ctx, frame, default_scene(2048), w, h)
+        assert hip["total"] == plain["total"] == ref["steps_total"]
+        print("ring default pose", cam, st)
+    ctx.close()
+
+
+def test_ring_fuzz_scenes_against_the_oracle(geo, torch_mod):
+    from schwarzschild_raytracer_wgpu_amd.scenes import make_sky
+
+    w, h = 96, 54
+    sky = make_sky("equirect", (256, 128))
+    ctx = geo.Context(0)
+    ctx.set_sky(sky)
+    seen = 0
+    steps_differ = 0
+    for seed in range(40_000, 40_300):
+        frame, scene, desc = random_scene(seed, w, h)
+        scene = _ring(geo, scene)
+        hip = _render(geo, torch_mod, ctx, frame, scene, w, h)
+        ref = O.render_f32(frame, scene, sky, w, h, threads=8)
+        band = O.ring_band(frame, scene, w, h).astype(bool)
+        seen += int(band.any())
+        st = _compare(hip, ref, band)
+        steps_differ += st["steps_differ"]
+    print(f"ring fuzz: 300 scenes, {seen} with band pixels, {steps_differ} band steps differ")
+    assert seen > 30
+    ctx.close()
+
+
+def test_ring_band_set_equals_rows(geo, torch_mod):
+    """The redraw follows the launch's band mapping: a band set equals the
+    same rows of the whole frame."""
+    from schwarzschild_raytracer_wgpu_amd.scenes import make_sky
+
+    torch = torch_mod
+    w, h = 320, 180
+    dev = torch.device("cuda:0")
+    ctx = geo.Context(0)
+    ctx.set_sky(make_sky("equirect", (256, 128)))
+    frame = default_frame(w, h)
+    scene = _ring(geo, default_scene(2048))
+    full = torch.empty(h * w * 4, dtype=torch.uint8, device=dev)
+    ctx.render_rows(frame, scene, w, h, 0, h, full)
+    row0, stride, band_rows = 8, 24, 8
+    nb = (h - row0 + stride - 1) // stride
+    out = torch.empty(nb * band_rows * w * 4, dtype=torch.uint8, device=dev)
+    ctx.render_band_set(frame, scene, w, h, band_rows, row0, stride, nb, out)
+    torch.cuda.synchronize()
+    img = full.view(h, w, 4).cpu().numpy()
+    got = out.view(nb * band_rows, w, 4).cpu().numpy()
+    rows = [y for j in range(nb) for y in range(row0 + j * stride, row0 + j * stride + band_rows)]
+    for k, y in enumerate(rows):
+        if y < h:
+            assert np.array_equal(got[k], img[y]), y
+    ctx.close()
+
+
+@pytest.mark.parametrize("cfgname", ["cfg2_1080p", "cfg3_4k"])
+def test_ring_config_frame_meets_the_bar_everywhere(geo, torch_mod, cfgname):
+    """Whole config frames against the f64 literal: with the flag no pixel is
+    over the 1e-4 UV bar (the capture band and the sky's poles included) and
+    no mask flips; the same frame without it has pixels over the bar next to
+    the orbit (profiles/r05p_f64_full_frame.json)."""
+    from schwarzschild_raytracer_wgpu_amd.scenes import CONFIGS, make_sky
+
+    torch = torch_mod
+    cfg = CONFIGS[cfgname]
+    w, h = cfg.width, cfg.height
+    obs = geo.Observer(cfg.rs, cfg.fov, w, h)
+    obs.set_position(*cfg.position)
+    obs.set_camera(*cfg.camera)
+    obs.set_energy(cfg.energy)
+    frame = obs.calc_transformation_pipeline()
+    r = obs.get_radial_position()
+    scene = geo.make_scene(cfg.rs, cfg.sphere_r, r, cfg.step, cfg.max_steps, geo.GEO_MODE_DIRECT)
+    ctx = geo.Context(0)
+    ctx.set_sky(make_sky("equirect", (512, 256)))
+    dev = torch.device("cuda:0")
+    rgba = torch.empty(h * w * 4, dtype=torch.uint8, device=dev)
+    mask = torch.empty(h * w, dtype=torch.uint8, device=dev)
+    uv = torch.empty(h * w * 2, dtype=torch.float32, device=dev)
+    ctx.render_rows(frame, _ring(geo, scene), w, h, 0, h, rgba, mask, uv)
+    torch.cuda.synchronize()
+    m = mask.view(h, w).cpu().numpy()
+    u = uv.view(h, w, 2).cpu().numpy()
+    ref = O.render_f64(frame, scene, w, h, threads=16)
+    sky = (m == 0) & (ref["mask"] == 0)
+    e = B.uv_err(u, ref["uv"])
+    over = int((sky & (e > B.UV_BAR)).sum())
+    flips = int((m != ref["mask"]).sum())
+    print(f"{cfgname} ring: uv max {e[sky].max():.3e}, over the bar {over}, mask flips {flips}")
+    assert flips == 0
+    assert over == 0
+    ctx.close()
+
+
+def test_ring_rejects_what_it_does_not_draw(geo, torch_mod):
+    import ctypes
+
+    from schwarzschild_raytracer_wgpu_amd import _lib
+    from schwarzschild_raytracer_wgpu_amd.scenes import make_sky
+
+    torch = torch_mod
+    w, h = 64, 32
+    ctx = geo.Context(0)
+    ctx.set_sky(make_sky("equirect", (64, 32)))
+    frame = default_frame(w, h)
+    out = torch.empty(2 * h * w * 4, dtype=torch.uint8, device=torch.device("cuda:0"))
+    stream = torch.cuda.current_stream().cuda_stream
+
+    def rows(scene):
+        return _lib.lib.geo_render_rows(ctx._h, ctypes.byref(frame), ctypes.byref(scene), w, h, 0, h,
+                                        out.data_ptr(), None, None, None, None, stream)
+
+    ok = _ring(geo, default_scene(64))
+    assert rows(ok) == _lib.GEO_OK
+    for mode in (geo.GEO_MODE_ADAPTIVE, geo.GEO_MODE_FAN):
+        s = _ring(geo, geo.make_scene(1.0, 50.0, 2.5, math.pi / 100, 64, mode))
+        if mode == geo.GEO_MODE_FAN:
+            ctx.solve_ray_fan(50.0, 1.0, 1000, math.pi / 100, 400, 2.5, host=False)
+        assert rows(s) == _lib.GEO_EINVAL, mode
+    for flag in (_lib.GEO_FLAG_COMPOSITE, _lib.GEO_FLAG_MIPS):
+        s = _ring(geo, default_scene(64))
+        s.flags |= flag
+        assert rows(s) == _lib.GEO_EINVAL, flag
+    fa = (geo.GeoFrame * 2)(frame, frame)
+    assert _lib.lib.geo_render_band_set_frames(ctx._h, fa, 2, ctypes.byref(ok), w, h, 8, 0, 8, 4, out.data_ptr(),
+                                               h * w * 4, None, stream) == _lib.GEO_EINVAL
+    # no capture orbit (flat space, inside the horizon): the flag draws the f32 frame
+    for s in (geo.make_scene(0.0, 50.0, 2.5, math.pi / 100, 64, geo.GEO_MODE_DIRECT),
+              geo.make_scene(1.0, 50.0, 0.7, math.pi / 100, 64, geo.GEO_MODE_DIRECT)):
+        assert O.ring_band(frame, _ring(geo, s), w, h).sum() == 0
+        assert rows(_ring(geo, s)) == _lib.GEO_OK
+    torch.cuda.synchronize()
+    ctx.close()

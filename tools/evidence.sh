@@ -17,6 +17,7 @@
 #                    bench line and the trace's timed-window average from the
 #                    SAME invocation (tools/trace_window.py)
 #   plain:<cfg>[:<mode>[:<steps>]]   bench.py alone (default flags)
+#                    (bench and plain: BENCH_ARGS="..." adds bench.py flags, e.g. --ring-f64)
 #   pmc:<cfg>[:<mode>]  the PMC passes (each its own rocprofv3 run)
 #   motion           bench.py --motion none|orbit|fall x --dispatch learned|natural, N = 1 and --share 1/8
 #   timeline[:cases] tools/wave_timeline.py: every wave's span in a launch (diagnostic build)
@@ -77,7 +78,7 @@ EOF
       [ $rc -eq 0 ] || { tail -20 "$OUT/gloo8_bench.err"; exit $rc; } ;;
     bench|plain)
       cfg=${a1:-cfg3_4k}; mode=${a2:-}; steps=${a3:-20}
-      margs="--config $cfg --steps $steps --warmup 5"; [ -n "$mode" ] && margs="$margs --mode $mode"
+      margs="--config $cfg --steps $steps --warmup 5 ${BENCH_ARGS:-}"; [ -n "$mode" ] && margs="$margs --mode $mode"
       name=${cfg}${mode:+_$mode}
       if [ $kind = plain ]; then
         timeout -k 10 400 python3 bench.py $margs > "$OUT/${name}_bench.json" 2> "$OUT/${name}_bench.err"

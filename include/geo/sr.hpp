@@ -292,9 +292,11 @@ class BasicSphereBuffer : public SchwarzschildSphereShaderDraw {
     // mipmaps: sample the texture's 4-level mip chain trilinearly as the
     // reference's textureSample does (Texture::new_with_mipmaps(..., 4),
     // GEO_FLAG_MIPS); off, the level-0 bilinear sample the benchmark measures.
+    // ring_f64: the capture band's pixels redrawn in f64 (GEO_FLAG_RING_F64:
+    // direct mode, the level-0 sampler, the pass's first sphere).
     BasicSphereBuffer(int device, double sphere_radius, double schwarz_radius, const Image& texture_image,
                       uint32_t mode = GEO_MODE_DIRECT, uint32_t max_iter = MAX_ITER, double step = STEP,
-                      bool mipmaps = false)
+                      bool mipmaps = false, bool ring_f64 = false)
         : ctx_(std::make_shared<Context>(device)),
           ray_tracer_(sphere_radius, schwarz_radius, max_iter, step, NR_NODES_HALF, ctx_),
           sphere_radius_(sphere_radius),
@@ -302,7 +304,8 @@ class BasicSphereBuffer : public SchwarzschildSphereShaderDraw {
           max_iter_(max_iter),
           step_(step),
           mode_(mode),
-          mipmaps_(mipmaps) {
+          mipmaps_(mipmaps),
+          ring_f64_(ring_f64) {
         check(geo_set_sky(ctx_->get(), texture_image.rgba.data(), texture_image.width, texture_image.height),
               "geo_set_sky");
     }
@@ -326,7 +329,8 @@ class BasicSphereBuffer : public SchwarzschildSphereShaderDraw {
         s.step = (float)step_;
         s.max_steps = max_iter_;
         s.mode = mode_;
-        s.flags = (pass.cleared ? 0u : GEO_FLAG_COMPOSITE) | (mipmaps_ ? GEO_FLAG_MIPS : 0u);
+        s.flags = (pass.cleared ? 0u : GEO_FLAG_COMPOSITE) | (mipmaps_ ? GEO_FLAG_MIPS : 0u) |
+                  (ring_f64_ ? GEO_FLAG_RING_F64 : 0u);
         s.tol = 0.0f;
         check(geo_render_rows(ctx_->get(), &pass.uniform, &s, pass.width, pass.height, 0, pass.height, pass.target,
                               nullptr, nullptr, nullptr, nullptr, pass.stream),
@@ -343,6 +347,7 @@ class BasicSphereBuffer : public SchwarzschildSphereShaderDraw {
     double step_;
     uint32_t mode_;
     bool mipmaps_;
+    bool ring_f64_;
     double radial_position_ = 0.0;
 };
 

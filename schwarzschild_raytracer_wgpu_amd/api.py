@@ -360,13 +360,16 @@ class BasicSphereBuffer:
 
     def __init__(self, ctx: Context | int, sphere_radius: float, schwarz_radius: float, texture_rgba: np.ndarray,
                  max_iter: int = MAX_ITER, step: float = STEP, mode: int = _lib.GEO_MODE_DIRECT,
-                 mipmaps: bool = False):
+                 mipmaps: bool = False, ring_f64: bool = False):
         """mipmaps: sample the texture's 4-level mip chain trilinearly, as the
         reference's textureSample does (Texture::new_with_mipmaps(..., 4),
-        GEO_FLAG_MIPS); off, the level-0 bilinear sample the benchmark measures."""
+        GEO_FLAG_MIPS); off, the level-0 bilinear sample the benchmark measures.
+        ring_f64: redraw the capture band's pixels in f64 (GEO_FLAG_RING_F64:
+        direct mode, the level-0 sampler, not as a composited sphere)."""
         ctx = Context(ctx) if isinstance(ctx, int) else ctx
         self.ctx = ctx
         self.mipmaps = mipmaps
+        self.ring_f64 = ring_f64
         self.sphere_radius = sphere_radius
         self.schwarz_radius = schwarz_radius
         self.max_iter = max_iter
@@ -390,7 +393,8 @@ class BasicSphereBuffer:
         if self.radial_position is None:
             raise RuntimeError("update_ray_fan must be called before draw")
         return make_scene(self.schwarz_radius, self.sphere_radius, self.radial_position, self.step, self.max_iter,
-                          self.mode, flags=_lib.GEO_FLAG_MIPS if self.mipmaps else 0)
+                          self.mode, flags=(_lib.GEO_FLAG_MIPS if self.mipmaps else 0) |
+                          (_lib.GEO_FLAG_RING_F64 if self.ring_f64 else 0))
 
     def draw(self, frame: GeoFrame, target: RenderTarget, row0: int = 0, nrows: int | None = None,
              stream=None, composite: bool = False) -> None:

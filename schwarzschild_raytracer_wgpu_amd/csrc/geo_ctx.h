@@ -108,6 +108,7 @@ struct geo_ctx {
     size_t ring_cap;
     uint32_t* ring_count;  // a pair (ring_parity: this render's)
     int ring_parity;
+    bool ring_open;  // a fork not yet followed by its scatter
     hipEvent_t ring_fork, ring_join, ring_free;
     hipStream_t ring_free_stream;  // the stream of the last scatter
     bool ring_free_rec;

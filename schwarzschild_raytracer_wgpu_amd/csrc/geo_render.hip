@@ -1642,6 +1642,10 @@ static int ring_fork(geo_ctx* c, const RenderArgs& a, const FrameK& fk, const ge
         return GEO_EHIP;
     if (c->ring_free_rec && c->ring_free_stream != s && hipStreamWaitEvent(rs_, c->ring_free, 0) != hipSuccess)
         return GEO_EHIP;
+    // a render that failed between its fork and its scatter left its counter
+    // unread and not flipped: start this one from zero
+    if (c->ring_open && hipMemsetAsync(r.count, 0, sizeof(uint32_t), rs_) != hipSuccess) return GEO_EHIP;
+    c->ring_open = true;
     const uint32_t gy = r.tiles_y < kMaxGridY ? r.tiles_y : kMaxGridY;
     hipLaunchKernelGGL(geo_ring_scan, dim3((a.width + 15u) / 16u, gy), dim3(256), 0, rs_, r);
     hipLaunchKernelGGL(geo_ring_kernel, dim3(kRingBlocks), dim3(kRingThreads), 0, rs_, r);
@@ -1874,6 +1878,7 @@ static int render_impl(geo_ctx* c, const geo_frame* frames, uint32_t nframes, si
         c->ring_free_rec = true;
         c->ring_free_stream = s;
         c->ring_parity = 1 - c->ring_parity;
+        c->ring_open = false;
     }
     if (record) {
         // rebuild the order into the buffer not in use, on the context's

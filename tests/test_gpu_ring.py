@@ -233,3 +233,42 @@ def test_ring_rejects_what_it_does_not_draw(geo, torch_mod):
         assert rows(_ring(geo, s)) == _lib.GEO_OK
     torch.cuda.synchronize()
     ctx.close()
+
+
+def test_ring_across_streams_and_sizes(geo, torch_mod):
+    """The redraw's lists are shared by the context's renders: frames on two
+    streams in turn (the scatter of one and the band test of the next meet
+    through ring_free), and a larger frame after a smaller one (the lists
+    grow), each equal to the same frame drawn alone."""
+    from schwarzschild_raytracer_wgpu_amd.scenes import make_sky
+
+    torch = torch_mod
+    dev = torch.device("cuda:0")
+    ctx = geo.Context(0)
+    ctx.set_sky(make_sky("equirect", (256, 128)))
+    scene = _ring(geo, default_scene(2048))
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    sizes = [(160, 90), (320, 180), (480, 270)]
+    cams = [(math.pi + 0.1 * i, 0.05 * i) for i in range(6)]
+    refs = {}
+    ref_ctx = geo.Context(0)
+    ref_ctx.set_sky(make_sky("equirect", (256, 128)))
+    for w, h in sizes:
+        for i, cam in enumerate(cams):
+            out = torch.empty(h * w * 4, dtype=torch.uint8, device=dev)
+            ref_ctx.render_rows(default_frame(w, h, camera=cam), scene, w, h, 0, h, out)
+            refs[(w, h, i)] = out
+    torch.cuda.synchronize()
+    outs = {}
+    for w, h in sizes:
+        for i, cam in enumerate(cams):
+            st = s1 if i % 2 == 0 else s2
+            out = torch.empty(h * w * 4, dtype=torch.uint8, device=dev)
+            with torch.cuda.stream(st):
+                ctx.render_rows(default_frame(w, h, camera=cam), scene, w, h, 0, h, out, stream=st.cuda_stream)
+            outs[(w, h, i)] = (out, st)
+    torch.cuda.synchronize()
+    for k, (out, _) in outs.items():
+        assert torch.equal(out, refs[k]), k
+    ctx.close()
+    ref_ctx.close()

@@ -95,7 +95,9 @@ typedef enum geo_status {
                                    (RGBA, mask, UV, per-pixel steps) after both.  There
                                    the orbit amplifies the f32 roundings past the 1e-4 UV
                                    bar.  steps_total keeps counting the f32
-                                   draw's steps.  Not with GEO_FLAG_COMPOSITE,
+                                   draw's steps.  The context keeps 36 bytes per
+                                   pixel of its largest such render (the band's
+                                   lists).  Not with GEO_FLAG_COMPOSITE,
                                    GEO_FLAG_MIPS, more than one frame or 2^31 pixels
                                    (GEO_EINVAL). */
 #define GEO_RING_X 8e-3f

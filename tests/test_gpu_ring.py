@@ -13,6 +13,7 @@ one level where the UV differ.  Against the f64 literal on whole config
 frames: every pixel inside north_star's bar, the capture band included.
 """
 import math
+import os
 
 import numpy as np
 import pytest
@@ -113,7 +114,9 @@ def test_ring_fuzz_scenes_against_the_oracle(geo, torch_mod):
     ctx.set_sky(sky)
     seen = 0
     steps_differ = 0
-    for seed in range(40_000, 40_300):
+    n = int(os.environ.get("GEO_FUZZ_N", 300))
+    base = int(os.environ.get("GEO_FUZZ_BASE", 40_000))
+    for seed in range(base, base + n):
         frame, scene, desc = random_scene(seed, w, h)
         scene = _ring(geo, scene)
         hip = _render(geo, torch_mod, ctx, frame, scene, w, h)
@@ -122,8 +125,8 @@ def test_ring_fuzz_scenes_against_the_oracle(geo, torch_mod):
         seen += int(band.any())
         st = _compare(hip, ref, band)
         steps_differ += st["steps_differ"]
-    print(f"ring fuzz: 300 scenes, {seen} with band pixels, {steps_differ} band steps differ")
-    assert seen > 30
+    print(f"fuzz ring: {n} scenes, {seen} with band pixels, {steps_differ} band steps differ")
+    assert seen > n // 10
     ctx.close()
 
 

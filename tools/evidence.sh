@@ -23,7 +23,7 @@
 #   timeline[:cases] tools/wave_timeline.py: every wave's span in a launch (diagnostic build)
 #   ab:<cfgs>[:reps] interleaved A/B of LIBS="a.so b.so" and/or ABARGS="args;args" (bench lines;
 #                    configs comma-separated; replaces the round-5 fpl_ab.sh / batch_ab.sh)
-#   fuzz[:n[:base]]  long GPU fuzz sweeps (direct, adversarial, fan, mips, batched launches) on new seeds
+#   fuzz[:n[:base]]  long GPU fuzz sweeps (direct, adversarial, fan, mips, batched launches, ring f64) on new seeds
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOT=$(pwd)
@@ -173,8 +173,8 @@ print('%-14s %-44s %-28s rep%s  ms/frame %.5f  kernel %.5f  frac %.4f  frame_che
     fuzz)
       # long GPU fuzz sweeps on seeds beyond the committed ones: fuzz:<n>:<base>
       for t in test_gpu_fuzz_bitexact test_gpu_fuzz_adversarial_bitexact test_gpu_fuzz_fan_mode_bitexact \
-               test_gpu_fuzz_mips_bitexact test_gpu_fuzz_batch_bitexact; do
-        GEO_FUZZ_N=${a1:-2000} GEO_FUZZ_BASE=${a2:-500000} timeout -k 10 900 python -u -m pytest tests/test_gpu_fuzz.py \
+               test_gpu_fuzz_mips_bitexact test_gpu_fuzz_batch_bitexact test_ring_fuzz_scenes_against_the_oracle; do
+        GEO_FUZZ_N=${a1:-2000} GEO_FUZZ_BASE=${a2:-500000} timeout -k 10 900 python -u -m pytest tests/test_gpu_fuzz.py tests/test_gpu_ring.py \
           -m gpu -q -s -k "$t" --timeout 850 --timeout-method thread > "$OUT/fuzz_$t.txt" 2>&1
         rc=$?; grep -h "^fuzz" "$OUT/fuzz_$t.txt"; tail -1 "$OUT/fuzz_$t.txt"; [ $rc -eq 0 ] || exit $rc
       done ;;

@@ -1588,6 +1588,8 @@ static int ensure_ring(geo_ctx* c, size_t n) {
     }
     if (c->ring_cap >= n) return GEO_OK;
     if (c->ring_free_rec && hipEventSynchronize(c->ring_free) != hipSuccess) return GEO_EHIP;
+    // a fork whose render failed before its scatter: its redraw may still run
+    if (c->ring_open && hipEventSynchronize(c->ring_join) != hipSuccess) return GEO_EHIP;
     if (c->ring_list) (void)hipFree(c->ring_list);
     if (c->ring_pix) (void)hipFree(c->ring_pix);
     c->ring_list = c->ring_pix = nullptr;

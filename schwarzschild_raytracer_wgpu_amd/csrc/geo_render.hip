@@ -1206,6 +1206,9 @@ int geo_ctx_create(int device, geo_ctx** out) {
 static int wait_renders(geo_ctx* c) {
     for (int i = 0; i < c->n_render_streams; ++i)
         if (hipEventSynchronize(c->render_done[i]) != hipSuccess) return GEO_EHIP;
+    // a ring redraw whose render failed before its scatter (which `done`
+    // would have covered) may still read the sky
+    if (c->ring_open && hipEventSynchronize(c->ring_join) != hipSuccess) return GEO_EHIP;
     return GEO_OK;
 }
 

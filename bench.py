@@ -334,8 +334,9 @@ def main():
     tol = cfg.tol if mode == g.GEO_MODE_ADAPTIVE else 0.0
     sampler_flags = g._lib.GEO_FLAG_MIPS if args.mips else 0
     if args.ring_f64:
-        if mode != g.GEO_MODE_DIRECT or args.mips or world > 1 or args.frames_per_launch > 1:
-            raise SystemExit("--ring-f64: direct mode, level-0 sampler, N = 1, one frame per launch (geo.h)")
+        if mode != g.GEO_MODE_DIRECT or args.mips or world > 1 or args.frames_per_launch > 1 or args.share:
+            raise SystemExit("--ring-f64: direct mode, level-0 sampler, N = 1, one frame per launch, no --share "
+                             "(geo.h)")
         sampler_flags |= g._lib.GEO_FLAG_RING_F64
     scene = g.make_scene(cfg.rs, cfg.sphere_r, obs.get_radial_position(), cfg.step, cfg.max_steps, mode,
                          flags=sampler_flags, tol=tol)

@@ -36,6 +36,33 @@ def test_spec_vs_f64_literal_config_rows(cfgname, row_step):
     assert st["band_pixels"] <= 0.01 * st["pixels"]
 
 
+def test_config2_every_pixel_against_the_f64_literal():
+    """Config 2's whole frame (every row, not a sample): the bar outside the
+    model's band, the model's bound inside it; and with GEO_FLAG_RING_F64 no
+    pixel over the bar at all, no mask flip (tools/f64_full_frame.py,
+    profiles/r05p_f64_full_frame*.json)."""
+    from schwarzschild_raytracer_wgpu_amd import GeoScene
+    from schwarzschild_raytracer_wgpu_amd._lib import GEO_FLAG_RING_F64
+
+    cfg = CONFIGS["cfg2_1080p"]
+    w, h = cfg.width, cfg.height
+    frame = _frame(cfg)
+    scene = default_scene(cfg.max_steps)
+    sky = make_sky("equirect", (64, 32))
+    ref = B.f64_rows(frame, scene, w, h, 0, h, 1, threads=8)
+    p = O.render_f32(frame, scene, sky, w, h, threads=8)
+    st = B.compare(p["mask"], p["uv"], ref, cfg.rs, R_OBS)
+    assert st["mask_flips"] == 0 and st["uv_over_bar_outside_band"] == 0, st
+    assert st["in_band_over_model"] == 0, st
+    assert st["uv_max_all"] > B.UV_BAR  # the f32 draw has pixels over the bar next to the orbit
+    ring = GeoScene.from_buffer_copy(bytes(scene))
+    ring.flags |= GEO_FLAG_RING_F64
+    q = O.render_f32(frame, ring, sky, w, h, threads=8)
+    sky_px = (q["mask"] == 0) & (ref["mask"] == 0)
+    assert np.array_equal(q["mask"], ref["mask"])
+    assert B.uv_err(q["uv"], ref["uv"])[sky_px].max() <= B.UV_BAR
+
+
 SWEEP = [(math.pi, 0.0), (math.pi + 0.5, 0.4), (math.pi - 1.0, -0.7), (0.3, 0.2), (math.pi, 1.3)]
 
 

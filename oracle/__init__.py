@@ -90,6 +90,7 @@ def _load() -> ctypes.CDLL:
                                            vp]),
         "geo_oracle_ring_kx": (ctypes.c_float, [vp]),
         "geo_oracle_ring_band": (i, [vp, vp, u32, u32, u32, u32, u32, vp]),
+        "geo_oracle_ring_x": (i, [vp, vp, u32, u32, u32, u32, u32, vp]),
     }
     for n, (r, a) in sig.items():
         fn = getattr(lib, n)
@@ -196,6 +197,18 @@ def ring_band(frame, scene, width, height, row0=0, nrows=None, row_step=1):
     if rc != 0:
         raise ValueError(f"geo_oracle_ring_band: {rc}")
     return band
+
+
+def ring_x(frame, scene, width, height, row0=0, nrows=None, row_step=1):
+    """|kx cos(theta) - 1| of each pixel's f32 ray (GEO_FLAG_RING_F64's band
+    test quantity) on rows row0 + i row_step."""
+    nrows = (height - row0 + row_step - 1) // row_step if nrows is None else nrows
+    x = np.empty((nrows, width), np.float32)
+    fr, sc = as_frame(frame), as_scene(scene)
+    rc = lib.geo_oracle_ring_x(_addr(fr), _addr(sc), width, height, row0, nrows, row_step, _np(x))
+    if rc != 0:
+        raise ValueError(f"geo_oracle_ring_x: {rc}")
+    return x
 
 
 def render_f32(frame, scene, sky, width, height, row0=0, nrows=None, row_step=1, fan=None, threads=8,

@@ -744,6 +744,23 @@ static int ring_applies(const geo_scene* s) {
 /* the band test on the f32 ray's cos(theta) */
 static int in_ring(float kx, float ct) { return fabsf(kx * ct - 1.0f) < GEO_RING_X; }
 
+/* |kx cos(theta) - 1| of every pixel's f32 ray on rows row0 + i row_step
+ * (the band test's quantity; the scene's kx whatever its flags). */
+int geo_oracle_ring_x(const geo_frame* f, const geo_scene* s, uint32_t width, uint32_t height, uint32_t row0,
+                      uint32_t nrows, uint32_t row_step, float* x) {
+    if (!f || !s || !x || width == 0 || height == 0 || row_step == 0) return -1;
+    if ((uint64_t)row0 + (uint64_t)(nrows ? nrows - 1 : 0) * row_step >= height) return -1;
+    float kx = geo_oracle_ring_kx(s);
+    cam_f32 cam = camera_f32(f, width, height);
+    for (uint32_t r = 0; r < nrows; ++r)
+        for (uint32_t px = 0; px < width; ++px) {
+            float c2[3];
+            camera_c2(f, &cam, px, row0 + r * row_step, c2);
+            x[(size_t)r * width + px] = fabsf(kx * sqrtf(fmaf(c2[1], c2[1], c2[0] * c2[0])) - 1.0f);
+        }
+    return 0;
+}
+
 int geo_oracle_ring_band(const geo_frame* f, const geo_scene* s, uint32_t width, uint32_t height, uint32_t row0,
                          uint32_t nrows, uint32_t row_step, uint8_t* band) {
     if (!f || !s || !band || width == 0 || height == 0 || row_step == 0) return -1;

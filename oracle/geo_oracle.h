@@ -82,6 +82,8 @@ int geo_oracle_render_f32(const geo_frame* f, const geo_scene* s, const float* f
 float geo_oracle_ring_kx(const geo_scene* s);
 int geo_oracle_ring_band(const geo_frame* f, const geo_scene* s, uint32_t width, uint32_t height, uint32_t row0,
                          uint32_t nrows, uint32_t row_step, uint8_t* band);
+int geo_oracle_ring_x(const geo_frame* f, const geo_scene* s, uint32_t width, uint32_t height, uint32_t row0,
+                      uint32_t nrows, uint32_t row_step, float* x);
 
 /* GEO_FLAG_MIPS mirror (geo_pixel.h): the 4-level box-filtered mip chain
  * (levels one after another, geo_oracle_mip_chain_texels(w, h) texels), and

@@ -881,8 +881,8 @@ struct RingEntry {
 struct RingArgs {
     FrameK f;
     uint32_t width, height, row0, nrows, band_rows, band_magic, band_stride;
-    uint32_t tiles_y;  // 16-row blocks of the launch's rows
     float kx;          // r_obs / (sqrt(1 - rs/r_obs) 3 sqrt(3)/2 rs), rounded once (geo_oracle_ring_kx)
+    float skip_slack;  // geo_ring_scan: a tile whose centre's test exceeds GEO_RING_X by this holds no band pixel
     double rs, sphere_r, r_obs, step;
     uint32_t max_steps;
     const uint32_t* sky;
@@ -1031,43 +1031,78 @@ __device__ void ring_pixel_f64(const RingArgs& a, uint32_t px, uint32_t py, doub
     (void)PI;
 }
 
-// The band test, kRingScanRows pixels per lane (a column of them 16 rows
-// apart: 16 x 256 pixels per workgroup, few long waves, as the wave launch
-// rate bounds a grid of short ones; geo_render_kernel's band mapping): the
-// band's pixels go to a dense list, a wave's pixels of one row with one
-// atomic (the lanes' ranks in its ballot).
-constexpr uint32_t kRingScanRows = 16;
-__global__ __launch_bounds__(256) void geo_ring_scan(const RingArgs a) {
+// The band test on the f32 ray of one pixel (the oracle's in_ring): its
+// cos(theta) by the f32 draw's own camera ray.
+__device__ __forceinline__ float ring_x(const RingArgs& a, uint32_t px, uint32_t py) {
+    float c2x, c2y, c2z;
+    geo::pixel_central_dir(a.f.cam, a.f.frame.movement_to_central, a.f.frame.psi_factor_and_position[0], a.f.kt, px,
+                           py, &c2x, &c2y, &c2z);
+    return fabsf(a.kx * geo::central_rho(c2x, c2y) - 1.0f);
+}
+
+// The band test.  One wave per kRingScanTiles^2 tiles of 8 x 8 pixels: lane
+// t first tests tile t's centre pixel against the band widened by
+// a.skip_slack, the most the test's |kx cos(theta) - 1| can change within 4
+// pixels of it (ring_fork: a Lipschitz bound on the ray's direction over the
+// frame, so no band pixel is ever in a skipped tile); then the wave tests
+// every pixel of the tiles that may hold band pixels, one tile per pass
+// (few tiles per wave: the passes are a chain of camera rays), and lists the
+// band's pixels (one atomic per wave; each pixel's slot from its rank in its
+// tile's ballot).  A tile's 8 rows lie in one band of the launch's band
+// layout (band heights are multiples of 8), so its frame rows are
+// consecutive.
+constexpr uint32_t kRingScanTiles = 4;
+__global__ __launch_bounds__(64) void geo_ring_scan(const RingArgs a) {
     __builtin_amdgcn_s_setprio(2);  // beside the f32 draw (ring_fork): it gates the f64 redraw
-    const uint32_t lane = threadIdx.x & 63u;
-    for (uint32_t by = blockIdx.y; by < a.tiles_y; by += gridDim.y) {
-        const uint32_t px = blockIdx.x * 16u + (threadIdx.x & 15u);
-        for (uint32_t k = 0; k < kRingScanRows; ++k) {
-            const uint32_t lr = by * (16u * kRingScanRows) + k * 16u + (threadIdx.x >> 4);
-            bool in = px < a.width && lr < a.nrows;
-            uint32_t py = 0;
-            if (in) {
-                const uint32_t band = __umulhi(lr, a.band_magic);
-                py = a.row0 + band * a.band_stride + (lr - band * a.band_rows);
-                in = py < a.height;
-            }
-            bool ring = false;
-            if (in) {
-                float c2x, c2y, c2z;
-                geo::pixel_central_dir(a.f.cam, a.f.frame.movement_to_central, a.f.frame.psi_factor_and_position[0],
-                                       a.f.kt, px, py, &c2x, &c2y, &c2z);
-                const float ct = geo::central_rho(c2x, c2y);
-                ring = fabsf(a.kx * ct - 1.0f) < GEO_RING_X;
-            }
-            const uint64_t m = __ballot(ring);
-            if (m == 0) continue;
-            const uint32_t first = (uint32_t)__ffsll((unsigned long long)m) - 1u;
-            uint32_t base = 0;
-            if (lane == first) base = atomicAdd(a.count, (uint32_t)__popcll(m));
-            base = (uint32_t)__shfl((int)base, (int)first);
-            const uint32_t slot = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-            if (ring && slot < a.cap) a.pix[slot] = RingPixel{px, lr, py};
+    constexpr uint32_t T = kRingScanTiles;
+    const uint32_t lane = threadIdx.x;
+    const uint32_t tx0 = blockIdx.x * T, ty0 = blockIdx.y * T;  // in 8-pixel tiles
+    auto frame_row = [&](uint32_t lr) {
+        const uint32_t band = __umulhi(lr, a.band_magic);
+        return a.row0 + band * a.band_stride + (lr - band * a.band_rows);
+    };
+    bool may = false;
+    if (lane < T * T) {
+        const uint32_t tx = tx0 + lane % T, ty = ty0 + lane / T;
+        if (tx * 8u < a.width && ty * 8u < a.nrows) {
+            const float x = ring_x(a, tx * 8u + 4u, frame_row(ty * 8u + 4u));
+            may = !(x >= GEO_RING_X + a.skip_slack);  // NaN: tested pixel by pixel
         }
+    }
+    // pass 1: each candidate tile's band pixels as a ballot (kept in LDS),
+    // and their count; one atomic reserves the wave's entries; pass 2: the
+    // entries
+    const uint64_t cand = __ballot(may);
+    __shared__ uint64_t masks[T * T];
+    uint32_t total = 0;
+    for (uint64_t tiles = cand; tiles != 0; tiles &= tiles - 1ull) {
+        const uint32_t t = (uint32_t)__ffsll((unsigned long long)tiles) - 1u;
+        const uint32_t px = (tx0 + t % T) * 8u + (lane & 7u);
+        const uint32_t lr = (ty0 + t / T) * 8u + (lane >> 3);
+        bool ring = false;
+        if (px < a.width && lr < a.nrows) {
+            const uint32_t py = frame_row(lr);
+            ring = py < a.height && ring_x(a, px, py) < GEO_RING_X;
+        }
+        const uint64_t m = __ballot(ring);
+        if (lane == 0) masks[t] = m;
+        total += (uint32_t)__popcll(m);
+    }
+    if (total == 0) return;
+    __syncthreads();
+    uint32_t base = 0;
+    if (lane == 0) base = atomicAdd(a.count, total);
+    base = (uint32_t)__shfl((int)base, 0);
+    for (uint64_t tiles = cand; tiles != 0; tiles &= tiles - 1ull) {
+        const uint32_t t = (uint32_t)__ffsll((unsigned long long)tiles) - 1u;
+        const uint64_t m = masks[t];
+        if ((m >> lane) & 1ull) {
+            const uint32_t px = (tx0 + t % T) * 8u + (lane & 7u);
+            const uint32_t lr = (ty0 + t / T) * 8u + (lane >> 3);
+            const uint32_t slot = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+            if (slot < a.cap) a.pix[slot] = RingPixel{px, lr, frame_row(lr)};
+        }
+        base += (uint32_t)__popcll(m);
     }
 }
 
@@ -1621,9 +1656,34 @@ static int ring_fork(geo_ctx* c, const RenderArgs& a, const FrameK& fk, const ge
     r.band_rows = a.band_rows;
     r.band_magic = a.band_magic;
     r.band_stride = a.band_stride;
-    r.tiles_y = (a.nrows + 16u * kRingScanRows - 1u) / (16u * kRingScanRows);
     const double rs = (double)sc.rs, ro = (double)sc.r_obs;
     r.kx = (float)(ro / (std::sqrt(1.0 - rs / ro) * (1.5 * std::sqrt(3.0) * rs)));  // geo_oracle_ring_kx
+    // geo_ring_scan's tile skip.  A pixel within 4 of a tile's centre (in x
+    // and y) has the unnormalised ray d = py a + px b + c within
+    // D = 4(|a| + |b|) of the centre's, and every d lies on the plane
+    // through c spanned by a and b, at least dist = |(a x b).c| / |a x b|
+    // from the origin: the two directions are at most asin(D / dist) apart
+    // (D < dist).  The aberration (a boost by psi_k) stretches angles by at
+    // most sqrt((1 + |k|)/(1 - |k|)), the rotation to the central frame not
+    // at all, and cos(theta) = |sin(polar angle)| moves by at most the
+    // angle; so |kx cos(theta) - 1| moves by at most kx times that (1 %
+    // more, plus 1e-4 for the f32 roundings).  No bound (a degenerate
+    // camera): every tile is tested pixel by pixel.
+    {
+        const geo::CameraConsts& cc = fk.cam;
+        const double A[3] = {cc.a[0], cc.a[1], cc.a[2]}, B[3] = {cc.b[0], cc.b[1], cc.b[2]},
+                     C[3] = {cc.c[0], cc.c[1], cc.c[2]};
+        const double n[3] = {A[1] * B[2] - A[2] * B[1], A[2] * B[0] - A[0] * B[2], A[0] * B[1] - A[1] * B[0]};
+        const double nn = std::sqrt(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]);
+        const double dist = nn > 0.0 ? std::fabs(n[0] * C[0] + n[1] * C[1] + n[2] * C[2]) / nn : 0.0;
+        const double D = 4.0 * (std::sqrt(A[0] * A[0] + A[1] * A[1] + A[2] * A[2]) +
+                                std::sqrt(B[0] * B[0] + B[1] * B[1] + B[2] * B[2]));
+        const double k = std::fabs((double)fk.frame.psi_factor_and_position[0]);
+        double slack = HUGE_VAL;
+        if (dist > 0.0 && D < dist && k < 1.0)
+            slack = (double)r.kx * std::sqrt((1.0 + k) / (1.0 - k)) * std::asin(D / dist) * 1.01 + 1e-4;
+        r.skip_slack = std::isfinite(slack) ? (float)slack : HUGE_VALF;
+    }
     r.rs = rs;
     r.sphere_r = (double)sc.sphere_r;
     r.r_obs = ro;
@@ -1639,20 +1699,22 @@ static int ring_fork(geo_ctx* c, const RenderArgs& a, const FrameK& fk, const ge
     r.list = static_cast<RingEntry*>(c->ring_list);
     r.count = c->ring_count + c->ring_parity;  // zeroed by the previous scatter (or at allocation)
     r.cap = (uint32_t)((size_t)a.nrows * a.width);
-    // the band test and the f64 redraw on the ring stream, beside the f32
-    // draw: after the caller's stream so far, and after the previous
-    // scatter (which read the lists) if that ran on another stream
+    // the band test and the f64 redraw on the ring stream, forked before the
+    // f32 draw and running beside it: after the caller's stream so far, and
+    // after the previous scatter (which read the lists) if that ran on
+    // another stream.  A render that failed between its fork and its
+    // scatter left its counter unread and not flipped: this one starts it
+    // from zero.
     hipStream_t rs_ = c->ring_stream;
     if (hipEventRecord(c->ring_fork, s) != hipSuccess || hipStreamWaitEvent(rs_, c->ring_fork, 0) != hipSuccess)
         return GEO_EHIP;
     if (c->ring_free_rec && c->ring_free_stream != s && hipStreamWaitEvent(rs_, c->ring_free, 0) != hipSuccess)
         return GEO_EHIP;
-    // a render that failed between its fork and its scatter left its counter
-    // unread and not flipped: start this one from zero
     if (c->ring_open && hipMemsetAsync(r.count, 0, sizeof(uint32_t), rs_) != hipSuccess) return GEO_EHIP;
     c->ring_open = true;
-    const uint32_t gy = r.tiles_y < kMaxGridY ? r.tiles_y : kMaxGridY;
-    hipLaunchKernelGGL(geo_ring_scan, dim3((a.width + 15u) / 16u, gy), dim3(256), 0, rs_, r);
+    const uint32_t scan_px = 8u * kRingScanTiles;
+    hipLaunchKernelGGL(geo_ring_scan, dim3((a.width + scan_px - 1u) / scan_px, (a.nrows + scan_px - 1u) / scan_px),
+                       dim3(64), 0, rs_, r);
     hipLaunchKernelGGL(geo_ring_kernel, dim3(kRingBlocks), dim3(kRingThreads), 0, rs_, r);
     if (hipGetLastError() != hipSuccess) return GEO_EHIP;
     if (hipEventRecord(c->ring_join, rs_) != hipSuccess) return GEO_EHIP;

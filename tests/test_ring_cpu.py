@@ -82,7 +82,8 @@ def _skip_slack(frame, scene, w, h):
     dist = abs(float(n @ C)) / nn if nn > 0 else 0.0
     D = 4.0 * (float(np.linalg.norm(A)) + float(np.linalg.norm(B)))
     k = abs(float(f[48]))
-    kx = float(O.lib.geo_oracle_ring_kx(O._addr(O.as_scene(scene))))
+    sc = O.as_scene(scene)  # alive across the call
+    kx = float(O.lib.geo_oracle_ring_kx(O._addr(sc)))
     if not (dist > 0 and D < dist and k < 1):
         return math.inf
     return kx * math.sqrt((1 + k) / (1 - k)) * math.asin(D / dist) * 1.01 + 1e-4

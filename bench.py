@@ -101,8 +101,10 @@ def parse():
                    help="sample the sky through its mip chain (GEO_FLAG_MIPS, the reference's textureSample); "
                         "the metric's line is the level-0 path")
     p.add_argument("--ring-f64", action="store_true",
-                   help="GEO_FLAG_RING_F64: redraw the capture band's pixels in f64 beside the f32 draw (N = 1, "
-                        "direct mode, one frame per launch; off on the metric's line)")
+                   help="GEO_FLAG_RING_F64 on every frame: the capture band's lanes integrate in f64 inside the "
+                        "render kernel (N = 1, direct or adaptive mode, one frame per launch).  Without it an N = 1 "
+                        "direct/adaptive line still measures the mode beside the metric, as its `ring_f64` record")
+    p.add_argument("--no-ring-record", action="store_true", help="skip the `ring_f64` record")
     p.add_argument("--no-frame-check", action="store_true",
                    help="skip rank 0's check, after the timed region, that every frame of the timed run's last "
                         "batch (the frames as assembled for present) equals a single-launch render of the frame; "
@@ -334,9 +336,9 @@ def main():
     tol = cfg.tol if mode == g.GEO_MODE_ADAPTIVE else 0.0
     sampler_flags = g._lib.GEO_FLAG_MIPS if args.mips else 0
     if args.ring_f64:
-        if mode != g.GEO_MODE_DIRECT or args.mips or world > 1 or args.frames_per_launch > 1 or args.share:
-            raise SystemExit("--ring-f64: direct mode, level-0 sampler, N = 1, one frame per launch, no --share "
-                             "(geo.h)")
+        if mode == g.GEO_MODE_FAN or args.mips or world > 1 or args.frames_per_launch > 1 or args.share:
+            raise SystemExit("--ring-f64: direct or adaptive mode, level-0 sampler, N = 1, one frame per launch, "
+                         "no --share (geo.h)")
         sampler_flags |= g._lib.GEO_FLAG_RING_F64
     scene = g.make_scene(cfg.rs, cfg.sphere_r, obs.get_radial_position(), cfg.step, cfg.max_steps, mode,
                          flags=sampler_flags, tol=tol)
@@ -785,17 +787,20 @@ def main():
         fan = None
         if mode == g.GEO_MODE_FAN:  # the fan the draws read, as the host's copy
             fan = ctx.solve_ray_fan(cfg.sphere_r, cfg.rs, cfg.max_steps, cfg.step, 400, obs.get_radial_position())
-        # (with --ring-f64 the CPU path is the f32 draw's, compared with the f32 draw)
-        cpu_scene = scene
-        if args.ring_f64:
-            cpu_scene = g.GeoScene.from_buffer_copy(bytes(scene))
-            cpu_scene.flags &= ~g._lib.GEO_FLAG_RING_F64
-        out["cpu_baseline"] = cpu_baseline(frame, cpu_scene, sky, W, H, args, ctx, fan)
+        # (with --ring-f64 the CPU path draws the band in f64 too: geo_band.h on the host)
+        out["cpu_baseline"] = cpu_baseline(frame, scene, sky, W, H, args, ctx, fan)
         cpu_ok = out["cpu_baseline"]["matches_gpu"]["ok"]
         if mode != g.GEO_MODE_FAN:
             out["reference_equivalent"] = reference_fan_cost(ctx, cfg, obs.get_radial_position())
     out["frame_check"] = frame_check
+    ring_ok = True
+    if (world == 1 and mode != g.GEO_MODE_FAN and not args.ring_f64 and not args.mips and not args.share
+            and args.motion == "none" and not args.no_ring_record and cfg.rs > 0.0):
+        out["ring_f64"] = ring_record(g, ctx, frame, scene, sky, W, H, args, flops_of, dev)
+        ring_ok = out["ring_f64"]["matches_cpu"]["ok"]
     print(json.dumps(out), flush=True)
+    if not ring_ok:
+        raise SystemExit("ring_f64: the GPU's band rows differ from the CPU path's (matches_cpu)")
     if not cpu_ok:
         raise SystemExit("cpu_baseline: the CPU path's rows differ from the GPU frame's (matches_gpu)")
     if world > 1:
@@ -1167,6 +1172,124 @@ def cpu_baseline(frame, scene, sky, W, H, args, ctx, fan=None):
         },
         "implementation": "geo_render_cpu (libgeo_cpu.so): geo_pixel.h compiled for the host, g++ -O2 "
                           "-ffp-contract=off -mfma -msse4.1, scalar, std::thread row blocks",
+    }
+
+
+def ring_record(g, ctx, frame, scene, sky, W, H, args, flops_of, dev):
+    """GEO_FLAG_RING_F64 beside the metric's line (geo.h): the
+    same frame with the capture band's lanes integrated in f64 inside the
+    render kernel, the mode that meets north_star's UV bar against the
+    reference's own f64 arithmetic on every pixel.  Plain and ring frames are
+    timed interleaved (3 x K frames each, one launch per frame, one stream,
+    the learned dispatch order of each), each launch's kernel by an event
+    pair on its dispatch; then the GPU's rows through the band against the
+    CPU path's (geo_render_cpu: geo_band.h on the host)."""
+    import ctypes
+
+    import numpy as np
+    import torch
+
+    from schwarzschild_raytracer_wgpu_amd.timing import HipEvent
+
+    def flagged(flags):
+        sc = g.GeoScene.from_buffer_copy(bytes(scene))
+        sc.flags = (scene.flags | flags) & ~g._lib.GEO_FLAG_DEFER_STEPS
+        return sc
+
+    ring = flagged(g._lib.GEO_FLAG_RING_F64)
+    plain_d = flagged(g._lib.GEO_FLAG_DEFER_STEPS)
+    ring_d = flagged(g._lib.GEO_FLAG_RING_F64 | g._lib.GEO_FLAG_DEFER_STEPS)
+    out = torch.empty(H * W * 4, dtype=torch.uint8, device=dev)
+    # the ring frame's steps and hits (the band's pixels report their f64 steps)
+    mask = torch.empty(H * W, dtype=torch.uint8, device=dev)
+    steps = torch.empty(H * W, dtype=torch.int32, device=dev)
+    total = torch.zeros(1, dtype=torch.int64, device=dev)
+    ctx.render_rows(frame, ring, W, H, 0, H, out, out_mask=mask, out_steps=steps, steps_total=total)
+    torch.cuda.synchronize()
+    hits = int(((mask == 0) & (steps > 0)).sum().item())
+    ring_steps = int(total.item())
+    flops = flops_of(ring_steps, hits)
+    del mask, steps
+    K = args.steps
+    ev = {i: (HipEvent(), HipEvent()) for i in range(0, K, max(1, args.event_every))}
+
+    def run(sc, n, events=None):
+        for i in range(n):
+            if events is not None and i in events:
+                ctx.time_next_render(*events[i])
+            ctx.render_rows(frame, sc, W, H, 0, H, out)
+
+    run(ring_d, 100)  # its order learned, the clock settled
+    run(plain_d, 100)
+    res = {"plain": [], "ring": [], "plain_k": [], "ring_k": []}
+    for rep in range(3):
+        for name, sc in (("plain", plain_d), ("ring", ring_d)):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            run(sc, K, ev)
+            torch.cuda.synchronize()
+            res[name].append((time.perf_counter() - t0) / K * 1e3)
+            res[name + "_k"].append(sum(a.elapsed_time(b) for a, b in ev.values()) / len(ev))
+    ctx.steps_flush(torch.zeros(1, dtype=torch.int64, device=dev))  # discard
+    plain_ms, ring_ms = min(res["plain"]), min(res["ring"])
+    ring_kms = sum(res["ring_k"]) / len(res["ring_k"])
+    plain_kms = sum(res["plain_k"]) / len(res["plain_k"])
+    # the comparator: the rows through the band's widest part, GPU vs CPU
+    lib = _cpu_lib()
+    rows = list(range(H // 2 - 8, H // 2 + 8))
+    n = len(rows)
+    sky_c = np.ascontiguousarray(sky, dtype=np.uint8)
+    c_rgba = np.empty((n, W, 4), np.uint8)
+    c_mask = np.empty((n, W), np.uint8)
+    c_uv = np.empty((n, W, 2), np.float32)
+    c_steps = np.empty((n, W), np.uint32)
+    tot = ctypes.c_ulonglong()
+    rc = lib.geo_render_cpu(ctypes.addressof(frame), ctypes.addressof(ring), sky_c.ctypes.data, sky_c.shape[1],
+                            sky_c.shape[0], None, 0, W, H, rows[0], n, 1, 16, c_rgba.ctypes.data, c_mask.ctypes.data,
+                            c_uv.ctypes.data, c_steps.ctypes.data, ctypes.addressof(tot))
+    if rc != 0:
+        raise SystemExit(f"geo_render_cpu (ring): {rc}")
+    g_rgba = torch.empty(H * W * 4, dtype=torch.uint8, device=dev)
+    g_mask = torch.empty(H * W, dtype=torch.uint8, device=dev)
+    g_uv = torch.empty(H * W * 2, dtype=torch.float32, device=dev)
+    g_steps = torch.empty(H * W, dtype=torch.int32, device=dev)
+    ctx.render_rows(frame, ring, W, H, 0, H, g_rgba, out_mask=g_mask, out_uv=g_uv, out_steps=g_steps)
+    torch.cuda.synchronize()
+    sl = slice(rows[0], rows[0] + n)
+    same = (np.array_equal(g_rgba.view(H, W, 4)[sl].cpu().numpy(), c_rgba)
+            and np.array_equal(g_mask.view(H, W)[sl].cpu().numpy(), c_mask)
+            and np.array_equal(g_uv.view(H, W, 2)[sl].cpu().numpy().view(np.uint32), c_uv.view(np.uint32))
+            and np.array_equal(g_steps.view(H, W)[sl].cpu().numpy().view(np.uint32), c_steps))
+    # the rows' band pixels: where the f64 path changed the steps or the UV
+    p_uv = torch.empty(H * W * 2, dtype=torch.float32, device=dev)
+    p_steps = torch.empty(H * W, dtype=torch.int32, device=dev)
+    plain = flagged(0)
+    ctx.render_rows(frame, plain, W, H, 0, H, out, out_uv=p_uv, out_steps=p_steps)
+    torch.cuda.synchronize()
+    changed = int(((g_steps != p_steps) | (g_uv.view(-1, 2) != p_uv.view(-1, 2)).any(dim=1)).sum().item())
+    achieved = flops / (ring_kms * 1e-3) / 1e12
+    return {
+        "ms_per_step": ring_ms,
+        "plain_ms_per_step": plain_ms,
+        "overhead": ring_ms / plain_ms - 1.0,
+        "kernel_ms": ring_kms,
+        "plain_kernel_ms": plain_kms,
+        "kernel_overhead": ring_kms / plain_kms - 1.0,
+        "value": ring_steps / (ring_ms * 1e-3),
+        "unit": "geodesic-steps·pixels/s" if scene.mode != 2 else "geodesic-step-attempts·pixels/s",
+        "roofline": {"achieved": achieved, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
+                     "frac": achieved / PEAK_FP32_TFLOPS, "algorithmic_flops_per_launch": flops,
+                     "what": "the ring frame's algorithmic flops (its band's steps are f64) over its kernel's "
+                             "event-timed duration (the whole frame is one launch: the f32 lanes and the f64 "
+                             "band's lanes in one kernel)"},
+        "reps": {k: [round(v, 5) for v in vals] for k, vals in res.items()},
+        "pixels_changed": changed,
+        "matches_cpu": {"ok": bool(same), "rows": [rows[0], rows[-1]],
+                        "what": "GPU rows vs geo_render_cpu's (geo_band.h on the host) through the band: RGBA, "
+                                "mask, UV bits, steps"},
+        "what": "GEO_FLAG_RING_F64: the capture band's lanes (|b/b_c - 1| < 8e-3 by the f32 ray) integrate in f64 "
+                "inside the render kernel; ms_per_step and plain_ms_per_step are the best of 3 interleaved "
+                "runs of K frames each (one launch per frame, one stream)",
     }
 
 

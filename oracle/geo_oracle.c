@@ -650,20 +650,148 @@ static void camera_c2(const geo_frame* f, const cam_f32* cam, uint32_t px, uint3
     }
 }
 
+/* GEO_FLAG_RING_F64 (geo.h; DESIGN.md §2 "The capture band in f64"): the
+ * traveled angle of a band pixel in f64, restated from the specification
+ * (the product's geo_band.h is not shared):
+ *   - the camera ray d = py a + px b + c with the frame constants of
+ *     camera_f32 in f64, not rounded, and the aberration as the f32 path's
+ *     z-boost (shader.wgsl:60-75), in f64;
+ *   - solve_ray_fan's node (sphere_ray_tracer.rs:38-49, r > rs) and
+ *     solve_geodesic's radial cases, pre-filters and initial slope
+ *     (:60-132) as written;
+ *   - the main loop (:134-191) one step at a time, on the scaled state
+ *     U = (3 rs/2) u with the 14-operation RK4 form,
+ *     the loop test, the crossing, the escape, Newton's three refinements;
+ * returns lambda' = pi/2 - angle; *steps = the RK4 steps taken. */
+static void band_rk4(double U, double V, double h, double hh, double hh2, double hhh, double h6, double h2_6,
+                     double* NU, double* NV) {
+    double fu = fma(U, U, -U);
+    double au = fma(hh, V, U);
+    double uh = fma(h, V, U);
+    double fa = fma(au, au, -au);
+    double bu = fma(hh2, fu, au);
+    double fb = fma(bu, bu, -bu);
+    double cu = fma(hhh, fa, uh);
+    double fc = fma(cu, cu, -cu);
+    double fab = fa + fb;
+    *NU = fma(h2_6, fu + fab, uh);
+    *NV = fma(h6, fma(2.0, fab, fu) + fc, V);
+}
+
+static double band_lambda(const geo_frame* f, const geo_scene* s, uint32_t width, uint32_t height, uint32_t px,
+                          uint32_t py, uint32_t* steps) {
+    const float* m0 = f->display_to_movement;
+    const float* m1 = f->movement_to_central;
+    double w = (double)width, hgt = (double)height;
+    double sx = 2.0 / w, ox = (1.0 - w) / w, sy = -2.0 / hgt, oy = (hgt - 1.0) / hgt;
+    double d[3];
+    for (int i = 0; i < 3; ++i) {
+        double p = -(double)m0[12] * (double)m0[i];
+        double q = -(double)m0[13] * (double)m0[4 + i];
+        double r_ = (double)m0[14] * (double)m0[8 + i];
+        double a = sy * p, b = sx * q, c = (oy * p + ox * q) + r_;
+        d[i] = fma((double)py, a, fma((double)px, b, c));
+    }
+    double k = (double)f->psi_factor_and_position[0];
+    double kt = sqrt(1.0 - k * k);
+    double len = sqrt(fma(d[2], d[2], fma(d[1], d[1], d[0] * d[0])));
+    double id = 1.0 / fma(-k, d[2], len);
+    double g = kt * id;
+    double e[3] = {d[0] * g, d[1] * g, fma(-k, len, d[2]) * id};
+    int ident = m1[0] == 1.0f && m1[1] == 0.0f && m1[2] == 0.0f && m1[4] == 0.0f && m1[5] == 1.0f &&
+                m1[6] == 0.0f && m1[8] == 0.0f && m1[9] == 0.0f && m1[10] == 1.0f;
+    double c2[3];
+    if (ident) {
+        c2[0] = e[0]; c2[1] = e[1]; c2[2] = e[2];
+    } else {
+        for (int i = 0; i < 3; ++i)
+            c2[i] = fma((double)m1[8 + i], e[2], fma((double)m1[4 + i], e[1], (double)m1[i] * e[0]));
+    }
+    double st = c2[2] > -1.0 ? (c2[2] < 1.0 ? c2[2] : 1.0) : -1.0;
+    double ct = sqrt(fma(c2[1], c2[1], c2[0] * c2[0]));
+    /* solve_ray_fan (:38-49), r > rs */
+    double schwarz_r = (double)s->rs, sphere_r = (double)s->sphere_r, r = (double)s->r_obs;
+    double rotation = r * ct;
+    int r_falling = st > 0.0;
+    double energy = sqrt(1. - schwarz_r / r);
+    /* solve_geodesic (:60-132) */
+    *steps = 0;
+    int sphere_outside = sphere_r > schwarz_r;
+    int inside_sphere = r < sphere_r;
+    double lam0 = O_FRAC_PI_2;
+    if (rotation < 1e-10) {
+        if (inside_sphere) return lam0 - (r_falling ? O_NO_VALUE : 0.);
+        return lam0 - ((sphere_outside && r_falling) ? 0. : O_NO_VALUE);
+    }
+    double b = rotation / energy;
+    int barrier_3r_2 = 1. / (b * b) < 4. / (27. * schwarz_r * schwarz_r);
+    double r3_2 = 3. * schwarz_r / 2.;
+    int different_sides_3r_2 = ((r < r3_2) ^ (sphere_r < r3_2)) && fabs(r - r3_2) > 1e-10;
+    if ((inside_sphere && !sphere_outside) || (barrier_3r_2 && different_sides_3r_2) ||
+        (r < r3_2 && inside_sphere && r_falling) || (r > r3_2 && !inside_sphere && !r_falling))
+        return lam0 - O_NO_VALUE;
+    double u_bar0 = (r_falling ? 1. : -1.) * sqrt(1. / (b * b) - (1. - schwarz_r / r) / (r * r));
+    /* the scaled state and thresholds (U = c u, c = 3 rs/2) */
+    double c = r3_2;
+    double u0 = 1. / r;
+    double U = c * u0, V = c * u_bar0;
+    double SU = c / sphere_r;
+    double BD = c * (0.9 * fmin(u0, 1. / fmax(sphere_r, r3_2)));
+    double HU = c / schwarz_r;
+    double h = (double)s->step;
+    double hh = h / 2., hh2 = h * h / 4., hhh = h * h / 2., h6 = h / 6., h2_6 = h * h / 6.;
+    double angle = 0.;
+    uint32_t it = 0;
+    for (;;) {
+        if ((U > HU && V > 0.) || it >= s->max_steps || !(U > 0.)) { /* :134-135 */
+            *steps = it;
+            return lam0 - O_NO_VALUE;
+        }
+        double NU, NV;
+        band_rk4(U, V, h, hh, hh2, hhh, h6, h2_6, &NU, &NV);
+        *steps = it + 1;
+        if ((NU > SU) != (U > SU)) { /* :150-182 */
+            double ns, wu, wv;
+            if (fabs(V) > fabs(NV)) {
+                ns = 0.; wu = U; wv = V;
+            } else {
+                ns = h; wu = NU; wv = NV;
+            }
+            for (int n = 0; n < 3; ++n) {
+                ns -= (wu - SU) / wv;
+                double n2 = ns * ns;
+                band_rk4(U, V, ns, ns / 2., n2 / 4., n2 / 2., ns / 6., n2 / 6., &wu, &wv);
+            }
+            return lam0 - (angle + ns);
+        }
+        if (NU < BD) return lam0 - O_NO_VALUE; /* :184 */
+        U = NU;
+        V = NV;
+        it += 1;
+        angle += h;
+    }
+}
+
+/* ring_kx > 0: GEO_FLAG_RING_F64 applies (the band test |kx ct - 1| < GEO_RING_X on the f32 ray) */
 static void pixel_f32(const geo_frame* f, const cam_f32* cam, const fconsts* k, int mode, const float* fan, uint32_t n_fan,
                       const uint32_t* sky, uint32_t sw, uint32_t sh, int opaque, int composite, uint32_t width,
                       uint32_t height, uint32_t px, uint32_t py, uint32_t* rgba, uint8_t* bh_out, float* uv,
-                      uint32_t* steps, float* ct_out) {
+                      uint32_t* steps, float ring_kx, const geo_scene* s) {
     float c2[3];
     camera_c2(f, cam, px, py, c2);
     float st = c2[2] > -1.0f ? c2[2] : -1.0f; /* med3(c2z, -1, 1): NaN -> -1 */
     st = st < 1.0f ? st : 1.0f;
     float rho2 = sqrtf(fmaf(c2[1], c2[1], c2[0] * c2[0])); /* cos theta */
     float rrho = 1.0f / rho2;
-    if (ct_out) *ct_out = rho2;
     float lam;
+    int bh;
     *steps = 0;
-    if (mode == (int)GEO_MODE_FAN) {
+    if (ring_kx > 0.0f && fabsf(ring_kx * rho2 - 1.0f) < GEO_RING_X) {
+        /* the capture-orbit band: lambda' and the mask in f64, the sky from the f32 ray */
+        double l = band_lambda(f, s, width, height, px, py, steps);
+        lam = (float)l;
+        bh = l < -7.0;
+    } else if (mode == (int)GEO_MODE_FAN) {
         float theta = geo_oracle_asinf(st);
         float t = clampf((F_PI2 - theta) / F_PI, 0.0f, 1.0f);
         t = t * (float)(n_fan - 1u);
@@ -672,10 +800,11 @@ static void pixel_f32(const geo_frame* f, const cam_f32* cam, const fconsts* k, 
         float w = t - fl;
         uint32_t i1 = (i + 1u < n_fan) ? i + 1u : n_fan - 1u;
         lam = fan[i] * (1.0f - w) + fan[i1] * w;
+        bh = lam < -7.0f;
     } else {
         lam = F_PI2 - geodesic_f32(k, st, rho2, rrho, mode == (int)GEO_MODE_ADAPTIVE, steps);
+        bh = lam < -7.0f;
     }
-    int bh = lam < -7.0f;
     /* sky_uv */
     float sl, cll;
     geo_oracle_sincosf(lam, &sl, &cll);
@@ -765,7 +894,7 @@ int geo_oracle_ring_band(const geo_frame* f, const geo_scene* s, uint32_t width,
                          uint32_t nrows, uint32_t row_step, uint8_t* band) {
     if (!f || !s || !band || width == 0 || height == 0 || row_step == 0) return -1;
     if ((uint64_t)row0 + (uint64_t)(nrows ? nrows - 1 : 0) * row_step >= height) return -1;
-    int ring = ring_applies(s) && s->mode == GEO_MODE_DIRECT;
+    int ring = ring_applies(s) && s->mode != GEO_MODE_FAN;
     float kx = ring ? geo_oracle_ring_kx(s) : 0.0f;
     cam_f32 cam = camera_f32(f, width, height);
     for (uint32_t r = 0; r < nrows; ++r)
@@ -790,25 +919,12 @@ static void* job_f32(void* arg) {
             size_t o = (size_t)r * j->width + px;
             uint32_t rgba, st;
             uint8_t bh;
-            float uv[2], ct;
+            float uv[2];
             memcpy(&rgba, j->rgba + 4 * o, 4); /* the target, for GEO_FLAG_COMPOSITE */
             pixel_f32(j->f, &j->cam, &j->k, (int)j->s->mode, j->fan, j->n_fan, j->sky, j->sw, j->sh, j->opaque,
-                      (j->s->flags & GEO_FLAG_COMPOSITE) != 0, j->width, j->height, px, py, &rgba, &bh, uv, &st, &ct);
-            total += st; /* steps_total counts the f32 draw's steps (geo.h GEO_FLAG_RING_F64) */
-            if (j->ring && in_ring(j->ring_kx, ct)) {
-                /* the capture-orbit band: the pixel again in f64 (the literal
-                 * restatement), sampled at its UV rounded to f32 */
-                geo_oracle_px p;
-                geo_oracle_pixel_f64(j->f, j->s, NULL, 0, j->width, j->height, px, py, &p);
-                float U = (float)p.u, V = (float)p.v;
-                if (!(U == U)) U = 0.0f;
-                if (!(V == V)) V = 0.0f;
-                uv[0] = clampf(U, 0.0f, 1.0f);
-                uv[1] = clampf(V, 0.0f, 1.0f);
-                bh = (uint8_t)p.bh;
-                st = p.steps;
-                rgba = bh ? 0xFF000000u : blend_over(bilinear_level(j->sky, j->sw, j->sh, uv[0], uv[1]), 0xFF000000u);
-            }
+                      (j->s->flags & GEO_FLAG_COMPOSITE) != 0, j->width, j->height, px, py, &rgba, &bh, uv, &st,
+                      j->ring ? j->ring_kx : 0.0f, j->s);
+            total += st; /* the steps each pixel reports (the band's: its f64 steps) */
             memcpy(j->rgba + 4 * o, &rgba, 4);
             if (j->mask) j->mask[o] = bh;
             if (j->uv) {
@@ -887,7 +1003,7 @@ int geo_oracle_render_f32(const geo_frame* f, const geo_scene* s, const float* f
     if ((uint64_t)row0 + (uint64_t)(nrows ? nrows - 1 : 0) * row_step >= height) return -1;
     if (s->mode == GEO_MODE_FAN && (!fan || n_fan < 2)) return -1;
     if ((s->flags & GEO_FLAG_RING_F64) &&
-        (s->mode != GEO_MODE_DIRECT || (s->flags & (GEO_FLAG_COMPOSITE | GEO_FLAG_MIPS))))
+        (s->mode == GEO_MODE_FAN || (s->flags & (GEO_FLAG_COMPOSITE | GEO_FLAG_MIPS))))
         return -1; /* the library's GEO_EINVAL */
     job_t j;
     memset(&j, 0, sizeof(j));
@@ -1022,7 +1138,7 @@ static void* job_grid(void* arg) {
             size_t o = (size_t)r * g->gw + x;
             uint32_t rgba = 0;
             pixel_f32(g->f, g->cam, g->k, g->mode, g->fan, g->n_fan, g->sky, g->sw, g->sh, 1, 0, g->width, g->height,
-                      x, g->r_lo + r, &rgba, &g->bh[o], &g->uv[2 * o], &g->steps[o], NULL);
+                      x, g->r_lo + r, &rgba, &g->bh[o], &g->uv[2 * o], &g->steps[o], 0.0f, NULL);
         }
     return NULL;
 }

@@ -11,6 +11,7 @@
 #include <vector>
 
 #include "../../include/geo/geo_cpu.h"
+#include "geo_band.h"
 #include "geo_pixel.h"
 
 namespace {
@@ -35,6 +36,9 @@ struct CpuJob {
     bool mips;
     const uint32_t* lvl[geo::kSkyMipLevels];
     uint32_t lw[geo::kSkyMipLevels], lh[geo::kSkyMipLevels];
+    // GEO_FLAG_RING_F64 (geo_band.h): the band's f64 constants, when it applies
+    bool ring;
+    geo::BandConsts band;
 };
 
 float geodesic(const CpuJob& j, float st, float ct, float rct, uint32_t* n) {
@@ -158,8 +162,16 @@ unsigned long long run_rows(const CpuJob& j, unsigned tid, unsigned nthreads) {
             const float ct = geo::central_rho(c2x, c2y);
             const float rct = geo::rcpf_(ct);
             uint32_t n = 0;
-            const float lam = geodesic(j, st, ct, rct, &n);
-            const bool bh = lam < geo::kBlackHoleLambda;
+            float lam;
+            bool bh;
+            if (j.ring && geo::in_band(j.band.kx, ct)) {
+                const double l = geo::band_lambda(j.band, px, py, &n);
+                lam = (float)l;
+                bh = l < (double)geo::kBlackHoleLambda;
+            } else {
+                lam = geodesic(j, st, ct, rct, &n);
+                bh = lam < geo::kBlackHoleLambda;
+            }
             float U = 0.0f, V = 0.0f;
             if (!bh || j.uv) geo::sky_uv(j.f->central_to_uv, c2x, c2y, ct, rct, lam, &U, &V);
             const size_t o = (size_t)ly * j.width + px;
@@ -200,7 +212,11 @@ extern "C" int geo_render_cpu(const geo_frame* frame, const geo_scene* scene, co
     if ((uint64_t)row0 + (uint64_t)(nrows - 1) * row_step >= height) return GEO_EINVAL;
     if (scene->mode != GEO_MODE_DIRECT && scene->mode != GEO_MODE_FAN && scene->mode != GEO_MODE_ADAPTIVE)
         return GEO_EINVAL;
-    if ((scene->flags & ~(GEO_FLAG_DEFER_STEPS | GEO_FLAG_COMPOSITE | GEO_FLAG_MIPS)) != 0) return GEO_EINVAL;
+    if ((scene->flags & ~(GEO_FLAG_DEFER_STEPS | GEO_FLAG_COMPOSITE | GEO_FLAG_MIPS | GEO_FLAG_RING_F64)) != 0)
+        return GEO_EINVAL;
+    const bool ring_flag = (scene->flags & GEO_FLAG_RING_F64) != 0;
+    if (ring_flag && (scene->mode == GEO_MODE_FAN || (scene->flags & (GEO_FLAG_COMPOSITE | GEO_FLAG_MIPS)) != 0))
+        return GEO_EINVAL;
     if (scene->mode == GEO_MODE_FAN && (!fan || n_fan < 2)) return GEO_EINVAL;
     if (scene->mode != GEO_MODE_FAN &&
         (!(scene->step > 0.0f) || !(scene->r_obs > 0.0f) || !(scene->sphere_r > 0.0f) || !(scene->rs >= 0.0f)))
@@ -240,6 +256,8 @@ extern "C" int geo_render_cpu(const geo_frame* frame, const geo_scene* scene, co
     j.mask = out_mask;
     j.uv = out_uv;
     j.steps = out_steps;
+    j.ring = ring_flag && scene->rs > 0.0f && scene->r_obs > scene->rs;
+    if (j.ring) j.band = geo::band_consts(*frame, *scene, width, height);
     // GEO_FLAG_MIPS: the chain geo_set_sky builds (geo::mip_down, level by level)
     j.mips = (scene->flags & GEO_FLAG_MIPS) != 0;
     std::vector<uint32_t> chain[geo::kSkyMipLevels];

@@ -98,20 +98,6 @@ struct geo_ctx {
     bool rebuild_keep;          // its order is still wanted (same grid and mode since)
     int rebuild_nb;             // the order buffer it writes
     unsigned long long costs_recorded, orders_adopted;  // geo_dispatch_stats
-    // GEO_FLAG_RING_F64 (geo_render.hip ring_fork): the f64 redraw's side
-    // stream, its pixel and entry lists (ring_cap entries) and count, and its
-    // events: fork (the caller's stream so far), join (the redraw done),
-    // free (the last scatter, which read the lists)
-    hipStream_t ring_stream;
-    void* ring_list;  // RingEntry[ring_cap]
-    void* ring_pix;   // RingPixel[ring_cap]
-    size_t ring_cap;
-    uint32_t* ring_count;  // a pair (ring_parity: this render's)
-    int ring_parity;
-    bool ring_open;  // a fork not yet followed by its scatter
-    hipEvent_t ring_fork, ring_join, ring_free;
-    hipStream_t ring_free_stream;  // the stream of the last scatter
-    bool ring_free_rec;
     // geo_time_next_render: events for the next render's kernel dispatch
     hipEvent_t time_start, time_stop;
 #if defined(GEO_WAVE_LOG)

@@ -26,6 +26,7 @@
 
 #include "../../include/geo/geo.h"
 #include "geo_ctx.h"
+#include "geo_band.h"
 #include "geo_pixel.h"
 
 // Work decomposition (measured): 32 x 8-pixel workgroup tiles
@@ -233,9 +234,9 @@ __device__ __forceinline__ float lane_xor16(float v) {
 
 // Epilogue of one pixel (shader.wgsl:88-105): black-hole test, sky UV,
 // bilinear sample, blend and the optional outputs at index o.
-__device__ __forceinline__ void shade_pixel(const RenderArgs& a, const float* central_to_uv, float c2x, float c2y,
-                                            float ct, float rct, float lam, uint32_t steps, size_t o) {
-    const bool bh = lam < geo::kBlackHoleLambda;
+// bh: the mask (lam < -7, or the band's f64 decision, GEO_FLAG_RING_F64).
+__device__ __forceinline__ void shade_pixel_bh(const RenderArgs& a, const float* central_to_uv, float c2x, float c2y,
+                                               float ct, float rct, float lam, bool bh, uint32_t steps, size_t o) {
     // A black-hole pixel is discarded (shader.wgsl:88): it needs its UV
     // only when the caller asks for it, so a wave inside the shadow skips
     // the sincos/atan2/asin and the sample (config 3 -0.3 %, config 5 -4.4 %)
@@ -258,6 +259,27 @@ __device__ __forceinline__ void shade_pixel(const RenderArgs& a, const float* ce
     if (a.out_uv) a.out_uv[o] = make_float2(U, V);
     if (a.out_steps) a.out_steps[o] = steps;
 }
+__device__ __forceinline__ void shade_pixel(const RenderArgs& a, const float* central_to_uv, float c2x, float c2y,
+                                            float ct, float rct, float lam, uint32_t steps, size_t o) {
+    shade_pixel_bh(a, central_to_uv, c2x, c2y, ct, rct, lam, lam < geo::kBlackHoleLambda, steps, o);
+}
+
+// GEO_FLAG_RING_F64's kernel argument: the band's f64 constants (geo_band.h);
+// empty in the other instantiations.
+template <bool RING>
+struct BandArg {};
+template <>
+struct BandArg<true> {
+    geo::BandConsts k;
+};
+// The band's constants reach the band's lanes through LDS: the kernel copies
+// them there from its argument segment at its start (one dword per thread,
+// one barrier).  Kernel arguments are loaded at the kernel's entry and held
+// in SGPRs to their last use: read in the band branch they took the kernel
+// to 106 SGPRs (6 waves per SIMD instead of 8); from LDS they are loaded
+// where the band's lanes use them.
+constexpr uint32_t kBandDwords = (uint32_t)(sizeof(geo::BandConsts) / 4u);
+static_assert(sizeof(geo::BandConsts) % 8u == 0 && kBandDwords <= kBlock, "one dword per thread");
 
 // GEO_FLAG_MIPS epilogue: the pixel's UV and its quad footprint rho2 are
 // known; the trilinear sample in place of the level-0 one.
@@ -396,8 +418,11 @@ __device__ __forceinline__ void fan_tile(const RenderArgs& a, const FrameK& f, s
 
 // NF: frames of the launch (FrameBatch; 1, or up to kMaxBatchFrames with the
 // frame in blockIdx.z and its output a.out_frame_px pixels after the last's).
-template <int MODE, int KIND, bool MIPS, uint32_t NF>
-__global__ __launch_bounds__(kBlock) void geo_render_kernel(const RenderArgs a, const FrameBatch<NF> fb) {
+// RING: GEO_FLAG_RING_F64 (geo_band.h): the lanes of the capture-orbit band
+// take their traveled angle from the f64 path instead of the f32 one.
+template <int MODE, int KIND, bool MIPS, uint32_t NF, bool RING>
+__global__ __launch_bounds__(kBlock) void geo_render_kernel(const RenderArgs a, const FrameBatch<NF> fb,
+                                                            const BandArg<RING> bk) {
 #if defined(GEO_WAVE_LOG)
     const unsigned long long t_wave0 = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -412,6 +437,13 @@ __global__ __launch_bounds__(kBlock) void geo_render_kernel(const RenderArgs a, 
     }
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x) >> 6;
     const uint32_t lane = threadIdx.x & 63u;
+    // RING: the band's constants in LDS (kBandDwords)
+    __shared__ double band_lds[RING ? kBandDwords / 2u : 1u];
+    if constexpr (RING) {
+        if (threadIdx.x < kBandDwords)
+            reinterpret_cast<uint32_t*>(band_lds)[threadIdx.x] = reinterpret_cast<const uint32_t*>(&bk.k)[threadIdx.x];
+        __syncthreads();
+    }
     const uint32_t px = tile.x * kTileW + (wave % kWavesX) * kWaveW + lane % kWaveW;
     // local row -> frame row.  band_rows is a multiple of 8 (checked on the
     // host): each wave's rows (at most 8) lie in one band and the mapping is
@@ -422,6 +454,8 @@ __global__ __launch_bounds__(kBlock) void geo_render_kernel(const RenderArgs a, 
     const uint32_t band = __umulhi(wl0, a.band_magic);
     const uint32_t py = a.row0 + band * a.band_stride + (wl0 - band * a.band_rows) + (ly - wl0);
     uint32_t steps = 0;
+    uint32_t cost_scale = 1u;  // RING: the band's lanes record their f64 steps at twice the cost
+    (void)cost_scale;
     const bool in_frame = px < a.width && ly < a.nrows && py < a.height;
     if constexpr (LR > 1) {
         fan_tile<LR>(a, f, obase, tile, wave, lane);
@@ -433,8 +467,34 @@ __global__ __launch_bounds__(kBlock) void geo_render_kernel(const RenderArgs a, 
             const float st = geo::central_sin(c2z);
             const float ct = geo::central_rho(c2x, c2y);
             const float rct = geo::rcpf_(ct);  // shared by the ray's 1/b^2 and its sky direction
-            const float lam = pixel_lambda<MODE, KIND>(a, frame_consts(a, fb, z), st, ct, rct, &steps);
-            shade_pixel(a, f.frame.central_to_uv, c2x, c2y, ct, rct, lam, steps, obase + (size_t)ly * a.width + px);
+            if constexpr (RING) {
+                // the band's lanes skip the f32 integration (its loop runs on
+                // the other lanes) and take lambda' and the mask from the f64
+                // path; both then draw the sky from the f32 ray
+                const geo::BandConsts& bkl = *reinterpret_cast<const geo::BandConsts*>(band_lds);
+                const bool band = geo::in_band(bk.k.kx, ct);
+                float lam = 0.0f;
+                bool bh = false;
+                if (!band) {
+                    lam = pixel_lambda<MODE, KIND>(a, frame_consts(a, fb, z), st, ct, rct, &steps);
+                    bh = lam < geo::kBlackHoleLambda;
+                }
+                if (geo::ballot_(band) != 0) {
+                    if (band) {
+                        GEO_COLD_ARM();
+                        const double l = geo::band_lambda(bkl, px, py, &steps);
+                        lam = (float)l;
+                        bh = l < (double)geo::kBlackHoleLambda;
+                        cost_scale = 2u;  // an f64 step issues as two f32 ones
+                    }
+                }
+                shade_pixel_bh(a, f.frame.central_to_uv, c2x, c2y, ct, rct, lam, bh, steps,
+                               obase + (size_t)ly * a.width + px);
+            } else {
+                const float lam = pixel_lambda<MODE, KIND>(a, frame_consts(a, fb, z), st, ct, rct, &steps);
+                shade_pixel(a, f.frame.central_to_uv, c2x, c2y, ct, rct, lam, steps,
+                            obase + (size_t)ly * a.width + px);
+            }
         }
     } else {
         // Every lane traces its pixel, the ones outside the frame or the
@@ -479,7 +539,7 @@ __global__ __launch_bounds__(kBlock) void geo_render_kernel(const RenderArgs a, 
             // a wave holds its slot until its slowest lane stops: the tile's
             // cost is the sum of its waves' largest step counts (frame 0's
             // of a batch: the order is per tile)
-            const uint32_t wmax = wave_max_u32(steps);
+            const uint32_t wmax = wave_max_u32(RING ? steps * cost_scale : steps);
             if ((threadIdx.x & 63) == 0)
                 atomicAdd(&a.tile_cost[tile.y * gridDim.x + tile.x], wmax + a.cost_overhead);
         }
@@ -858,303 +918,6 @@ __global__ void geo_fan_kernel(double sphere_r, double schwarz_r, uint32_t max_i
     fan[i] = (float)(FRAC_PI_2 - angle);
 }
 
-// ---- GEO_FLAG_RING_F64 (geo.h; DESIGN.md §2, "The capture band in f64") ----
-// Next to the capture orbit the orbit's instability amplifies the f32 draw's
-// roundings past the UV bar; these pixels are drawn again in f64 by a kernel
-// on a side stream, concurrently with the f32 draw, and written over its
-// output afterwards (geo_ring_scatter).  The band is decided on the f32 ray,
-// exactly as the oracle decides it (the same f32 operations), so which
-// pixels are redrawn is part of the specification.
-
-// One pixel of the band: its column, local (output) row and frame row
-// (geo_ring_scan), then what the f64 redraw gives it (geo_ring_kernel).
-struct RingPixel {
-    uint32_t px, lr, py;
-};
-struct RingEntry {
-    uint64_t o;
-    uint32_t rgba;
-    uint32_t steps_bh;  // steps; bit 31: black hole
-    float u, v;
-};
-
-struct RingArgs {
-    FrameK f;
-    uint32_t width, height, row0, nrows, band_rows, band_magic, band_stride;
-    float kx;          // r_obs / (sqrt(1 - rs/r_obs) 3 sqrt(3)/2 rs), rounded once (geo_oracle_ring_kx)
-    float skip_slack;  // geo_ring_scan: a tile whose centre's test exceeds GEO_RING_X by this holds no band pixel
-    double rs, sphere_r, r_obs, step;
-    uint32_t max_steps;
-    const uint32_t* sky;
-    uint32_t sky_bytes, sky_pitch_b, sky_opaque;
-    float sky_w256, sky_h256;
-    RingPixel* pix;
-    RingEntry* list;
-    uint32_t* count;
-    uint32_t cap;  // entries the lists hold (a pixel is listed once: >= the launch's pixels)
-};
-
-// The literal loop's exits with its step count (sphere_ray_tracer.rs:134-191:
-// `steps = iteration + 1` once a step is taken; the loop test on the state
-// before it ends the loop without one), on fan_integrate's scaled f64 RK4
-// and its groups of steps per exit branch.
-template <bool FLAT>
-__device__ __attribute__((noinline)) double ring_integrate(double sphere_r, double schwarz_r, uint32_t max_iter, double step, double r,
-                                 double u_bar0, uint32_t* steps) {
-    const double NO_VALUE = GEO_NO_VALUE;
-    const double r3_2 = 3. * schwarz_r / 2.;
-    const double c = FLAT ? 1. : r3_2;
-    const double u0 = 1. / r;
-    const double SU = c / sphere_r;
-    const double BD = c * (0.9 * fmin(u0, 1. / fmax(sphere_r, r3_2)));
-    const double HU = FLAT ? __builtin_inf() : c / schwarz_r;
-    const double h = step, hh = step / 2., hh2 = step * step / 4., hhh = step * step / 2., h6 = step / 6.,
-                 h2_6 = step * step / 6.;
-    double U = c * u0, V = c * u_bar0;
-    *steps = 0;
-    if (!(U > 0.)) return NO_VALUE;
-    double angle = 0.;
-    uint32_t it = 0;
-    // fan_integrate's groups: one exit branch per kFanGroup steps, a stopping
-    // group replayed step by step below (the same arithmetic, the literal
-    // loop's step count)
-    while (it + kFanGroup <= max_iter) {
-        double su[kFanGroup + 1], sv[kFanGroup + 1];
-        su[0] = U;
-        sv[0] = V;
-        bool stop = false;
-#pragma unroll
-        for (int j = 0; j < kFanGroup; ++j) {
-            fan_rk4<FLAT>(su[j], sv[j], h, hh, hh2, hhh, h6, h2_6, &su[j + 1], &sv[j + 1]);
-            stop |= fan_test<FLAT>(su[j], sv[j], su[j + 1], SU, BD, HU) != 0;
-        }
-        if (stop) break;
-        U = su[kFanGroup];
-        V = sv[kFanGroup];
-#pragma unroll
-        for (int j = 0; j < kFanGroup; ++j) angle += step;
-        it += kFanGroup;
-        *steps = it;
-    }
-    for (; it < max_iter; ++it) {
-        if (!FLAT && U > HU && V > 0.) return NO_VALUE;
-        double NU, NV;
-        fan_rk4<FLAT>(U, V, h, hh, hh2, hhh, h6, h2_6, &NU, &NV);
-        *steps = it + 1;
-        if ((NU > SU) != (U > SU)) {
-            double ns, wu, wv;
-            if (fabs(V) > fabs(NV)) {
-                ns = 0.;
-                wu = U;
-                wv = V;
-            } else {
-                ns = h;
-                wu = NU;
-                wv = NV;
-            }
-            for (int n = 0; n < 3; ++n) {
-                ns -= (wu - SU) / wv;
-                const double n2 = ns * ns;
-                fan_rk4<FLAT>(U, V, ns, ns / 2., n2 / 4., n2 / 2., ns / 6., n2 / 6., &wu, &wv);
-            }
-            return angle + ns;
-        }
-        if (NU < BD) return NO_VALUE;
-        U = NU;
-        V = NV;
-        angle += step;
-    }
-    return NO_VALUE;
-}
-
-// ocml's f64 atan2, asin, sin, cos as calls: inlined, they take the
-// kernel's registers past 200 VGPRs (2 waves per SIMD beside the f32 draw)
-__device__ __attribute__((noinline)) double ring_atan2(double y, double x) { return atan2(y, x); }
-__device__ __attribute__((noinline)) double ring_asin(double x) { return asin(x); }
-__device__ __attribute__((noinline)) double ring_sin(double x) { return sin(x); }
-__device__ __attribute__((noinline)) double ring_cos(double x) { return cos(x); }
-
-__device__ __forceinline__ void ring_m3v(const float* m, const double* v, double* o) {
-    for (int i = 0; i < 3; ++i) o[i] = (double)m[i] * v[0] + (double)m[4 + i] * v[1] + (double)m[8 + i] * v[2];
-}
-__device__ __attribute__((noinline)) void ring_to_cart(double phi, double lam, double* c) {
-    c[0] = ring_cos(phi) * ring_cos(lam);
-    c[1] = ring_sin(phi) * ring_cos(lam);
-    c[2] = ring_sin(lam);
-}
-
-// The pixel as the literal f64 restatement draws it (shader.wgsl:57-106 with
-// the geodesic at theta = the pixel's lambda, geo_oracle_pixel_f64): UV, the
-// black-hole test and the steps.  Direct mode, rs > 0, r_obs > rs.
-__device__ void ring_pixel_f64(const RingArgs& a, uint32_t px, uint32_t py, double* u, double* v, bool* bh,
-                               uint32_t* steps) {
-    const double PI = 3.14159265358979323846, FRAC_PI_2 = 1.57079632679489661923;
-    const geo_frame& f = a.f.frame;
-    const float* m0 = f.display_to_movement;
-    const double ndc_x = ((double)px + 0.5) / (double)a.width * 2. - 1.;
-    const double ndc_y = 1. - ((double)py + 0.5) / (double)a.height * 2.;
-    double c[3] = {-ndc_y * (double)m0[12], -ndc_x * (double)m0[13], 1. * (double)m0[14]};
-    double d[3];
-    ring_m3v(m0, c, d);
-    const double len = sqrt(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]);
-    d[0] /= len;
-    d[1] /= len;
-    d[2] /= len;
-    double phi = ring_atan2(d[1], d[0]);
-    double lam = ring_asin(d[2]);
-    const double k = (double)f.psi_factor_and_position[0];
-    const double sin_result = ring_sin(lam);
-    lam = ring_asin((sin_result - k) / (1. - sin_result * k));
-    ring_to_cart(phi, lam, c);
-    ring_m3v(f.movement_to_central, c, d);
-    phi = ring_atan2(d[1], d[0]);
-    const double theta = ring_asin(d[2]);
-    // sphere_ray_tracer.rs:38-49 at theta (r_obs > rs: the outside branch)
-    const double r = a.r_obs;
-    const double rotation = r * ring_cos(theta);
-    const bool r_falling = theta > 0.;
-    const double energy = sqrt(1. - a.rs / r);
-    double angle, u_bar0;
-    *steps = 0;
-    if (solve_geodesic_f64_init(a.sphere_r, a.rs, r, energy, rotation, r_falling, &angle, &u_bar0))
-        angle = ring_integrate<false>(a.sphere_r, a.rs, a.max_steps, a.step, r, u_bar0, steps);
-    const double lam2 = FRAC_PI_2 - angle;
-    *bh = lam2 < -7.;
-    ring_to_cart(phi, lam2, c);
-    ring_m3v(f.central_to_uv, c, d);
-    phi = ring_atan2(d[1], d[0]);
-    lam = ring_asin(d[2]);
-    double uu = phi / (FRAC_PI_2 * 4.);
-    if (uu < 0.) uu += 1.;
-    *u = uu;
-    *v = 0.5 - lam / (FRAC_PI_2 * 2.);
-    (void)PI;
-}
-
-// The band test on the f32 ray of one pixel (the oracle's in_ring): its
-// cos(theta) by the f32 draw's own camera ray.
-__device__ __forceinline__ float ring_x(const RingArgs& a, uint32_t px, uint32_t py) {
-    float c2x, c2y, c2z;
-    geo::pixel_central_dir(a.f.cam, a.f.frame.movement_to_central, a.f.frame.psi_factor_and_position[0], a.f.kt, px,
-                           py, &c2x, &c2y, &c2z);
-    return fabsf(a.kx * geo::central_rho(c2x, c2y) - 1.0f);
-}
-
-// The band test.  One wave per kRingScanTiles^2 tiles of 8 x 8 pixels: lane
-// t first tests tile t's centre pixel against the band widened by
-// a.skip_slack, the most the test's |kx cos(theta) - 1| can change within 4
-// pixels of it (ring_fork: a Lipschitz bound on the ray's direction over the
-// frame, so no band pixel is ever in a skipped tile); then the wave tests
-// every pixel of the tiles that may hold band pixels, one tile per pass
-// (few tiles per wave: the passes are a chain of camera rays), and lists the
-// band's pixels (one atomic per wave; each pixel's slot from its rank in its
-// tile's ballot).  A tile's 8 rows lie in one band of the launch's band
-// layout (band heights are multiples of 8), so its frame rows are
-// consecutive.
-constexpr uint32_t kRingScanTiles = 4;
-__global__ __launch_bounds__(64) void geo_ring_scan(const RingArgs a) {
-    __builtin_amdgcn_s_setprio(2);  // beside the f32 draw (ring_fork): it gates the f64 redraw
-    constexpr uint32_t T = kRingScanTiles;
-    const uint32_t lane = threadIdx.x;
-    const uint32_t tx0 = blockIdx.x * T, ty0 = blockIdx.y * T;  // in 8-pixel tiles
-    auto frame_row = [&](uint32_t lr) {
-        const uint32_t band = __umulhi(lr, a.band_magic);
-        return a.row0 + band * a.band_stride + (lr - band * a.band_rows);
-    };
-    bool may = false;
-    if (lane < T * T) {
-        const uint32_t tx = tx0 + lane % T, ty = ty0 + lane / T;
-        if (tx * 8u < a.width && ty * 8u < a.nrows) {
-            const float x = ring_x(a, tx * 8u + 4u, frame_row(ty * 8u + 4u));
-            may = !(x >= GEO_RING_X + a.skip_slack);  // NaN: tested pixel by pixel
-        }
-    }
-    // pass 1: each candidate tile's band pixels as a ballot (kept in LDS),
-    // and their count; one atomic reserves the wave's entries; pass 2: the
-    // entries
-    const uint64_t cand = __ballot(may);
-    __shared__ uint64_t masks[T * T];
-    uint32_t total = 0;
-    for (uint64_t tiles = cand; tiles != 0; tiles &= tiles - 1ull) {
-        const uint32_t t = (uint32_t)__ffsll((unsigned long long)tiles) - 1u;
-        const uint32_t px = (tx0 + t % T) * 8u + (lane & 7u);
-        const uint32_t lr = (ty0 + t / T) * 8u + (lane >> 3);
-        bool ring = false;
-        if (px < a.width && lr < a.nrows) {
-            const uint32_t py = frame_row(lr);
-            ring = py < a.height && ring_x(a, px, py) < GEO_RING_X;
-        }
-        const uint64_t m = __ballot(ring);
-        if (lane == 0) masks[t] = m;
-        total += (uint32_t)__popcll(m);
-    }
-    if (total == 0) return;
-    __syncthreads();
-    uint32_t base = 0;
-    if (lane == 0) base = atomicAdd(a.count, total);
-    base = (uint32_t)__shfl((int)base, 0);
-    for (uint64_t tiles = cand; tiles != 0; tiles &= tiles - 1ull) {
-        const uint32_t t = (uint32_t)__ffsll((unsigned long long)tiles) - 1u;
-        const uint64_t m = masks[t];
-        if ((m >> lane) & 1ull) {
-            const uint32_t px = (tx0 + t % T) * 8u + (lane & 7u);
-            const uint32_t lr = (ty0 + t / T) * 8u + (lane >> 3);
-            const uint32_t slot = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-            if (slot < a.cap) a.pix[slot] = RingPixel{px, lr, frame_row(lr)};
-        }
-        base += (uint32_t)__popcll(m);
-    }
-}
-
-// The f64 redraw of the listed pixels, one lane each (a dense list: the
-// long f64 chains run on full waves).
-constexpr uint32_t kRingBlocks = 2048, kRingThreads = 64;
-__global__ __launch_bounds__(kRingThreads) void geo_ring_kernel(const RingArgs a) {
-    // its few waves are long f64 chains beside the f32 draw's waves: they
-    // issue first (the draw keeps the rest of each SIMD's issue)
-    __builtin_amdgcn_s_setprio(3);
-    const uint32_t n = min(*a.count, a.cap);
-    for (uint32_t i = blockIdx.x * kRingThreads + threadIdx.x; i < n; i += kRingBlocks * kRingThreads) {
-        const RingPixel p = a.pix[i];
-        double u, v;
-        bool bh;
-        uint32_t steps;
-        ring_pixel_f64(a, p.px, p.py, &u, &v, &bh, &steps);
-        float U = (float)u, V = (float)v;
-        if (!(U == U)) U = 0.0f;
-        if (!(V == V)) V = 0.0f;
-        U = fminf(fmaxf(U, 0.0f), 1.0f);
-        V = fminf(fmaxf(V, 0.0f), 1.0f);
-        const PaddedSkyQuad quad{__builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(a.sky), 0, (int)a.sky_bytes,
-                                                                   kBufferRsrcWord3),
-                                 a.sky_pitch_b};
-        RingEntry e;
-        e.o = (uint64_t)p.lr * a.width + p.px;
-        e.rgba = bh ? geo::kBlackRGBA : geo::sample_sky_qf(quad, a.sky_w256, a.sky_h256, a.sky_opaque != 0, U, V);
-        e.steps_bh = (steps & 0x7FFFFFFFu) | (bh ? 0x80000000u : 0u);
-        e.u = U;
-        e.v = V;
-        a.list[i] = e;
-    }
-}
-
-// After the f32 draw and geo_ring_kernel: the redrawn pixels over the output.
-// (The count is read after both: the list's entries < count are written.)
-__global__ __launch_bounds__(256) void geo_ring_scatter(const RingEntry* list, const uint32_t* count, uint32_t cap,
-                                                        uint32_t* next, uint32_t* rgba, uint8_t* mask, float2* uv,
-                                                        uint32_t* steps) {
-    const uint32_t n = min(*count, cap);
-    // the next render's counter (the other of the pair; nothing reads it now)
-    if (blockIdx.x == 0 && threadIdx.x == 0) *next = 0u;
-    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u) {
-        const RingEntry e = list[i];
-        rgba[e.o] = e.rgba;
-        if (mask) mask[e.o] = (uint8_t)(e.steps_bh >> 31);
-        if (uv) uv[e.o] = make_float2(e.u, e.v);
-        if (steps) steps[e.o] = e.steps_bh & 0x7FFFFFFFu;
-    }
-}
-
 }  // namespace
 
 
@@ -1241,9 +1004,6 @@ int geo_ctx_create(int device, geo_ctx** out) {
 static int wait_renders(geo_ctx* c) {
     for (int i = 0; i < c->n_render_streams; ++i)
         if (hipEventSynchronize(c->render_done[i]) != hipSuccess) return GEO_EHIP;
-    // a ring redraw whose render failed before its scatter (which `done`
-    // would have covered) may still read the sky
-    if (c->ring_open && hipEventSynchronize(c->ring_join) != hipSuccess) return GEO_EHIP;
     return GEO_OK;
 }
 
@@ -1317,15 +1077,6 @@ void geo_ctx_destroy(geo_ctx* c) {
     if (c->step_slots) (void)hipFree(c->step_slots);
     if (c->learn_valid || c->tile_cap) (void)hipEventSynchronize(c->order_written);
     if (c->learn_stream) (void)hipStreamDestroy(c->learn_stream);
-    if (c->ring_free_rec) (void)hipEventSynchronize(c->ring_free);
-    if (c->ring_stream) (void)hipStreamSynchronize(c->ring_stream);
-    if (c->ring_list) (void)hipFree(c->ring_list);
-    if (c->ring_pix) (void)hipFree(c->ring_pix);
-    if (c->ring_count) (void)hipFree(c->ring_count);
-    if (c->ring_fork) (void)hipEventDestroy(c->ring_fork);
-    if (c->ring_join) (void)hipEventDestroy(c->ring_join);
-    if (c->ring_free) (void)hipEventDestroy(c->ring_free);
-    if (c->ring_stream) (void)hipStreamDestroy(c->ring_stream);
     for (int b = 0; b < 2; ++b)
         if (c->order[b]) (void)hipFree(c->order[b]);
     if (c->tile_cost) (void)hipFree(c->tile_cost);
@@ -1506,7 +1257,8 @@ extern "C++" {
 // after it.
 template <int MODE, int KIND, uint32_t NF>
 static int launch_tiles(RenderArgs a, const FrameBatch<NF>& fb, uint32_t nframes, bool mips, uint32_t tiles_x,
-                        uint32_t tiles_y, hipStream_t s, hipEvent_t done, hipEvent_t t_start, hipEvent_t t_stop) {
+                        uint32_t tiles_y, hipStream_t s, hipEvent_t done, hipEvent_t t_start, hipEvent_t t_stop,
+                        const geo::BandConsts* band) {
     for (uint32_t y0 = 0; y0 < tiles_y; y0 += kMaxGridY) {
         a.tile_y0 = y0;
         const uint32_t ny = tiles_y - y0 < kMaxGridY ? tiles_y - y0 : kMaxGridY;
@@ -1515,15 +1267,25 @@ static int launch_tiles(RenderArgs a, const FrameBatch<NF>& fb, uint32_t nframes
         hipEvent_t stop = last ? (t_stop ? t_stop : done) : nullptr;
         const dim3 grid(tiles_x, ny, nframes);
         if constexpr (NF == 1) {
+            if constexpr (MODE != GEO_MODE_FAN && KIND != geo::kFlat) {
+                if (band) {  // GEO_FLAG_RING_F64 (one frame, level-0 sampler)
+                    BandArg<true> bk;
+                    bk.k = *band;
+                    hipExtLaunchKernelGGL((geo_render_kernel<MODE, KIND, false, 1, true>), grid, dim3(kBlock), 0, s,
+                                          start, stop, 0, a, fb, bk);
+                    if (hipGetLastError() != hipSuccess) return GEO_EHIP;
+                    continue;
+                }
+            }
             if (mips)
-                hipExtLaunchKernelGGL((geo_render_kernel<MODE, KIND, true, 1>), grid, dim3(kBlock), 0, s, start, stop,
-                                      0, a, fb);
+                hipExtLaunchKernelGGL((geo_render_kernel<MODE, KIND, true, 1, false>), grid, dim3(kBlock), 0, s,
+                                      start, stop, 0, a, fb, BandArg<false>{});
             else
-                hipExtLaunchKernelGGL((geo_render_kernel<MODE, KIND, false, 1>), grid, dim3(kBlock), 0, s, start,
-                                      stop, 0, a, fb);
+                hipExtLaunchKernelGGL((geo_render_kernel<MODE, KIND, false, 1, false>), grid, dim3(kBlock), 0, s,
+                                      start, stop, 0, a, fb, BandArg<false>{});
         } else {
-            hipExtLaunchKernelGGL((geo_render_kernel<MODE, KIND, false, NF>), grid, dim3(kBlock), 0, s, start, stop,
-                                  0, a, fb);
+            hipExtLaunchKernelGGL((geo_render_kernel<MODE, KIND, false, NF, false>), grid, dim3(kBlock), 0, s, start,
+                                  stop, 0, a, fb, BandArg<false>{});
         }
         if (hipGetLastError() != hipSuccess) return GEO_EHIP;
     }
@@ -1533,16 +1295,19 @@ static int launch_tiles(RenderArgs a, const FrameBatch<NF>& fb, uint32_t nframes
 
 // One frame (FrameBatch<1>, the kernel arguments as before batching), or a
 // batch of 2 .. kMaxBatchFrames in one launch (FrameBatch<kMaxBatchFrames>,
-// the frame in blockIdx.z; no mip-mapped sampler).
+// the frame in blockIdx.z; no mip-mapped sampler).  band: GEO_FLAG_RING_F64's
+// constants (one frame), or null.
 static_assert(sizeof(RenderArgs) + sizeof(FrameBatch<kMaxBatchFrames>) <= 4096, "kernel arguments fit 4 KiB");
+static_assert(sizeof(RenderArgs) + sizeof(FrameBatch<1>) + sizeof(BandArg<true>) <= 4096,
+              "kernel arguments fit 4 KiB");
 template <int MODE, int KIND>
 static int launch_frames(const RenderArgs& a, const FrameK* fk, const geo::PixelConsts* pk, uint32_t nframes,
                          bool mips, uint32_t tiles_x, uint32_t tiles_y, hipStream_t s, hipEvent_t done,
-                         hipEvent_t t_start, hipEvent_t t_stop) {
+                         hipEvent_t t_start, hipEvent_t t_stop, const geo::BandConsts* band = nullptr) {
     if (nframes == 1) {
         FrameBatch<1> fb;
         fb.f[0] = fk[0];
-        return launch_tiles<MODE, KIND, 1>(a, fb, 1, mips, tiles_x, tiles_y, s, done, t_start, t_stop);
+        return launch_tiles<MODE, KIND, 1>(a, fb, 1, mips, tiles_x, tiles_y, s, done, t_start, t_stop, band);
     }
     FrameBatch<kMaxBatchFrames> fb;
     std::memset(&fb, 0, sizeof(fb));
@@ -1551,7 +1316,7 @@ static int launch_frames(const RenderArgs& a, const FrameK* fk, const geo::Pixel
         fb.k[i] = pk[i];
     }
     return launch_tiles<MODE, KIND, kMaxBatchFrames>(a, fb, nframes, false, tiles_x, tiles_y, s, done, t_start,
-                                                     t_stop);
+                                                     t_stop, nullptr);
 }
 }
 
@@ -1600,127 +1365,6 @@ static int invalid_call(geo_ctx* c) {
 // out_frame_stride bytes after frame f - 1's (a batch draws colour only).
 // scene_per_frame: `scene` points at nframes scenes, frame f's at scene[f]
 // (they may differ in r_obs only); otherwise one scene for every frame.
-// GEO_FLAG_RING_F64: the list holds one entry per pixel of the launch at
-// most (the band may cover a whole frame); growing it waits for the last
-// scatter, which read the old one.  The side stream and its events are
-// made on first use.
-constexpr uint32_t kRingScatterBlocks = 512;
-static int ensure_ring(geo_ctx* c, size_t n) {
-    if (!c->ring_stream) {
-        if (hipStreamCreateWithFlags(&c->ring_stream, hipStreamNonBlocking) != hipSuccess) {
-            c->ring_stream = nullptr;
-            return GEO_EHIP;
-        }
-        if (hipEventCreateWithFlags(&c->ring_fork, kCtxEventFlags) != hipSuccess ||
-            hipEventCreateWithFlags(&c->ring_join, kCtxEventFlags) != hipSuccess ||
-            hipEventCreateWithFlags(&c->ring_free, kCtxEventFlags) != hipSuccess)
-            return GEO_EHIP;
-        if (hipMalloc(&c->ring_count, 256) != hipSuccess) {
-            c->ring_count = nullptr;
-            return GEO_ENOMEM;
-        }
-        // the pair of counters: render k counts into ring_count[k % 2], and
-        // its scatter zeroes the other one for render k + 1
-        if (hipMemset(c->ring_count, 0, 256) != hipSuccess) return GEO_EHIP;
-        c->ring_parity = 0;
-    }
-    if (c->ring_cap >= n) return GEO_OK;
-    if (c->ring_free_rec && hipEventSynchronize(c->ring_free) != hipSuccess) return GEO_EHIP;
-    // a fork whose render failed before its scatter: its redraw may still run
-    if (c->ring_open && hipEventSynchronize(c->ring_join) != hipSuccess) return GEO_EHIP;
-    if (c->ring_list) (void)hipFree(c->ring_list);
-    if (c->ring_pix) (void)hipFree(c->ring_pix);
-    c->ring_list = c->ring_pix = nullptr;
-    c->ring_cap = 0;
-    if (hipMalloc(&c->ring_list, n * sizeof(RingEntry)) != hipSuccess ||
-        hipMalloc(&c->ring_pix, n * sizeof(RingPixel)) != hipSuccess) {
-        if (c->ring_list) (void)hipFree(c->ring_list);
-        c->ring_list = c->ring_pix = nullptr;
-        return GEO_ENOMEM;
-    }
-    c->ring_cap = n;
-    return GEO_OK;
-}
-
-// The band test (geo_ring_scan) and the f64 redraw (geo_ring_kernel) forked
-// onto the ring stream before the f32 draw; ring_join marks their end.
-static int ring_fork(geo_ctx* c, const RenderArgs& a, const FrameK& fk, const geo_scene& sc, hipStream_t s) {
-    const int est = ensure_ring(c, (size_t)a.nrows * a.width);
-    if (est) return est;
-    RingArgs r;
-    r.f = fk;
-    r.width = a.width;
-    r.height = a.height;
-    r.row0 = a.row0;
-    r.nrows = a.nrows;
-    r.band_rows = a.band_rows;
-    r.band_magic = a.band_magic;
-    r.band_stride = a.band_stride;
-    const double rs = (double)sc.rs, ro = (double)sc.r_obs;
-    r.kx = (float)(ro / (std::sqrt(1.0 - rs / ro) * (1.5 * std::sqrt(3.0) * rs)));  // geo_oracle_ring_kx
-    // geo_ring_scan's tile skip.  A pixel within 4 of a tile's centre (in x
-    // and y) has the unnormalised ray d = py a + px b + c within
-    // D = 4(|a| + |b|) of the centre's, and every d lies on the plane
-    // through c spanned by a and b, at least dist = |(a x b).c| / |a x b|
-    // from the origin: the two directions are at most asin(D / dist) apart
-    // (D < dist).  The aberration (a boost by psi_k) stretches angles by at
-    // most sqrt((1 + |k|)/(1 - |k|)), the rotation to the central frame not
-    // at all, and cos(theta) = |sin(polar angle)| moves by at most the
-    // angle; so |kx cos(theta) - 1| moves by at most kx times that (1 %
-    // more, plus 1e-4 for the f32 roundings).  No bound (a degenerate
-    // camera): every tile is tested pixel by pixel.
-    {
-        const geo::CameraConsts& cc = fk.cam;
-        const double A[3] = {cc.a[0], cc.a[1], cc.a[2]}, B[3] = {cc.b[0], cc.b[1], cc.b[2]},
-                     C[3] = {cc.c[0], cc.c[1], cc.c[2]};
-        const double n[3] = {A[1] * B[2] - A[2] * B[1], A[2] * B[0] - A[0] * B[2], A[0] * B[1] - A[1] * B[0]};
-        const double nn = std::sqrt(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]);
-        const double dist = nn > 0.0 ? std::fabs(n[0] * C[0] + n[1] * C[1] + n[2] * C[2]) / nn : 0.0;
-        const double D = 4.0 * (std::sqrt(A[0] * A[0] + A[1] * A[1] + A[2] * A[2]) +
-                                std::sqrt(B[0] * B[0] + B[1] * B[1] + B[2] * B[2]));
-        const double k = std::fabs((double)fk.frame.psi_factor_and_position[0]);
-        double slack = HUGE_VAL;
-        if (dist > 0.0 && D < dist && k < 1.0)
-            slack = (double)r.kx * std::sqrt((1.0 + k) / (1.0 - k)) * std::asin(D / dist) * 1.01 + 1e-4;
-        r.skip_slack = std::isfinite(slack) ? (float)slack : HUGE_VALF;
-    }
-    r.rs = rs;
-    r.sphere_r = (double)sc.sphere_r;
-    r.r_obs = ro;
-    r.step = (double)sc.step;
-    r.max_steps = sc.max_steps;
-    r.sky = a.sky;
-    r.sky_bytes = a.sky_bytes;
-    r.sky_pitch_b = a.sky_pitch_b;
-    r.sky_opaque = a.sky_opaque;
-    r.sky_w256 = a.sky_w256;
-    r.sky_h256 = a.sky_h256;
-    r.pix = static_cast<RingPixel*>(c->ring_pix);
-    r.list = static_cast<RingEntry*>(c->ring_list);
-    r.count = c->ring_count + c->ring_parity;  // zeroed by the previous scatter (or at allocation)
-    r.cap = (uint32_t)((size_t)a.nrows * a.width);
-    // the band test and the f64 redraw on the ring stream, forked before the
-    // f32 draw and running beside it: after the caller's stream so far, and
-    // after the previous scatter (which read the lists) if that ran on
-    // another stream.  A render that failed between its fork and its
-    // scatter left its counter unread and not flipped: this one starts it
-    // from zero.
-    hipStream_t rs_ = c->ring_stream;
-    if (hipEventRecord(c->ring_fork, s) != hipSuccess || hipStreamWaitEvent(rs_, c->ring_fork, 0) != hipSuccess)
-        return GEO_EHIP;
-    if (c->ring_free_rec && c->ring_free_stream != s && hipStreamWaitEvent(rs_, c->ring_free, 0) != hipSuccess)
-        return GEO_EHIP;
-    if (c->ring_open && hipMemsetAsync(r.count, 0, sizeof(uint32_t), rs_) != hipSuccess) return GEO_EHIP;
-    c->ring_open = true;
-    const uint32_t scan_px = 8u * kRingScanTiles;
-    hipLaunchKernelGGL(geo_ring_scan, dim3((a.width + scan_px - 1u) / scan_px, (a.nrows + scan_px - 1u) / scan_px),
-                       dim3(64), 0, rs_, r);
-    hipLaunchKernelGGL(geo_ring_kernel, dim3(kRingBlocks), dim3(kRingThreads), 0, rs_, r);
-    if (hipGetLastError() != hipSuccess) return GEO_EHIP;
-    if (hipEventRecord(c->ring_join, rs_) != hipSuccess) return GEO_EHIP;
-    return GEO_OK;
-}
-
 static int render_impl(geo_ctx* c, const geo_frame* frames, uint32_t nframes, size_t out_frame_stride,
                        const geo_scene* scene, bool scene_per_frame, uint32_t width, uint32_t height, uint32_t row0, uint32_t nrows,
                        uint32_t band_rows, uint32_t band_stride, uint8_t* out_rgba8, uint8_t* out_mask,
@@ -1735,9 +1379,8 @@ static int render_impl(geo_ctx* c, const geo_frame* frames, uint32_t nframes, si
     if ((scene->flags & ~(GEO_FLAG_DEFER_STEPS | GEO_FLAG_COMPOSITE | GEO_FLAG_MIPS | GEO_FLAG_RING_F64)) != 0)
         return GEO_EINVAL;
     const bool ring_flag = (scene->flags & GEO_FLAG_RING_F64) != 0;
-    if (ring_flag && (scene->mode != GEO_MODE_DIRECT || nframes != 1 ||
-                      (scene->flags & (GEO_FLAG_COMPOSITE | GEO_FLAG_MIPS)) != 0 ||
-                      (uint64_t)nrows * width >= (1ull << 31)))  // the lists' 32-bit counts
+    if (ring_flag && (scene->mode == GEO_MODE_FAN || nframes != 1 ||
+                      (scene->flags & (GEO_FLAG_COMPOSITE | GEO_FLAG_MIPS)) != 0))
         return GEO_EINVAL;
     // frame-aligned 2 x 2 quads: the rows a wave covers start on even frame rows
     const bool mips = (scene->flags & GEO_FLAG_MIPS) != 0;
@@ -1836,6 +1479,9 @@ static int render_impl(geo_ctx* c, const geo_frame* frames, uint32_t nframes, si
             return GEO_EHIP;
         a.step_slots = c->step_slots + (size_t)(1 + call_set) * kSlotSetU64;
     }
+    // GEO_FLAG_RING_F64 (geo_band.h): the band's lanes take the f64 path; no
+    // capture orbit (rs = 0, or the observer inside the horizon): the plain draw
+    const bool ring = ring_flag && scene->rs > 0.0f && scene->r_obs > scene->rs;
     const int slot = render_slot(c, s);
     if (slot < 0) return GEO_EHIP;
     const hipEvent_t done = c->render_done[slot];
@@ -1847,8 +1493,9 @@ static int render_impl(geo_ctx* c, const geo_frame* frames, uint32_t nframes, si
             if (c->order_cur >= 0 && tiles_x == c->explicit_x && tiles_y == c->explicit_y)
                 a.tile_order = c->order[c->order_cur];
         } else if (c->dispatch_mode == GEO_DISPATCH_LONGEST_FIRST) {
-            const uint32_t key[9] = {width, height, row0, nrows, band_rows, band_stride, scene->mode, mips ? 1u : 0u,
-                                     tiles_x * tiles_y};
+            // (a GEO_FLAG_RING_F64 render learns its own order: its band's tiles cost more)
+            const uint32_t key[9] = {width, height, row0, nrows, band_rows, band_stride, scene->mode,
+                                     (mips ? 1u : 0u) | (ring ? 2u : 0u), tiles_x * tiles_y};
             if (!c->learn_valid || std::memcmp(key, c->learn_key, sizeof(key)) != 0) {
                 std::memcpy(c->learn_key, key, sizeof(key));
                 c->learn_valid = true;
@@ -1887,13 +1534,9 @@ static int render_impl(geo_ctx* c, const geo_frame* frames, uint32_t nframes, si
             if (c->order_cur >= 0) a.tile_order = c->order[c->order_cur];
         }
     }
-    // GEO_FLAG_RING_F64: the band's f64 redraw forks onto the context's ring
-    // stream before the f32 draw, so that its long f64 chains run beside it
-    const bool ring = ring_flag && scene->rs > 0.0f && scene->r_obs > scene->rs;
-    if (ring) {
-        const int rs = ring_fork(c, a, fk[0], *scene, s);
-        if (rs) return rs;
-    }
+    geo::BandConsts band_k;
+    if (ring) band_k = geo::band_consts(frames[0], *scene, width, height);
+    const geo::BandConsts* band = ring ? &band_k : nullptr;
     int st;
     if (scene->mode == GEO_MODE_FAN) {
         // after the solve that wrote the buffer (geo_ctx: on the solve's own
@@ -1919,34 +1562,18 @@ static int render_impl(geo_ctx* c, const geo_frame* frames, uint32_t nframes, si
         }
     } else if (adaptive) {
         switch (geo::geodesic_kind(a.k)) {
-            case geo::kCurvedOut: st = launch_frames<GEO_MODE_ADAPTIVE, geo::kCurvedOut>(a, fk, pk, nframes, mips, tiles_x, tiles_y, s, done, t_start, t_stop); break;
-            case geo::kCurvedIn: st = launch_frames<GEO_MODE_ADAPTIVE, geo::kCurvedIn>(a, fk, pk, nframes, mips, tiles_x, tiles_y, s, done, t_start, t_stop); break;
+            case geo::kCurvedOut: st = launch_frames<GEO_MODE_ADAPTIVE, geo::kCurvedOut>(a, fk, pk, nframes, mips, tiles_x, tiles_y, s, done, t_start, t_stop, band); break;
+            case geo::kCurvedIn: st = launch_frames<GEO_MODE_ADAPTIVE, geo::kCurvedIn>(a, fk, pk, nframes, mips, tiles_x, tiles_y, s, done, t_start, t_stop, band); break;
             default: st = launch_frames<GEO_MODE_ADAPTIVE, geo::kFlat>(a, fk, pk, nframes, mips, tiles_x, tiles_y, s, done, t_start, t_stop);
         }
     } else {
         switch (geo::geodesic_kind(a.k)) {
-            case geo::kCurvedOut: st = launch_frames<GEO_MODE_DIRECT, geo::kCurvedOut>(a, fk, pk, nframes, mips, tiles_x, tiles_y, s, done, t_start, t_stop); break;
-            case geo::kCurvedIn: st = launch_frames<GEO_MODE_DIRECT, geo::kCurvedIn>(a, fk, pk, nframes, mips, tiles_x, tiles_y, s, done, t_start, t_stop); break;
+            case geo::kCurvedOut: st = launch_frames<GEO_MODE_DIRECT, geo::kCurvedOut>(a, fk, pk, nframes, mips, tiles_x, tiles_y, s, done, t_start, t_stop, band); break;
+            case geo::kCurvedIn: st = launch_frames<GEO_MODE_DIRECT, geo::kCurvedIn>(a, fk, pk, nframes, mips, tiles_x, tiles_y, s, done, t_start, t_stop, band); break;
             default: st = launch_frames<GEO_MODE_DIRECT, geo::kFlat>(a, fk, pk, nframes, mips, tiles_x, tiles_y, s, done, t_start, t_stop);
         }
     }
     if (st) return st;
-    if (ring) {
-        // the redrawn pixels over the f32 draw; `done` then covers the ring
-        // kernel too (its sky reads), for geo_set_sky and the context's waits
-        if (hipStreamWaitEvent(s, c->ring_join, 0) != hipSuccess) return GEO_EHIP;
-        hipExtLaunchKernelGGL(geo_ring_scatter, dim3(kRingScatterBlocks), dim3(256), 0, s, nullptr, done, 0,
-                              static_cast<const RingEntry*>(c->ring_list), c->ring_count + c->ring_parity,
-                              (uint32_t)((size_t)a.nrows * a.width), c->ring_count + (1 - c->ring_parity), a.out_rgba,
-                              a.out_mask,
-                              a.out_uv, a.out_steps);
-        if (hipGetLastError() != hipSuccess) return GEO_EHIP;
-        if (hipEventRecord(c->ring_free, s) != hipSuccess) return GEO_EHIP;
-        c->ring_free_rec = true;
-        c->ring_free_stream = s;
-        c->ring_parity = 1 - c->ring_parity;
-        c->ring_open = false;
-    }
     if (record) {
         // rebuild the order into the buffer not in use, on the context's
         // learn stream, after every render of the context issued so far (this

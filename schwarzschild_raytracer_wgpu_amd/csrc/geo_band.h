@@ -48,12 +48,16 @@ struct BandConsts {
     double h, hh, hh2, hhh, h6, h2_6;  // step, step/2, step^2/4, step^2/2, step/6, step^2/6
     float kx;                 // r / (energy b_c) rounded once: the band test |kx cos(theta) - 1| (f32)
     uint32_t max_steps;
+    uint32_t above0;          // U0 > SU: the observer inside the sphere (the group exit's short form)
     uint32_t pf_always, pf_falling, pf_outgoing;  // the pre-filters' frame-uniform terms (:113-117)
     uint32_t m1_identity;
 };
 
 // The band test on the f32 draw's cos(theta) (central_rho).
-GEO_HD bool in_band(float kx, float ct) { return __builtin_fabsf(kx * ct - 1.0f) < GEO_RING_X; }
+#if !defined(GEO_BAND_X)  // (A/B variants only; the specification is GEO_RING_X)
+#define GEO_BAND_X GEO_RING_X
+#endif
+GEO_HD bool in_band(float kx, float ct) { return __builtin_fabsf(kx * ct - 1.0f) < GEO_BAND_X; }
 
 // Host: the constants for a frame and scene with rs > 0 and r_obs > rs.
 inline BandConsts band_consts(const geo_frame& f, const geo_scene& s, uint32_t width, uint32_t height) {
@@ -98,7 +102,8 @@ inline BandConsts band_consts(const geo_frame& f, const geo_scene& s, uint32_t w
     k.SU = c / sr;
     k.BD = c * (0.9 * __builtin_fmin(u0, 1.0 / __builtin_fmax(sr, r3_2)));
     k.HU = c / rs;
-    if (k.U0 > k.SU) {  // inside the sphere: stops below SU (crossing, escape) or above HU (horizon)
+    k.above0 = k.U0 > k.SU ? 1u : 0u;
+    if (k.above0) {  // inside the sphere: stops below SU (crossing, escape) or above HU (horizon)
         k.lo = __builtin_nextafter(k.SU, __builtin_inf());
         k.hi = k.HU;
     } else {  // outside it: stops above SU (crossing, horizon) or below BD (escape)
@@ -138,12 +143,41 @@ GEO_HD void band_rk4(double U, double V, double h, double hh, double hh2, double
 // of the reference's loop is at such a state: a crossing from inside the
 // sphere (U <= SU < lo), an escape (U < BD <= lo), the horizon test on the
 // state after a step (U > HU >= hi), a crossing from outside (U > SU >= hi).
-GEO_HD bool band_out(const BandConsts& k, double x) { return !(x >= k.lo) || x > k.hi; }
+GEO_HD bool band_out(const BandConsts& k, double x) { return !(x >= k.lo) | (x > k.hi); }
+
+// IEEE minNum of two doubles (a NaN operand yields the other) as one
+// v_min_f64 (hipcc would canonicalise both operands first; the states are
+// arithmetic results, never signaling NaNs).
+GEO_HD double min64_(double a, double b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    double r;
+    asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+#else
+    return __builtin_fmin(a, b);
+#endif
+}
+
+// The group exit for the four states u1..u4 of a group: true if any of them
+// is one band_out must look at.  Inside the sphere (above0) in five
+// operations: a state above hi = HU with U' > 0 keeps every later state
+// above it (U > 1 makes every RK4 stage slope U(U - 1) positive, so the map
+// raises U and U'), so only u4 needs the upper test; a state above hi with
+// U' <= 0 is no stop; below lo, the minimum of u1..u3 (a NaN state makes
+// every later one NaN, which u4's tests see: minNum skips NaN operands).
+GEO_HD bool band_group_out(const BandConsts& k, double u1, double u2, double u3, double u4) {
+    if (k.above0)
+        return (int)(min64_(min64_(u1, u2), u3) < k.lo) | (int)!(u4 >= k.lo) | (int)(u4 > k.hi);
+    return (int)band_out(k, u1) | (int)band_out(k, u2) | (int)band_out(k, u3) | (int)band_out(k, u4);
+}
 
 // The reference's main loop (sphere_ray_tracer.rs:134-191) from the scaled
-// state (U, V) at step `it` with `angle` traveled: its exits, its step count
-// (*steps = the RK4 steps taken) and Newton's refinement.
-GEO_HD double band_steps(const BandConsts& k, double U, double V, uint32_t it, double angle, uint32_t* steps) {
+// state (U, V) at step `it`: its exits, its step count (*steps = the RK4
+// steps taken) and Newton's refinement.  The traveled angle before step it,
+// the reference's `angle += step` summed it times, is it x step exactly:
+// step is an f32 value (24 significant bits), so every partial sum k step
+// (k < 2^24, at most 48 significant bits) is a double and no addition rounds.
+GEO_HD double band_steps(const BandConsts& k, double U, double V, uint32_t it, uint32_t* steps) {
     for (; it < k.max_steps; ++it) {
         if ((U > k.HU && V > 0.0) || !(U > 0.0)) {  // the loop test (:134-135)
             *steps = it;
@@ -169,7 +203,7 @@ GEO_HD double band_steps(const BandConsts& k, double U, double V, uint32_t it, d
                 band_rk4(U, V, ns, ns / 2.0, n2 / 4.0, n2 / 2.0, ns / 6.0, n2 / 6.0, &wu, &wv);
             }
             *steps = it + 1u;
-            return angle + ns;
+            return (double)it * k.h + ns;
         }
         if (NU < k.BD) {
             *steps = it + 1u;
@@ -177,7 +211,6 @@ GEO_HD double band_steps(const BandConsts& k, double U, double V, uint32_t it, d
         }
         U = NU;
         V = NV;
-        angle += k.h;
     }
     *steps = k.max_steps;
     return GEO_NO_VALUE;
@@ -222,23 +255,18 @@ GEO_HD double band_lambda(const BandConsts& k, uint32_t px, uint32_t py, uint32_
     // four RK4 steps per exit branch; a group with a state the exit must
     // look at is replayed step by step from its start (band_steps)
     uint32_t it = 0;
-    double angle = 0.0;
     while (it + 4u <= k.max_steps) {
         double u1, v1, u2, v2, u3, v3, u4, v4;
         band_rk4(U, V, k.h, k.hh, k.hh2, k.hhh, k.h6, k.h2_6, &u1, &v1);
         band_rk4(u1, v1, k.h, k.hh, k.hh2, k.hhh, k.h6, k.h2_6, &u2, &v2);
         band_rk4(u2, v2, k.h, k.hh, k.hh2, k.hhh, k.h6, k.h2_6, &u3, &v3);
         band_rk4(u3, v3, k.h, k.hh, k.hh2, k.hhh, k.h6, k.h2_6, &u4, &v4);
-        if (band_out(k, u1) || band_out(k, u2) || band_out(k, u3) || band_out(k, u4)) break;
+        if (band_group_out(k, u1, u2, u3, u4)) break;  // one exit branch per group
         U = u4;
         V = v4;
-        angle += k.h;
-        angle += k.h;
-        angle += k.h;
-        angle += k.h;
         it += 4u;
     }
-    return kHalfPi - band_steps(k, U, V, it, angle, steps);
+    return kHalfPi - band_steps(k, U, V, it, steps);
 }
 
 }  // namespace geo

@@ -279,7 +279,13 @@ struct BandArg<true> {
 // to 106 SGPRs (6 waves per SIMD instead of 8); from LDS they are loaded
 // where the band's lanes use them.
 constexpr uint32_t kBandDwords = (uint32_t)(sizeof(geo::BandConsts) / 4u);
-static_assert(sizeof(geo::BandConsts) % 8u == 0 && kBandDwords <= kBlock, "one dword per thread");
+// A ring render launches one wave per workgroup (the tile's four waves as
+// four workgroups): a wave with band lanes lives two to three times as long
+// as its tile's others, and a 4-wave workgroup keeps its finished waves'
+// slots from the next workgroup until it ends (config 3 +8.4 -> +7.4 %,
+// config 2 +15.0 -> +13.1 % over the plain frame, profiles/r06e_ring_wave_blocks_ab.txt).
+constexpr bool kRingWaveBlocks = true;
+static_assert(sizeof(geo::BandConsts) % 8u == 0 && kBandDwords / 2u <= 64u, "one 8-byte word per thread");
 
 // GEO_FLAG_MIPS epilogue: the pixel's UV and its quad footprint rho2 are
 // known; the trilinear sample in place of the level-0 one.
@@ -430,18 +436,24 @@ __global__ __launch_bounds__(kBlock) void geo_render_kernel(const RenderArgs a, 
     const uint32_t z = NF > 1 ? blockIdx.z : 0u;
     const FrameK& f = fb.f[z];
     const size_t obase = NF > 1 ? (size_t)z * a.out_frame_px : 0;
-    uint2 tile = make_uint2(blockIdx.x, a.tile_y0 + blockIdx.y);
+    // WB (RING, kRingWaveBlocks): one wave per workgroup, the tile's four
+    // waves as four consecutive workgroups (blockIdx.x = 4 tile.x + wave)
+    constexpr bool WB = RING && kRingWaveBlocks;
+    const uint32_t bx = WB ? blockIdx.x >> 2 : blockIdx.x;
+    const uint32_t tiles_x = WB ? gridDim.x >> 2 : gridDim.x;
+    uint2 tile = make_uint2(bx, a.tile_y0 + blockIdx.y);
     if (a.tile_order) {
-        const uint32_t t = a.tile_order[blockIdx.y * gridDim.x + blockIdx.x];  // one scalar load
+        const uint32_t t = a.tile_order[blockIdx.y * tiles_x + bx];  // one scalar load
         tile = make_uint2(t & 0xFFFFu, t >> 16);
     }
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x) >> 6;
+    const uint32_t wave = WB ? (blockIdx.x & 3u) : __builtin_amdgcn_readfirstlane(threadIdx.x) >> 6;
     const uint32_t lane = threadIdx.x & 63u;
     // RING: the band's constants in LDS (kBandDwords)
     __shared__ double band_lds[RING ? kBandDwords / 2u : 1u];
     if constexpr (RING) {
-        if (threadIdx.x < kBandDwords)
-            reinterpret_cast<uint32_t*>(band_lds)[threadIdx.x] = reinterpret_cast<const uint32_t*>(&bk.k)[threadIdx.x];
+        // one 8-byte word per thread (kBandDwords / 2 <= 64)
+        if (threadIdx.x < kBandDwords / 2u)
+            reinterpret_cast<uint2*>(band_lds)[threadIdx.x] = reinterpret_cast<const uint2*>(&bk.k)[threadIdx.x];
         __syncthreads();
     }
     const uint32_t px = tile.x * kTileW + (wave % kWavesX) * kWaveW + lane % kWaveW;
@@ -454,7 +466,7 @@ __global__ __launch_bounds__(kBlock) void geo_render_kernel(const RenderArgs a, 
     const uint32_t band = __umulhi(wl0, a.band_magic);
     const uint32_t py = a.row0 + band * a.band_stride + (wl0 - band * a.band_rows) + (ly - wl0);
     uint32_t steps = 0;
-    uint32_t cost_scale = 1u;  // RING: the band's lanes record their f64 steps at twice the cost
+    uint32_t cost_scale = 1u;  // RING: 2 on the band's lanes (their steps are f64)
     (void)cost_scale;
     const bool in_frame = px < a.width && ly < a.nrows && py < a.height;
     if constexpr (LR > 1) {
@@ -472,7 +484,10 @@ __global__ __launch_bounds__(kBlock) void geo_render_kernel(const RenderArgs a, 
                 // the other lanes) and take lambda' and the mask from the f64
                 // path; both then draw the sky from the f32 ray
                 const geo::BandConsts& bkl = *reinterpret_cast<const geo::BandConsts*>(band_lds);
-                const bool band = geo::in_band(bk.k.kx, ct);
+                const bool band = geo::in_band(bkl.kx, ct);
+#if defined(GEO_RING_PRIO)  // A/B variant: a wave with band lanes issues first
+                if (geo::ballot_(band) != 0) __builtin_amdgcn_s_setprio(GEO_RING_PRIO);
+#endif
                 float lam = 0.0f;
                 bool bh = false;
                 if (!band) {
@@ -539,9 +554,13 @@ __global__ __launch_bounds__(kBlock) void geo_render_kernel(const RenderArgs a, 
             // a wave holds its slot until its slowest lane stops: the tile's
             // cost is the sum of its waves' largest step counts (frame 0's
             // of a batch: the order is per tile)
-            const uint32_t wmax = wave_max_u32(RING ? steps * cost_scale : steps);
+            // (RING: a wave runs its f32 lanes' loop, then its band lanes'
+            // f64 loop at about twice the cost per step)
+            const uint32_t wmax = RING ? wave_max_u32(cost_scale == 1u ? steps : 0u) +
+                                             2u * wave_max_u32(cost_scale == 1u ? 0u : steps)
+                                       : wave_max_u32(steps);
             if ((threadIdx.x & 63) == 0)
-                atomicAdd(&a.tile_cost[tile.y * gridDim.x + tile.x], wmax + a.cost_overhead);
+                atomicAdd(&a.tile_cost[tile.y * tiles_x + tile.x], wmax + a.cost_overhead);
         }
     }
 #if defined(GEO_WAVE_LOG)
@@ -1271,8 +1290,13 @@ static int launch_tiles(RenderArgs a, const FrameBatch<NF>& fb, uint32_t nframes
                 if (band) {  // GEO_FLAG_RING_F64 (one frame, level-0 sampler)
                     BandArg<true> bk;
                     bk.k = *band;
-                    hipExtLaunchKernelGGL((geo_render_kernel<MODE, KIND, false, 1, true>), grid, dim3(kBlock), 0, s,
-                                          start, stop, 0, a, fb, bk);
+                    if (kRingWaveBlocks)
+                        hipExtLaunchKernelGGL((geo_render_kernel<MODE, KIND, false, 1, true>),
+                                              dim3(grid.x * 4u, grid.y, grid.z), dim3(64), 0, s, start, stop, 0, a, fb,
+                                              bk);
+                    else
+                        hipExtLaunchKernelGGL((geo_render_kernel<MODE, KIND, false, 1, true>), grid, dim3(kBlock), 0,
+                                              s, start, stop, 0, a, fb, bk);
                     if (hipGetLastError() != hipSuccess) return GEO_EHIP;
                     continue;
                 }

@@ -159,11 +159,12 @@ PY
           for xa in "${argsets[@]}"; do
             for v in $libs; do
               cp "$v" "$LIB"
-              timeout -k 10 300 python3 bench.py $cargs $xa --no-cpu-baseline --steps 200 > "$OUT/ab.json" 2> "$OUT/ab.err"
+              GEO_AB_VARIANT=1 timeout -k 10 300 python3 bench.py $cargs $xa --no-cpu-baseline --steps 200 > "$OUT/ab.json" 2> "$OUT/ab.err"
               rc=$?; [ $rc -eq 0 ] || { tail -5 "$OUT/ab.err"; cp "$OUT/.orig.so" "$LIB"; exit $rc; }
               python3 -c "
 import json,sys; d=json.loads(open(sys.argv[1]).read().splitlines()[-1])
-print('%-14s %-44s %-28s rep%s  ms/frame %.5f  kernel %.5f  frac %.4f  frame_check %s' % (sys.argv[2], sys.argv[5], sys.argv[3].split('/')[-1], sys.argv[4], d['ms_per_step'], d['kernel_ms']['avg'], d['roofline']['frac'], (d.get('frame_check') or {}).get('ok')))" \
+r=d.get('ring_f64') or {}
+print('%-14s %-44s %-28s rep%s  ms/frame %.5f  kernel %.5f  frac %.4f  frame_check %s  ring %s' % (sys.argv[2], sys.argv[5], sys.argv[3].split('/')[-1], sys.argv[4], d['ms_per_step'], d['kernel_ms']['avg'], d['roofline']['frac'], (d.get('frame_check') or {}).get('ok'), ('%.5f/%.5f %+.4f' % (r['ms_per_step'], r['plain_ms_per_step'], r['overhead'])) if r else '-'))" \
                 "$OUT/ab.json" "$c" "$v" "$rep" "${xa:--}" | tee -a "$OUT/ab.txt"
             done
           done

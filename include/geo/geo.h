@@ -43,9 +43,12 @@
 extern "C" {
 #endif
 
-#define GEO_ABI_VERSION 6  /* 4: geo_render_band_set_frames, geo_assemble_shares;
+#define GEO_ABI_VERSION 7  /* 4: geo_render_band_set_frames, geo_assemble_shares;
                                 5: geo_render_band_set_batch, geo_dispatch_stats;
-                                6: GEO_FLAG_RING_F64 */
+                                6: GEO_FLAG_RING_F64;
+                                7: GEO_FLAG_RING_F64 inside the render kernel (any stream,
+                                   no context memory), in GEO_MODE_ADAPTIVE too; steps_total
+                                   counts the band's f64 steps */
 
 typedef enum geo_status {
     GEO_OK = 0,
@@ -84,21 +87,23 @@ typedef enum geo_status {
                                    level-0 bilinear sample otherwise).  Quads are frame-
                                    aligned, so row0 must be even (GEO_EINVAL otherwise);
                                    band layouts keep bands 8-row aligned. */
-#define GEO_FLAG_RING_F64 8u    /* (off on the benchmarked path) GEO_MODE_DIRECT only: the
-                                   pixels next to the capture orbit, |b/b_c - 1| <
-                                   GEO_RING_X by the f32 ray (b = r_obs cos(theta) /
-                                   sqrt(1 - rs/r_obs), b_c = 3 sqrt(3) rs / 2; rs > 0,
-                                   r_obs > rs), are drawn again in f64 -- the camera ray,
-                                   solve_geodesic and the sky direction, as the literal
-                                   f64 restatement does -- on a context side stream
-                                   concurrently with the f32 draw, and written over it
-                                   (RGBA, mask, UV, per-pixel steps) after both.  There
-                                   the orbit amplifies the f32 roundings past the 1e-4 UV
-                                   bar.  steps_total keeps counting the f32
-                                   draw's steps.  The context keeps 36 bytes per
-                                   pixel of its largest such render (the band's
-                                   lists).  Not with GEO_FLAG_COMPOSITE,
-                                   GEO_FLAG_MIPS, more than one frame or 2^31 pixels
+#define GEO_FLAG_RING_F64 8u    /* (off on the benchmarked path) GEO_MODE_DIRECT or
+                                   GEO_MODE_ADAPTIVE: the pixels next to the capture orbit,
+                                   |b/b_c - 1| < GEO_RING_X by the f32 ray (b = r_obs
+                                   cos(theta) / sqrt(1 - rs/r_obs), b_c = 3 sqrt(3) rs / 2;
+                                   rs > 0, r_obs > rs), take their traveled angle from an
+                                   f64 path inside the render kernel: the camera ray, the
+                                   reference's set-up and fixed-step RK4 loop at
+                                   geo_scene.step (with its exits, step count and Newton,
+                                   sphere_ray_tracer.rs:38-191) in f64; the mask is decided
+                                   in f64, the sky drawn from the f32 ray with lambda'
+                                   rounded to f32 (geo_band.h).  There the orbit amplifies
+                                   the f32 roundings (and, in the adaptive mode, its
+                                   tolerance) past the 1e-4 UV bar.  The
+                                   band's out_steps and steps_total are its f64 steps.  A
+                                   ring render launches one wave per workgroup and keeps
+                                   no state in the context.  Not with GEO_MODE_FAN,
+                                   GEO_FLAG_COMPOSITE, GEO_FLAG_MIPS or more than one frame
                                    (GEO_EINVAL). */
 #define GEO_RING_X 8e-3f
 
@@ -144,6 +149,10 @@ typedef struct geo_ctx geo_ctx;
 typedef struct geo_observer geo_observer;
 
 /* ---- library ---------------------------------------------------------- */
+/* Every call that launches device work first clears the calling thread's HIP
+ * last-error state (hipGetLastError), so that an earlier, unrelated failure
+ * of the caller is not reported as the call's: a caller that checks its own
+ * launches with hipGetLastError must do so before calling into libgeo. */
 int geo_abi_version(void);
 const char* geo_status_str(int status);
 

@@ -292,8 +292,8 @@ class BasicSphereBuffer : public SchwarzschildSphereShaderDraw {
     // mipmaps: sample the texture's 4-level mip chain trilinearly as the
     // reference's textureSample does (Texture::new_with_mipmaps(..., 4),
     // GEO_FLAG_MIPS); off, the level-0 bilinear sample the benchmark measures.
-    // ring_f64: the capture band's pixels redrawn in f64 (GEO_FLAG_RING_F64:
-    // direct mode, the level-0 sampler, the pass's first sphere).
+    // ring_f64: the capture band's lanes integrate in f64 (GEO_FLAG_RING_F64:
+    // direct or adaptive mode, the level-0 sampler, the pass's first sphere).
     BasicSphereBuffer(int device, double sphere_radius, double schwarz_radius, const Image& texture_image,
                       uint32_t mode = GEO_MODE_DIRECT, uint32_t max_iter = MAX_ITER, double step = STEP,
                       bool mipmaps = false, bool ring_f64 = false)

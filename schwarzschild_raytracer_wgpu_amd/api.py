@@ -364,8 +364,8 @@ class BasicSphereBuffer:
         """mipmaps: sample the texture's 4-level mip chain trilinearly, as the
         reference's textureSample does (Texture::new_with_mipmaps(..., 4),
         GEO_FLAG_MIPS); off, the level-0 bilinear sample the benchmark measures.
-        ring_f64: redraw the capture band's pixels in f64 (GEO_FLAG_RING_F64:
-        direct mode, the level-0 sampler, not as a composited sphere)."""
+        ring_f64: the capture band's lanes integrate in f64 (GEO_FLAG_RING_F64:
+        direct or adaptive mode, the level-0 sampler, not as a composited sphere)."""
         ctx = Context(ctx) if isinstance(ctx, int) else ctx
         self.ctx = ctx
         self.mipmaps = mipmaps

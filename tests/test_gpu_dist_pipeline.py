@@ -69,7 +69,8 @@ def _peer_bands(ctx, torch, frame, scene, W, H, B, r, world, lead, dev, bpp, pb=
 @pytest.mark.parametrize("world,K,nframes,lead", [(2, 4, 41, 1), (3, 3, 10, 1), (8, 4, 16, 1), (8, 1, 5, 1),
                                                   (2, 4, 13, 2), (2, 2, 7, 4), (4, 3, 10, 2), (8, 4, 9, 2),
                                                   (8, 2, 6, 4), (2, 3, 8, 3), (8, 4, 9, 3), (4, 2, 5, 6),
-                                                  (8, 4, 9, (3, 2)), (4, 3, 7, (5, 2)), (2, 2, 5, (3, 2))])
+                                                  (8, 4, 9, (3, 2)), (4, 3, 7, (5, 2)), (2, 2, 5, (3, 2)),
+                                                  (4, 4, 9, (3, 2))])
 def test_rank0_pipeline_assembles_frames(world, K, nframes, lead, S, rgb, batch):
     import torch
 

@@ -199,6 +199,55 @@ def test_ring_config_frame_meets_the_bar_everywhere(geo, torch_mod, cfgname):
     ctx.close()
 
 
+def test_ring_config5_meets_the_bar_against_the_fine_reference(geo, torch_mod):
+    """Config 5 (8K, adaptive RK5(4), observer inside the photon sphere) with
+    the flag, against the adaptive mode's own f64 check (fixed RK4 at
+    step/32) on every 54th row, with no model band: no mask flip, and every
+    sky pixel within the 1e-4 UV bar except at the poles (|latitude| > 89
+    deg, where U's sensitivity to the direction, 1/(2 pi cos lat), is over 9x
+    the equator's).  Without the flag the same rows have pixels over the bar
+    next to the orbit (the adaptive tolerance's error there)."""
+    from schwarzschild_raytracer_wgpu_amd.scenes import CONFIGS, make_sky
+
+    torch = torch_mod
+    cfg = CONFIGS["cfg5_8k_adaptive"]
+    w, h = cfg.width, cfg.height
+    obs = geo.Observer(cfg.rs, cfg.fov, w, h)
+    obs.set_position(*cfg.position)
+    obs.set_camera(*cfg.camera)
+    obs.set_energy(cfg.energy)
+    frame = obs.calc_transformation_pipeline()
+    r = obs.get_radial_position()
+    scene = geo.make_scene(cfg.rs, cfg.sphere_r, r, cfg.step, cfg.max_steps, geo.GEO_MODE_ADAPTIVE, tol=cfg.tol)
+    ctx = geo.Context(0)
+    ctx.set_sky(make_sky("equirect", (512, 256)))
+    dev = torch.device("cuda:0")
+    row_step = 54
+    row0 = row_step // 2
+    nrows = (h - row0 + row_step - 1) // row_step
+    fine = B.f64_rows(frame, scene, w, h, row0, nrows, row_step)
+    lat = np.pi * (0.5 - fine["uv"][..., 1].astype(np.float64))
+    pole = np.abs(lat) > np.radians(89.0)
+    res = {}
+    for name, sc in (("plain", scene), ("ring", _ring(geo, scene))):
+        rgba = torch.empty(h * w * 4, dtype=torch.uint8, device=dev)
+        mask = torch.empty(h * w, dtype=torch.uint8, device=dev)
+        uv = torch.empty(h * w * 2, dtype=torch.float32, device=dev)
+        ctx.render_rows(frame, sc, w, h, 0, h, rgba, mask, uv)
+        torch.cuda.synchronize()
+        m = mask.view(h, w)[row0::row_step].cpu().numpy()
+        u = uv.view(h, w, 2)[row0::row_step].cpu().numpy()
+        sky = (m == 0) & (fine["mask"] == 0)
+        e = B.uv_err(u, fine["uv"])
+        res[name] = {"flips": int((m != fine["mask"]).sum()), "over": int((sky & ~pole & (e > B.UV_BAR)).sum()),
+                     "uv_max_off_pole": float(e[sky & ~pole].max()), "pole_pixels": int((sky & pole).sum())}
+    print("config 5 vs f64 step/32:", res)
+    assert res["ring"]["flips"] == 0
+    assert res["ring"]["over"] == 0
+    assert res["plain"]["over"] > 0 or res["plain"]["flips"] > 0  # the band's adaptive error, fixed by the flag
+    ctx.close()
+
+
 def test_ring_rejects_what_it_does_not_draw(geo, torch_mod):
     import ctypes
 

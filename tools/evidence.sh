@@ -8,7 +8,7 @@
 # STEPs:
 #   suite            pytest -m gpu (one process) + smoke()
 #   tests:<k-expr>   pytest -m gpu -k <k-expr>
-#   gloo8            the driver's N = 8 form on this one GPU with gloo:
+#   gloo8 | gloo:N   the driver's N-rank form (N = 8 for gloo8) on this one GPU with gloo:
 #                    bench.py --gpus 8 --dist-backend gloo --steps 20 --warmup 5
 #                    (self-launcher, --rank0-lead auto, batched launches,
 #                    frame_check), its wall time recorded
@@ -52,30 +52,32 @@ for step in "$@"; do
       timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "$a1" \
         > "$OUT/tests_${a1//[^A-Za-z0-9_]/_}.txt" 2>&1
       rc=$?; tail -3 "$OUT/tests_${a1//[^A-Za-z0-9_]/_}.txt"; [ $rc -eq 0 ] || exit $rc ;;
-    gloo8)
+    gloo8|gloo)
+      # the driver's N-rank form on this one GPU with gloo (gloo8 = gloo:8)
+      n=${a1:-8}; [ $kind = gloo8 ] && n=8
       heartbeat
       t0=$(date +%s.%N)
-      timeout -k 10 1000 python3 bench.py --gpus 8 --dist-backend gloo --steps 20 --warmup 5 \
-        > "$OUT/gloo8_bench.json" 2> "$OUT/gloo8_bench.err"
+      timeout -k 10 1000 python3 bench.py --gpus $n --dist-backend gloo --steps 20 --warmup 5 \
+        > "$OUT/gloo${n}_bench.json" 2> "$OUT/gloo${n}_bench.err"
       rc=$?
       t1=$(date +%s.%N)
       stop_heartbeat
-      python3 - "$OUT" "$t0" "$t1" "$rc" <<'EOF'
+      python3 - "$OUT" "$t0" "$t1" "$rc" "$n" <<'EOF'
 import json, sys
-out, t0, t1, rc = sys.argv[1], float(sys.argv[2]), float(sys.argv[3]), int(sys.argv[4])
-rec = {"cmd": "python3 bench.py --gpus 8 --dist-backend gloo --steps 20 --warmup 5", "rc": rc,
+out, t0, t1, rc, n = sys.argv[1], float(sys.argv[2]), float(sys.argv[3]), int(sys.argv[4]), int(sys.argv[5])
+rec = {"cmd": f"python3 bench.py --gpus {n} --dist-backend gloo --steps 20 --warmup 5", "rc": rc,
        "wall_s": round(t1 - t0, 2), "driver_timeout_s": 600}
 try:
-    d = json.loads(open(out + "/gloo8_bench.json").read().strip().splitlines()[-1])
+    d = json.loads(open(f"{out}/gloo{n}_bench.json").read().strip().splitlines()[-1])
     rec.update({k: d[k] for k in ("n_gpus", "world_size", "dist_backend", "value", "ms_per_step", "frame_check")})
     rec["config"] = d["config"]
     rec["per_rank"] = d["per_rank"]
 except Exception as e:  # noqa: BLE001
     rec["parse_error"] = repr(e)
-json.dump(rec, open(out + "/gloo8_summary.json", "w"), indent=1)
+json.dump(rec, open(f"{out}/gloo{n}_summary.json", "w"), indent=1)
 print(json.dumps({k: rec.get(k) for k in ("rc", "wall_s", "frame_check")}))
 EOF
-      [ $rc -eq 0 ] || { tail -20 "$OUT/gloo8_bench.err"; exit $rc; } ;;
+      [ $rc -eq 0 ] || { tail -20 "$OUT/gloo${n}_bench.err"; exit $rc; } ;;
     bench|plain)
       cfg=${a1:-cfg3_4k}; mode=${a2:-}; steps=${a3:-20}
       margs="--config $cfg --steps $steps --warmup 5 ${BENCH_ARGS:-}"; [ -n "$mode" ] && margs="$margs --mode $mode"

@@ -39,6 +39,10 @@ def main():
     p.add_argument("--threads", type=int, default=os.cpu_count() or 8)
     p.add_argument("--chunk", type=int, default=216, help="rows per oracle call (bounds memory)")
     p.add_argument("--ring", action="store_true", help="GEO_FLAG_RING_F64: the band's pixels in f64 (geo.h)")
+    p.add_argument("--fine", action="store_true",
+                   help="adaptive configs: against the fine f64 reference (fixed RK4 at step/32, oracle pixel_f64 "
+                        "in the adaptive mode) instead of the fixed-step literal")
+    p.add_argument("--row-step", type=int, default=1, help="every k-th row (1: all)")
     p.add_argument("--out", default=None)
     a = p.parse_args()
     res = {}
@@ -57,26 +61,34 @@ def main():
         if a.ring:
             scene.flags |= g._lib.GEO_FLAG_RING_F64
         literal = g.make_scene(cfg.rs, cfg.sphere_r, r, cfg.step, cfg.max_steps, g.GEO_MODE_DIRECT)
+        if a.fine and mode == g.GEO_MODE_ADAPTIVE:
+            literal = g.make_scene(cfg.rs, cfg.sphere_r, r, cfg.step, cfg.max_steps, mode, tol=cfg.tol)
         sky = make_sky(cfg.sky, (64, 32))  # the UV and mask do not depend on the sky
         t0 = time.time()
-        mask = np.empty((h, w), np.uint8)
-        uv = np.empty((h, w, 2), np.float32)
-        ref = {"mask": np.empty((h, w), np.uint8), "uv": np.empty((h, w, 2), np.float32),
-               "theta": np.empty((h, w), np.float64)}
-        for r0 in range(0, h, a.chunk):
-            n = min(a.chunk, h - r0)
-            f32 = O.render_f32(frame, scene, sky, w, h, row0=r0, nrows=n, threads=a.threads, want_steps=False)
-            mask[r0:r0 + n], uv[r0:r0 + n] = f32["mask"], f32["uv"]
-            f64 = O.render_f64(frame, literal, w, h, row0=r0, nrows=n, threads=a.threads)
+        k_ = a.row_step
+        hs = (h + k_ - 1) // k_  # sampled rows 0, k, 2k, ...
+        mask = np.empty((hs, w), np.uint8)
+        uv = np.empty((hs, w, 2), np.float32)
+        ref = {"mask": np.empty((hs, w), np.uint8), "uv": np.empty((hs, w, 2), np.float32),
+               "theta": np.empty((hs, w), np.float64)}
+        for i0 in range(0, hs, a.chunk):
+            n = min(a.chunk, hs - i0)
+            f32 = O.render_f32(frame, scene, sky, w, h, row0=i0 * k_, nrows=n, row_step=k_, threads=a.threads,
+                               want_steps=False)
+            mask[i0:i0 + n], uv[i0:i0 + n] = f32["mask"], f32["uv"]
+            f64 = O.render_f64(frame, literal, w, h, row0=i0 * k_, nrows=n, row_step=k_, threads=a.threads)
             for k in ref:
-                ref[k][r0:r0 + n] = f64[k]
+                ref[k][i0:i0 + n] = f64[k]
         st = B.compare(mask, uv, ref, cfg.rs, r)
         x, _, _ = B.model(ref["theta"], ref["uv"], cfg.rs, r)
         e = B.uv_err(uv, ref["uv"])
         sky_px = (mask == 0) & (ref["mask"] == 0)
         over = sky_px & (e > B.UV_BAR)
-        band = O.ring_band(frame, scene, w, h).astype(bool) if a.ring else np.zeros((h, w), bool)
-        st.update(config=name, rows=f"all {h} rows", ring_f64=a.ring, ring_pixels=int(band.sum()), reference="f64 literal, step pi/100",
+        band = (O.ring_band(frame, scene, w, h, 0, hs, k_).astype(bool) if a.ring else np.zeros((hs, w), bool))
+        fine = a.fine and mode == g.GEO_MODE_ADAPTIVE
+        st.update(config=name, rows=f"all {h} rows" if k_ == 1 else f"every {k_}th row ({hs})", ring_f64=a.ring,
+                  ring_pixels=int(band.sum()),
+                  reference="f64 RK4 at step/32 (the adaptive mode's own check)" if fine else "f64 literal, step pi/100",
                   side="oracle f32 mirror (= HIP bit for bit)", seconds=round(time.time() - t0, 1),
                   pixels_over_bar=int(over.sum()),
                   min_abs_x=float(np.min(x)) if np.isfinite(x).any() else None,

@@ -285,6 +285,11 @@ constexpr uint32_t kBandDwords = (uint32_t)(sizeof(geo::BandConsts) / 4u);
 // slots from the next workgroup until it ends (config 3 +8.4 -> +7.4 %,
 // config 2 +15.0 -> +13.1 % over the plain frame, profiles/r06e_ring_wave_blocks_ab.txt).
 constexpr bool kRingWaveBlocks = true;
+// The same for a plain one-frame direct-mode render (tiles differ ~30x in
+// cost, and its waves' lifetimes within a tile differ too): config 3
+// -0.7 %, config 2 -1 % per frame; the adaptive mode measured +0.8 % and
+// keeps 4-wave workgroups (profiles/r06h_all_wave_blocks_ab.txt)
+constexpr bool kDirectWaveBlocks = true;
 static_assert(sizeof(geo::BandConsts) % 8u == 0 && kBandDwords / 2u <= 64u, "one 8-byte word per thread");
 
 // GEO_FLAG_MIPS epilogue: the pixel's UV and its quad footprint rho2 are
@@ -438,7 +443,7 @@ __global__ __launch_bounds__(kBlock) void geo_render_kernel(const RenderArgs a, 
     const size_t obase = NF > 1 ? (size_t)z * a.out_frame_px : 0;
     // WB (RING, kRingWaveBlocks): one wave per workgroup, the tile's four
     // waves as four consecutive workgroups (blockIdx.x = 4 tile.x + wave)
-    constexpr bool WB = RING && kRingWaveBlocks;
+    constexpr bool WB = (RING && kRingWaveBlocks) || (kDirectWaveBlocks && MODE == GEO_MODE_DIRECT && !MIPS && NF == 1);
     const uint32_t bx = WB ? blockIdx.x >> 2 : blockIdx.x;
     const uint32_t tiles_x = WB ? gridDim.x >> 2 : gridDim.x;
     uint2 tile = make_uint2(bx, a.tile_y0 + blockIdx.y);
@@ -568,7 +573,7 @@ __global__ __launch_bounds__(kBlock) void geo_render_kernel(const RenderArgs a, 
         const uint32_t wmax = wave_max_u32(steps);
         const unsigned long long t_wave1 = __builtin_amdgcn_s_memrealtime();
         if ((threadIdx.x & 63) == 0) {
-            const size_t wg = ((size_t)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+            const size_t wg = ((size_t)blockIdx.z * gridDim.y + blockIdx.y) * tiles_x + bx;  // the tile, in launch order
             unsigned long long* p = a.wave_log + (wg * (kBlock / 64) + wave) * 4;
             const uint32_t hw_id = __builtin_amdgcn_s_getreg((31 << 11) | 4);  // HW_REG_HW_ID
             const uint32_t xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20);    // HW_REG_XCC_ID[3:0]
@@ -1304,6 +1309,10 @@ static int launch_tiles(RenderArgs a, const FrameBatch<NF>& fb, uint32_t nframes
             if (mips)
                 hipExtLaunchKernelGGL((geo_render_kernel<MODE, KIND, true, 1, false>), grid, dim3(kBlock), 0, s,
                                       start, stop, 0, a, fb, BandArg<false>{});
+            else if (kDirectWaveBlocks && MODE == GEO_MODE_DIRECT)
+                hipExtLaunchKernelGGL((geo_render_kernel<MODE, KIND, false, 1, false>),
+                                      dim3(grid.x * 4u, grid.y, grid.z), dim3(64), 0, s, start, stop, 0, a, fb,
+                                      BandArg<false>{});
             else
                 hipExtLaunchKernelGGL((geo_render_kernel<MODE, KIND, false, 1, false>), grid, dim3(kBlock), 0, s,
                                       start, stop, 0, a, fb, BandArg<false>{});

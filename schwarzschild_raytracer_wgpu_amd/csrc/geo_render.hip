@@ -18,6 +18,7 @@
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstring>
 #include <new>
@@ -94,6 +95,7 @@ struct RenderArgs {
     geo::PixelConsts k;  // scene constants, evaluated once on the host (IEEE f32, same bits)
     uint32_t width, height, row0, nrows;
     uint32_t tile_y0;  // first tile row of this launch (launch_tiles)
+    uint32_t tiles_x, launch_tiles;  // the frame's tiles per row; the tiles of this launch (wave_blocks)
     // dispatch order (geo_ctx): workgroup i draws tile
     // (order[i] & 0xFFFF, order[i] >> 16); null = row-major
     const uint32_t* tile_order;
@@ -290,6 +292,20 @@ constexpr bool kRingWaveBlocks = true;
 // -0.7 %, config 2 -1 % per frame; the adaptive mode measured +0.8 % and
 // keeps 4-wave workgroups (profiles/r06h_all_wave_blocks_ab.txt)
 constexpr bool kDirectWaveBlocks = true;
+// The four waves of a tile on one XCD (its L2 holds the tile's sky lines):
+// against four consecutive workgroups (on four XCDs), config 3 -0.6 to
+// -0.8 %, config 2 -0.8 % (profiles/r06k_wave_block_layout_ab.txt)
+#if defined(GEO_WB_XCD)
+constexpr bool kWaveBlocksXcd = GEO_WB_XCD != 0;
+#else
+constexpr bool kWaveBlocksXcd = true;
+#endif
+__host__ __device__ constexpr bool wave_blocks(int mode, bool mips, uint32_t nf, bool ring) {
+    return (ring && kRingWaveBlocks) || (kDirectWaveBlocks && mode == GEO_MODE_DIRECT && !mips && nf == 1);
+}
+// WB's 1-D grid for a launch of n tiles (n <= kMaxWaveBlockTiles: at most 2^31 workgroups)
+constexpr uint32_t kMaxWaveBlockTiles = 1u << 26;
+inline uint32_t wave_block_count(uint32_t n) { return kWaveBlocksXcd ? (n + 7u) / 8u * 32u : 4u * n; }
 static_assert(sizeof(geo::BandConsts) % 8u == 0 && kBandDwords / 2u <= 64u, "one 8-byte word per thread");
 
 // GEO_FLAG_MIPS epilogue: the pixel's UV and its quad footprint rho2 are
@@ -441,17 +457,34 @@ __global__ __launch_bounds__(kBlock) void geo_render_kernel(const RenderArgs a, 
     const uint32_t z = NF > 1 ? blockIdx.z : 0u;
     const FrameK& f = fb.f[z];
     const size_t obase = NF > 1 ? (size_t)z * a.out_frame_px : 0;
-    // WB (RING, kRingWaveBlocks): one wave per workgroup, the tile's four
-    // waves as four consecutive workgroups (blockIdx.x = 4 tile.x + wave)
-    constexpr bool WB = (RING && kRingWaveBlocks) || (kDirectWaveBlocks && MODE == GEO_MODE_DIRECT && !MIPS && NF == 1);
-    const uint32_t bx = WB ? blockIdx.x >> 2 : blockIdx.x;
-    const uint32_t tiles_x = WB ? gridDim.x >> 2 : gridDim.x;
-    uint2 tile = make_uint2(bx, a.tile_y0 + blockIdx.y);
-    if (a.tile_order) {
-        const uint32_t t = a.tile_order[blockIdx.y * tiles_x + bx];  // one scalar load
-        tile = make_uint2(t & 0xFFFFu, t >> 16);
+    // WB (wave_blocks): one wave per workgroup, on a 1-D grid: workgroup L
+    // draws wave w of the tile at dispatch position p (p indexes the order,
+    // or the launch's tiles row-major).  kWaveBlocksXcd: the hardware deals
+    // workgroups to the 8 XCDs round-robin (L mod 8), so the four waves of a
+    // tile are put 8 apart (p = 8 (L / 32) + L mod 8, w = (L / 8) mod 4) and
+    // share their XCD's L2 for the tile's sky lines; the grid is padded to
+    // whole groups of 8 tiles.  Otherwise p = L / 4, w = L mod 4.
+    constexpr bool WB = wave_blocks(MODE, MIPS, NF, RING);
+    uint32_t pos, wave;
+    if constexpr (WB) {
+        const uint32_t L = blockIdx.x;
+        pos = kWaveBlocksXcd ? ((L >> 5) << 3) + (L & 7u) : L >> 2;
+        wave = kWaveBlocksXcd ? (L >> 3) & 3u : L & 3u;
+        if (pos >= a.launch_tiles) return;  // the padding of the last group (a whole workgroup)
+    } else {
+        pos = blockIdx.y * gridDim.x + blockIdx.x;
+        wave = __builtin_amdgcn_readfirstlane(threadIdx.x) >> 6;
     }
-    const uint32_t wave = WB ? (blockIdx.x & 3u) : __builtin_amdgcn_readfirstlane(threadIdx.x) >> 6;
+    const uint32_t tiles_x = WB ? a.tiles_x : gridDim.x;
+    uint2 tile;
+    if (a.tile_order) {
+        const uint32_t t = a.tile_order[pos];  // one scalar load
+        tile = make_uint2(t & 0xFFFFu, t >> 16);
+    } else if constexpr (WB) {
+        tile = make_uint2(pos % tiles_x, a.tile_y0 + pos / tiles_x);
+    } else {
+        tile = make_uint2(blockIdx.x, a.tile_y0 + blockIdx.y);
+    }
     const uint32_t lane = threadIdx.x & 63u;
     // RING: the band's constants in LDS (kBandDwords)
     __shared__ double band_lds[RING ? kBandDwords / 2u : 1u];
@@ -573,7 +606,7 @@ __global__ __launch_bounds__(kBlock) void geo_render_kernel(const RenderArgs a, 
         const uint32_t wmax = wave_max_u32(steps);
         const unsigned long long t_wave1 = __builtin_amdgcn_s_memrealtime();
         if ((threadIdx.x & 63) == 0) {
-            const size_t wg = ((size_t)blockIdx.z * gridDim.y + blockIdx.y) * tiles_x + bx;  // the tile, in launch order
+            const size_t wg = (size_t)blockIdx.z * (WB ? a.launch_tiles : gridDim.x * gridDim.y) + pos;  // the tile, in launch order
             unsigned long long* p = a.wave_log + (wg * (kBlock / 64) + wave) * 4;
             const uint32_t hw_id = __builtin_amdgcn_s_getreg((31 << 11) | 4);  // HW_REG_HW_ID
             const uint32_t xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20);    // HW_REG_XCC_ID[3:0]
@@ -1283,9 +1316,14 @@ template <int MODE, int KIND, uint32_t NF>
 static int launch_tiles(RenderArgs a, const FrameBatch<NF>& fb, uint32_t nframes, bool mips, uint32_t tiles_x,
                         uint32_t tiles_y, hipStream_t s, hipEvent_t done, hipEvent_t t_start, hipEvent_t t_stop,
                         const geo::BandConsts* band) {
-    for (uint32_t y0 = 0; y0 < tiles_y; y0 += kMaxGridY) {
+    a.tiles_x = tiles_x;
+    // rows of tiles per launch: the 2-D grid's y limit, and WB's 1-D limit
+    const bool wb = NF == 1 && !mips && (band ? kRingWaveBlocks : wave_blocks(MODE, false, 1, false));
+    const uint32_t max_ny = wb ? std::min(kMaxGridY, kMaxWaveBlockTiles / tiles_x) : kMaxGridY;
+    for (uint32_t y0 = 0; y0 < tiles_y; y0 += max_ny) {
         a.tile_y0 = y0;
-        const uint32_t ny = tiles_y - y0 < kMaxGridY ? tiles_y - y0 : kMaxGridY;
+        const uint32_t ny = tiles_y - y0 < max_ny ? tiles_y - y0 : max_ny;
+        a.launch_tiles = tiles_x * ny;
         const bool last = y0 + ny >= tiles_y;
         hipEvent_t start = y0 == 0 ? t_start : nullptr;
         hipEvent_t stop = last ? (t_stop ? t_stop : done) : nullptr;
@@ -1297,8 +1335,8 @@ static int launch_tiles(RenderArgs a, const FrameBatch<NF>& fb, uint32_t nframes
                     bk.k = *band;
                     if (kRingWaveBlocks)
                         hipExtLaunchKernelGGL((geo_render_kernel<MODE, KIND, false, 1, true>),
-                                              dim3(grid.x * 4u, grid.y, grid.z), dim3(64), 0, s, start, stop, 0, a, fb,
-                                              bk);
+                                              dim3(wave_block_count(a.launch_tiles)), dim3(64), 0, s, start, stop, 0,
+                                              a, fb, bk);
                     else
                         hipExtLaunchKernelGGL((geo_render_kernel<MODE, KIND, false, 1, true>), grid, dim3(kBlock), 0,
                                               s, start, stop, 0, a, fb, bk);
@@ -1309,9 +1347,9 @@ static int launch_tiles(RenderArgs a, const FrameBatch<NF>& fb, uint32_t nframes
             if (mips)
                 hipExtLaunchKernelGGL((geo_render_kernel<MODE, KIND, true, 1, false>), grid, dim3(kBlock), 0, s,
                                       start, stop, 0, a, fb, BandArg<false>{});
-            else if (kDirectWaveBlocks && MODE == GEO_MODE_DIRECT)
+            else if (wave_blocks(MODE, false, 1, false))
                 hipExtLaunchKernelGGL((geo_render_kernel<MODE, KIND, false, 1, false>),
-                                      dim3(grid.x * 4u, grid.y, grid.z), dim3(64), 0, s, start, stop, 0, a, fb,
+                                      dim3(wave_block_count(a.launch_tiles)), dim3(64), 0, s, start, stop, 0, a, fb,
                                       BandArg<false>{});
             else
                 hipExtLaunchKernelGGL((geo_render_kernel<MODE, KIND, false, 1, false>), grid, dim3(kBlock), 0, s,
@@ -1521,7 +1559,8 @@ static int render_impl(geo_ctx* c, const geo_frame* frames, uint32_t nframes, si
     // The dispatch order (geo_ctx): a learned or explicit order for exactly
     // this grid, one launch, not in fan mode (its tiles all cost the same).
     bool record = false;
-    if (scene->mode != GEO_MODE_FAN && tiles_y <= kMaxGridY) {
+    // (one launch for the whole grid: the 2-D grid's y limit, and WB's tile count)
+    if (scene->mode != GEO_MODE_FAN && tiles_y <= kMaxGridY && (uint64_t)tiles_x * tiles_y <= kMaxWaveBlockTiles) {
         if (c->dispatch_mode == GEO_DISPATCH_EXPLICIT) {
             if (c->order_cur >= 0 && tiles_x == c->explicit_x && tiles_y == c->explicit_y)
                 a.tile_order = c->order[c->order_cur];

@@ -25,7 +25,7 @@ import isa_blocks as IB  # noqa: E402
 import schwarzschild_raytracer_wgpu_amd as g  # noqa: E402
 from schwarzschild_raytracer_wgpu_amd.scenes import CONFIGS, make_sky  # noqa: E402
 
-SYM = "geo_render_kernelILi2ELi0ELb0E"
+SYM = "geo_render_kernelILi2ELi0ELb0ELj1ELb0E"
 
 
 # the correctly rounded sqrt/reciprocal/division fix-ups (geo_math.h) sit in

@@ -96,6 +96,7 @@ struct RenderArgs {
     uint32_t width, height, row0, nrows;
     uint32_t tile_y0;  // first tile row of this launch (launch_tiles)
     uint32_t tiles_x, launch_tiles;  // the frame's tiles per row; the tiles of this launch (wave_blocks)
+    uint32_t persist_blocks;         // kFanPersist: workgroups of the fan draw's grid
     // dispatch order (geo_ctx): workgroup i draws tile
     // (order[i] & 0xFFFF, order[i] >> 16); null = row-major
     const uint32_t* tile_order;
@@ -303,6 +304,11 @@ constexpr bool kWaveBlocksXcd = true;
 __host__ __device__ constexpr bool wave_blocks(int mode, bool mips, uint32_t nf, bool ring) {
     return (ring && kRingWaveBlocks) || (kDirectWaveBlocks && mode == GEO_MODE_DIRECT && !mips && nf == 1);
 }
+#if defined(GEO_FAN_PERSIST)  // A/B variant: the fan-mode draw on a persistent grid
+constexpr bool kFanPersist = true;
+#else
+constexpr bool kFanPersist = false;
+#endif
 // WB's 1-D grid for a launch of n tiles (n <= kMaxWaveBlockTiles: at most 2^31 workgroups)
 constexpr uint32_t kMaxWaveBlockTiles = 1u << 26;
 inline uint32_t wave_block_count(uint32_t n) { return kWaveBlocksXcd ? (n + 7u) / 8u * 32u : 4u * n; }
@@ -508,7 +514,14 @@ __global__ __launch_bounds__(kBlock) void geo_render_kernel(const RenderArgs a, 
     (void)cost_scale;
     const bool in_frame = px < a.width && ly < a.nrows && py < a.height;
     if constexpr (LR > 1) {
-        fan_tile<LR>(a, f, obase, tile, wave, lane);
+        if constexpr (kFanPersist) {
+            // a persistent grid (its tiles all cost the same): workgroup b
+            // draws tiles b, b + G, ... of the launch
+            for (uint32_t t = blockIdx.x; t < a.launch_tiles; t += gridDim.x)
+                fan_tile<LR>(a, f, obase, make_uint2(t % a.tiles_x, a.tile_y0 + t / a.tiles_x), wave, lane);
+        } else {
+            fan_tile<LR>(a, f, obase, tile, wave, lane);
+        }
     } else if constexpr (!MIPS) {
         if (in_frame) {
             float c2x, c2y, c2z;
@@ -1327,7 +1340,9 @@ static int launch_tiles(RenderArgs a, const FrameBatch<NF>& fb, uint32_t nframes
         const bool last = y0 + ny >= tiles_y;
         hipEvent_t start = y0 == 0 ? t_start : nullptr;
         hipEvent_t stop = last ? (t_stop ? t_stop : done) : nullptr;
-        const dim3 grid(tiles_x, ny, nframes);
+        dim3 grid(tiles_x, ny, nframes);
+        if (MODE == GEO_MODE_FAN && kFanPersist && !mips)
+            grid = dim3(std::min(a.launch_tiles, a.persist_blocks), 1, nframes);
         if constexpr (NF == 1) {
             if constexpr (MODE != GEO_MODE_FAN && KIND != geo::kFlat) {
                 if (band) {  // GEO_FLAG_RING_F64 (one frame, level-0 sampler)
@@ -1496,6 +1511,7 @@ static int render_impl(geo_ctx* c, const geo_frame* frames, uint32_t nframes, si
         if (geo::geodesic_kind(pk[i]) != geo::geodesic_kind(pk[0])) return GEO_EINVAL;
     }
     a.out_frame_px = out_frame_stride / 4u;
+    a.persist_blocks = (uint32_t)c->num_cus * 8u;  // 8 workgroups of 4 waves per CU: every wave slot
 #if defined(GEO_WAVE_LOG)
     a.wave_log = c->wave_log;
 #endif

@@ -301,8 +301,15 @@ constexpr bool kWaveBlocksXcd = GEO_WB_XCD != 0;
 #else
 constexpr bool kWaveBlocksXcd = true;
 #endif
+#if defined(GEO_ADAPTIVE_WAVE_BLOCKS)  // A/B variant
+constexpr bool kAdaptiveWaveBlocks = true;
+#else
+constexpr bool kAdaptiveWaveBlocks = false;
+#endif
 __host__ __device__ constexpr bool wave_blocks(int mode, bool mips, uint32_t nf, bool ring) {
-    return (ring && kRingWaveBlocks) || (kDirectWaveBlocks && mode == GEO_MODE_DIRECT && !mips && nf == 1);
+    return (ring && kRingWaveBlocks) ||
+           (!mips && nf == 1 &&
+            ((kDirectWaveBlocks && mode == GEO_MODE_DIRECT) || (kAdaptiveWaveBlocks && mode == GEO_MODE_ADAPTIVE)));
 }
 #if defined(GEO_FAN_PERSIST)  // A/B variant: the fan-mode draw on a persistent grid
 constexpr bool kFanPersist = true;

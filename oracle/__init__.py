@@ -83,6 +83,9 @@ def _load() -> ctypes.CDLL:
         "geo_oracle_asinf": (ctypes.c_float, [ctypes.c_float]),
         "geo_oracle_atan2f": (ctypes.c_float, [ctypes.c_float, ctypes.c_float]),
         "geo_oracle_sincosf": (None, [ctypes.c_float, vp, vp]),
+        "geo_oracle_sincos_sky": (None, [ctypes.c_float, vp, vp]),
+        "geo_oracle_acos_pi": (ctypes.c_float, [ctypes.c_float]),
+        "geo_oracle_atan2_turns": (ctypes.c_float, [ctypes.c_float, ctypes.c_float]),
         "geo_oracle_mip_chain_texels": (ctypes.c_uint64, [u32, u32]),
         "geo_oracle_mip_chain": (None, [vp, u32, u32, vp]),
         "geo_oracle_lod_q8_n": (None, [vp, u32, vp]),
@@ -280,6 +283,23 @@ def sincosf(x: float):
     s, c = ctypes.c_float(), ctypes.c_float()
     lib.geo_oracle_sincosf(x, _addr(s), _addr(c))
     return s.value, c.value
+
+
+def sincos_sky(x: float):
+    """the per-pixel form (geo_math.h sincos_sky_)"""
+    s, c = ctypes.c_float(), ctypes.c_float()
+    lib.geo_oracle_sincos_sky(x, _addr(s), _addr(c))
+    return s.value, c.value
+
+
+def acos_pi(x: float) -> float:
+    """acos(x) / pi (geo_math.h acos_pi_)"""
+    return lib.geo_oracle_acos_pi(x)
+
+
+def atan2_turns(y: float, x: float) -> float:
+    """atan2(y, x) / 2pi taken into [0, 1] (geo_math.h atan2_turns_)"""
+    return lib.geo_oracle_atan2_turns(y, x)
 
 
 # ---- accretion-disk points (geo_oracle_points.c) ----------------------------

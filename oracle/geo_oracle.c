@@ -294,6 +294,62 @@ float geo_oracle_atan2f(float y, float x) {
     return copysignf(r, y);
 }
 
+/* The per-pixel sky-direction transcendentals (round 6; geo_math.h
+ * sincos_sky_, acos_pi_, atan2_turns_): restated with C's fmaf / sqrtf /
+ * fmaxf, the same coefficients and order. */
+static float o_sqrt_unit(float x) { return sqrtf(fmaxf(x, 0x1p-96f)); }
+
+void geo_oracle_sincos_sky(float x, float* so, float* co) {
+    float tj = fmaf(x, 0.318309886183790671538f, 12582912.0f);
+    float j = tj - 12582912.0f;
+    uint32_t tb;
+    memcpy(&tb, &tj, 4);
+    float r = fmaf(-j, 3.140625f, x);
+    r = fmaf(-j, 9.67653584666550159e-4f, r);
+    float z = r * r;
+    float ps = fmaf(fmaf(fmaf(2.600061634e-06f, z, -1.980661764e-04f), z, 8.333017118e-03f), z, -1.666665673e-01f);
+    float sn = fmaf(r * z, ps, r);
+    float pc = fmaf(fmaf(fmaf(2.319447049e-05f, z, -1.385593088e-03f), z, 4.166398942e-02f), z, -4.999993145e-01f);
+    float cs = fmaf(z, pc, 1.0f);
+    if (tb & 1u) { /* odd j: both signs flip */
+        sn = -sn;
+        cs = -cs;
+    }
+    *so = sn;
+    *co = cs;
+}
+
+float geo_oracle_acos_pi(float x) {
+    float a = fminf(fabsf(x), 1.0f); /* NaN -> 1 */
+    float s = o_sqrt_unit(1.0f - a);
+    float p = fmaf(8.312922437e-04f, a, -3.820668207e-03f);
+    p = fmaf(p, a, 8.837061934e-03f);
+    p = fmaf(p, a, -1.565995067e-02f);
+    p = fmaf(p, a, 2.827732079e-02f);
+    p = fmaf(p, a, -6.830646098e-02f);
+    p = fmaf(p, a, 4.999999702e-01f);
+    float h = s * p;
+    return x < 0.0f ? 1.0f - h : h;
+}
+
+float geo_oracle_atan2_turns(float y, float x) {
+    float ay = fabsf(y), ax = fabsf(x);
+    float num, den, y0;
+    if (ay > 2.414213562373095f * ax) {
+        num = -ax; den = ay; y0 = 0.25f;
+    } else if (ay > 0.4142135623730950f * ax) {
+        num = ay - ax; den = ay + ax; y0 = 0.125f;
+    } else {
+        num = ay; den = ax; y0 = 0.0f;
+    }
+    float t = den > 0.0f ? num * (1.0f / den) : 0.0f; /* divf_ */
+    float z = t * t;
+    float p = fmaf(fmaf(fmaf(-1.715674624e-02f, z, 3.116416559e-02f), z, -5.302115157e-02f), z, 1.591545641e-01f);
+    float r = fmaf(t, p, y0);
+    float h = x < 0.0f ? 0.5f - r : r;
+    return y < 0.0f ? 1.0f - h : h;
+}
+
 typedef struct {
     float rs, sphere_r, r, step;
     uint32_t max_steps;
@@ -792,9 +848,7 @@ static void pixel_f32(const geo_frame* f, const cam_f32* cam, const fconsts* k, 
         lam = (float)l;
         bh = l < -7.0;
     } else if (mode == (int)GEO_MODE_FAN) {
-        float theta = geo_oracle_asinf(st);
-        float t = clampf((F_PI2 - theta) / F_PI, 0.0f, 1.0f);
-        t = t * (float)(n_fan - 1u);
+        float t = geo_oracle_acos_pi(st) * (float)(n_fan - 1u); /* (pi/2 - asin st) / pi, in [0, 1] */
         float fl = floorf(t);
         uint32_t i = (uint32_t)fl;
         float w = t - fl;
@@ -807,7 +861,7 @@ static void pixel_f32(const geo_frame* f, const cam_f32* cam, const fconsts* k, 
     }
     /* sky_uv */
     float sl, cll;
-    geo_oracle_sincosf(lam, &sl, &cll);
+    geo_oracle_sincos_sky(lam, &sl, &cll);
     float ex = cll, ey = 0.0f;
     if (rho2 > 0.0f) {
         float w = cll * rrho;
@@ -816,14 +870,10 @@ static void pixel_f32(const geo_frame* f, const cam_f32* cam, const fconsts* k, 
     }
     float c3[3];
     m3vf(f->central_to_uv, ex, ey, sl, c3);
-    float U = geo_oracle_atan2f(c3[1], c3[0]) * 0.159154943091895335769f;
-    if (U < 0.0f) U += 1.0f;
-    U = U + 0.0f; /* -0 -> +0 (the kernel's med3 clamp) */
-    float V = 0.5f - geo_oracle_asinf(c3[2]) * 0.318309886183790671538f;
+    float U = geo_oracle_atan2_turns(c3[1], c3[0]); /* atan2 / 2pi taken into [0, 1] */
     if (!(U == U)) U = 0.0f;
-    if (!(V == V)) V = 0.0f;
     U = clampf(U, 0.0f, 1.0f);
-    V = clampf(V, 0.0f, 1.0f);
+    float V = geo_oracle_acos_pi(c3[2]); /* 1/2 - asin(z) / pi */
     uv[0] = U;
     uv[1] = V;
     *bh_out = (uint8_t)bh;

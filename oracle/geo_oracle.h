@@ -136,6 +136,10 @@ float geo_oracle_acosf(float x);
 float geo_oracle_asinf(float x);
 float geo_oracle_atan2f(float y, float x);
 void geo_oracle_sincosf(float x, float* s, float* c);
+/* the per-pixel sky-direction forms (round 6; geo_math.h sincos_sky_, acos_pi_, atan2_turns_) */
+void geo_oracle_sincos_sky(float x, float* s, float* c);
+float geo_oracle_acos_pi(float x);
+float geo_oracle_atan2_turns(float y, float x);
 
 #ifdef __cplusplus
 }

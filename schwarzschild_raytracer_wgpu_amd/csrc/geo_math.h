@@ -9,9 +9,11 @@
 // min max and compares; compile with -ffp-contract=off and correctly rounded
 // f32 divide/sqrt (hipcc default, pinned by -fhip-fp32-correctly-rounded-divide-sqrt).
 //
-// Algorithms: Cody-Waite reduction by pi/2 plus Cephes-style minimax
-// polynomials (sin/cos on [-pi/4, pi/4], asin on [0, 1/2], atan on
-// [-(sqrt2-1), sqrt2-1]).  Accuracy is checked against libm in
+// Algorithms: the general-purpose forms (point path, observer): Cody-Waite
+// reduction by pi/2 plus Cephes-style minimax polynomials (sin/cos on
+// [-pi/4, pi/4], asin on [0, 1/2], atan on [-(sqrt2-1), sqrt2-1]); the
+// per-pixel sky-direction forms (end of file): reduction by pi, acos/pi as
+// sqrt(1 - |x|) P(|x|), atan2 in turns.  Accuracy is checked against libm in
 // tests/test_math.py (<= 3 ulp / 2e-7 abs on the ranges used).
 #pragma once
 
@@ -203,5 +205,95 @@ GEO_HD float acosf_(float x) {
 }
 
 GEO_HD float atanf_(float x) { return atan2f_(x, 1.0f); }
+
+// ---- The per-pixel sky-direction transcendentals (round 6) ----
+// Specified for what they feed: angles in turns and half-turns, absolute
+// error <= 2e-7 (tools/fit_sky_polys.py fits the polynomials;
+// tests/test_math.py checks the error), against a UV bar of 1e-4.  The
+// general-purpose forms above stay for the point path and the observer.
+
+// sqrt(max(x, 2^-96)), correctly rounded, for x in [0, 1]: sqrtf_'s fast
+// sequence with the range test replaced by the max (x = 0 gives 2^-48; the
+// nonzero x here are >= 2^-24), so no branch.
+GEO_HD float sqrt_unit_(float x) {
+    const float xm = __builtin_fmaxf(x, 0x1p-96f);
+#if defined(__HIP_DEVICE_COMPILE__)
+    const float y = __builtin_amdgcn_rsqf(xm);
+    const float s0 = xm * y;
+    const float hy = 0.5f * y;
+    return __builtin_fmaf(__builtin_fmaf(-s0, s0, xm), hy, s0);
+#else
+    return __builtin_sqrtf(xm);
+#endif
+}
+
+// sin and cos of x, |x| < 2^21: j = rint(x / pi) by the 1.5 * 2^23 shifter
+// (one fma; its sum's low mantissa bit is j's parity), r = x - j pi in two
+// Cody-Waite parts (|r| <= pi/2 + 1 ulp; pi - P1 - P2 = 5e-12), cubic
+// polynomials in r^2, and both signs flipped for odd j by an XOR of the
+// parity bit.  17 VALU.
+GEO_HD void sincos_sky_(float x, float* s, float* c) {
+    constexpr float kShifter = 12582912.0f;  // 1.5 * 2^23
+    const float tj = fmaf_(x, kInvPi, kShifter);
+    const float j = tj - kShifter;
+    uint32_t tb;
+    __builtin_memcpy(&tb, &tj, 4);
+    const uint32_t flip = tb << 31;
+    float r = fmaf_(-j, 3.140625f, x);
+    r = fmaf_(-j, 9.67653584666550159e-4f, r);
+    const float z = r * r;
+    const float ps = fmaf_(fmaf_(fmaf_(2.600061634e-06f, z, -1.980661764e-04f), z, 8.333017118e-03f), z,
+                           -1.666665673e-01f);
+    const float sn = fmaf_(r * z, ps, r);
+    const float pc = fmaf_(fmaf_(fmaf_(2.319447049e-05f, z, -1.385593088e-03f), z, 4.166398942e-02f), z,
+                           -4.999993145e-01f);
+    const float cs = fmaf_(z, pc, 1.0f);
+    uint32_t sb, cb;
+    __builtin_memcpy(&sb, &sn, 4);
+    __builtin_memcpy(&cb, &cs, 4);
+    sb ^= flip;
+    cb ^= flip;
+    __builtin_memcpy(s, &sb, 4);
+    __builtin_memcpy(c, &cb, 4);
+}
+
+// acos(x) / pi in [0, 1] for x in [-1, 1] (|x| clamped to 1 by one
+// v_min_f32; a NaN x gives |x| = 1): h = sqrt(1 - |x|) P(|x|) with P of
+// degree 6, and 1 - h for x < 0.  h <= 0.5 + 1 ulp, so the result is in
+// [0, 1] for every input.  No branch; 18 VALU.
+GEO_HD float acos_pi_(float x) {
+    const float a = __builtin_fminf(__builtin_fabsf(x), 1.0f);
+    const float s = sqrt_unit_(1.0f - a);
+    float p = fmaf_(8.312922437e-04f, a, -3.820668207e-03f);
+    p = fmaf_(p, a, 8.837061934e-03f);
+    p = fmaf_(p, a, -1.565995067e-02f);
+    p = fmaf_(p, a, 2.827732079e-02f);
+    p = fmaf_(p, a, -6.830646098e-02f);
+    p = fmaf_(p, a, 4.999999702e-01f);
+    const float h = s * p;
+    return x < 0.0f ? 1.0f - h : h;
+}
+
+// atan2(y, x) / (2 pi) taken into [0, 1] (the sky's U before its clamp):
+// atan2f_'s reduction to |t| <= tan(pi/8) with its offsets in turns, a cubic
+// polynomial in t^2 with 1 / (2 pi) folded in, then the half-plane and
+// lower-half reflections (x < 0: 1/2 - r; y < 0: 1 - r).  atan2(+-0, 0) = 0;
+// a NaN y gives NaN (the caller's clamp maps it to 0).
+GEO_HD float atan2_turns_(float y, float x) {
+    const float ay = __builtin_fabsf(y);
+    const float ax = __builtin_fabsf(x);
+    const bool big = ay > 2.414213562373095f * ax;
+    const bool mid = ay > 0.4142135623730950f * ax;
+    const float num = big ? -ax : (mid ? ay - ax : ay);
+    const float den = big ? ay : (mid ? ay + ax : ax);
+    const float y0 = big ? 0.25f : (mid ? 0.125f : 0.0f);
+    const float t = den > 0.0f ? divf_(num, den) : 0.0f;
+    const float z = t * t;
+    const float p = fmaf_(fmaf_(fmaf_(-1.715674624e-02f, z, 3.116416559e-02f), z, -5.302115157e-02f), z,
+                          1.591545641e-01f);
+    const float r = fmaf_(t, p, y0);
+    const float h = x < 0.0f ? 0.5f - r : r;
+    return y < 0.0f ? 1.0f - h : h;
+}
 
 }  // namespace geo

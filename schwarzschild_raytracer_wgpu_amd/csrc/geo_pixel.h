@@ -1012,26 +1012,16 @@ GEO_HD int32_t floor_i32_(float x) {
 }
 
 // Fan lookup (shader.wgsl:77-84); i+1 clamped to n-1 (weight 0 there).
-// On the device, with the same bits: the quotient by pi as a * RN(1/pi) plus
-// one fma correction (exhaustively equal to a / pi over fan_lerp's domain,
-// tests/native/divpi_exhaustive.hip), the index by v_cvt_flr_i32_f32 and the
+// (pi/2 - asin(st)) / pi is acos(st) / pi, computed as such (acos_pi_, in
+// [0, 1] for every input, so the node index is in [0, n-1] with no clamp).
+// On the device, with the same bits: the index by v_cvt_flr_i32_f32 and the
 // weight by v_fract_f32 (t - floor(t), exact for t >= 0).
 struct FanPos {
     uint32_t i, i1;  // nodes
     float w;         // weight of node i1
 };
 GEO_HD FanPos fan_pos(uint32_t n, float st) {
-    const float theta = asinf_(st);
-    const float a = kPi2 - theta;
-#if defined(__HIP_DEVICE_COMPILE__)
-    constexpr float kRcpPi = 1.0f / kPi;
-    const float q0 = a * kRcpPi;
-    const float quot = fmaf_(fmaf_(-q0, kPi, a), kRcpPi, q0);
-#else
-    const float quot = a / kPi;
-#endif
-    float t = clampf_(quot, 0.0f, 1.0f);
-    t = t * (float)(n - 1u);
+    const float t = acos_pi_(st) * (float)(n - 1u);
 #if defined(__HIP_DEVICE_COMPILE__)
     const uint32_t i = (uint32_t)floor_i32_(t);
     const float w = __builtin_amdgcn_fractf(t);
@@ -1058,7 +1048,7 @@ GEO_HD float central_rho(float c2x, float c2y) { return sqrtf_(fmaf_(c2y, c2y, c
 // shader.wgsl:90-100 — (phi of c2, lambda') to sky-sphere (U, V); rho = central_rho, rrho = rcpf_(rho).
 GEO_HD void sky_uv(const float* m2, float c2x, float c2y, float rho, float rrho, float lam, float* U, float* V) {
     float sl, cl;
-    sincosf_(lam, &sl, &cl);
+    sincos_sky_(lam, &sl, &cl);
     // to_cart(phi, lam) with (cos phi, sin phi) = (c2x, c2y)/rho
     float ex = cl, ey = 0.0f;
     if (rho > 0.0f) {
@@ -1068,15 +1058,12 @@ GEO_HD void sky_uv(const float* m2, float c2x, float c2y, float rho, float rrho,
     }
     float x, y, z;
     mat3_mul(m2, ex, ey, sl, &x, &y, &z);
-    float u = atan2f_(y, x) * kInvTwoPi;
-    if (u < 0.0f) u += 1.0f;
-    const float v = 0.5f - asinf_(z) * kInvPi;
-    // clamped to [0, 1] with NaN -> 0, one v_med3_f32 each (the med3 of a NaN
-    // is the IEEE min of the other two, 0); u + 0 first turns the -0 of an
-    // atan2(-0, x) into +0, the one signed zero the median could order either
-    // way (v = 1/2 - t is never -0)
-    *U = med3_(u + 0.0f, 0.0f, 1.0f);
-    *V = med3_(v, 0.0f, 1.0f);
+    // polar.x / 2pi wrapped into [0, 1] and 1/2 - polar.y / pi = acos(z) / pi
+    // (:95-100).  U is clamped with NaN -> 0 by one v_med3_f32 (the med3 of a
+    // NaN is the IEEE min of the other two, 0; atan2_turns_ never returns -0);
+    // V is in [0, 1] for every z (acos_pi_).
+    *U = med3_(atan2_turns_(y, x), 0.0f, 1.0f);
+    *V = acos_pi_(z);
 }
 
 // Packed channel pairs of the bilinear sample: R|B and G|A in the two 16-bit

@@ -371,7 +371,11 @@ __device__ __forceinline__ const geo::PixelConsts& frame_consts(const RenderArgs
 // Four pixels per lane (a 32 x 32 tile, 47 VGPRs) measured the same as two
 // (4K draw 0.0373 vs 0.0370 ms, 3 x 3 interleaved, profiles/r04g_fan_lr_ab.txt):
 // the draw's waves are not short of independent work.
+#if defined(GEO_FAN_LANE_ROWS)  // A/B variant
+constexpr uint32_t kFanLaneRows = GEO_FAN_LANE_ROWS;
+#else
 constexpr uint32_t kFanLaneRows = 2;
+#endif
 __host__ __device__ constexpr uint32_t lane_rows(int mode, bool mips) {
     return mode == GEO_MODE_FAN && !mips ? kFanLaneRows : 1u;
 }
@@ -399,6 +403,12 @@ __device__ __forceinline__ void fan_tile(const RenderArgs& a, const FrameK& f, s
         py[k] = p0;
         py[k + 1] = p0 + kWaveRows;
     }
+#if defined(GEO_FAN_PROBE) && (GEO_FAN_PROBE & 4)  // diagnostic: the stores alone
+#pragma unroll
+    for (uint32_t k = 0; k < LR; ++k)
+        if (px < a.width && ly[k] < a.nrows && py[k] < a.height) a.out_rgba[obase + (size_t)ly[k] * a.width + px] = py[k];
+    return;
+#endif
     float c2x[LR], c2y[LR], st[LR], ct[LR], rct[LR], lam[LR];
 #pragma unroll
     for (uint32_t k = 0; k < LR; ++k) {
@@ -413,7 +423,13 @@ __device__ __forceinline__ void fan_tile(const RenderArgs& a, const FrameK& f, s
 #pragma unroll
     for (uint32_t k = 0; k < LR; ++k) fp[k] = geo::fan_pos(a.n_fan, st[k]);
 #pragma unroll
-    for (uint32_t k = 0; k < LR; ++k) lam[k] = geo::fan_at(a.fan, fp[k]);
+    for (uint32_t k = 0; k < LR; ++k) {
+#if defined(GEO_FAN_PROBE) && (GEO_FAN_PROBE & 2)  // diagnostic: no fan loads
+        lam[k] = st[k] + fp[k].w;
+#else
+        lam[k] = geo::fan_at(a.fan, fp[k]);
+#endif
+    }
     bool in[LR], bh[LR];
     bool all_bh = true;
 #pragma unroll
@@ -439,7 +455,14 @@ __device__ __forceinline__ void fan_tile(const RenderArgs& a, const FrameK& f, s
                                      a.sky_pitch_b};
             uint32_t smp[LR];
 #pragma unroll
-            for (uint32_t k = 0; k < LR; ++k) smp[k] = geo::sample_sky_quad_f(quad, a.sky_w256, a.sky_h256, U[k], V[k]);
+            for (uint32_t k = 0; k < LR; ++k) {
+#if defined(GEO_FAN_PROBE) && (GEO_FAN_PROBE & 1)  // diagnostic: no texel loads
+                smp[k] = __float_as_uint(U[k]) ^ __float_as_uint(V[k]);
+                (void)quad;
+#else
+                smp[k] = geo::sample_sky_quad_f(quad, a.sky_w256, a.sky_h256, U[k], V[k]);
+#endif
+            }
 #pragma unroll
             for (uint32_t k = 0; k < LR; ++k)
                 rgba[k] = bh[k] ? geo::kBlackRGBA : geo::over_clear(smp[k], a.sky_opaque != 0);

@@ -104,6 +104,17 @@ extern "C" void host_math(const float* x, uint32_t n, float* out_sin, float* out
     }
 }
 
+// The per-pixel sky-direction forms (sincos_sky_, acos_pi_ of x,
+// atan2_turns_(y, x)) on n inputs, for bit comparisons with the oracle.
+extern "C" void host_sky_math(const float* x, const float* y, uint32_t n, float* out_sin, float* out_cos,
+                              float* out_acos_pi, float* out_turns) {
+    for (uint32_t i = 0; i < n; ++i) {
+        geo::sincos_sky_(x[i], &out_sin[i], &out_cos[i]);
+        out_acos_pi[i] = geo::acos_pi_(x[i]);
+        out_turns[i] = geo::atan2_turns_(y[i], x[i]);
+    }
+}
+
 // GEO_FLAG_MIPS pieces of the header on the host: the mip chain (levels one
 // after another) and the level of detail, for comparisons with the oracle.
 extern "C" void host_mip_chain(const uint8_t* rgba8, uint32_t w, uint32_t h, uint32_t* out) {

@@ -1,7 +1,8 @@
 """Device math that must equal hipcc's correctly rounded builtins bit for bit,
 over all 2^32 inputs on the GPU (built here with hipcc for gfx950):
 geo::sqrtf_ against __builtin_sqrtf (tests/native/sqrt_exhaustive.hip) and
-geo::rcpf_ against 1.0f / x (tests/native/rcp_exhaustive.hip); and the sky
+geo::rcpf_ against 1.0f / x (tests/native/rcp_exhaustive.hip), geo::sqrt_unit_
+against sqrtf(fmaxf(x, 2^-96)) on [0, 1] (tests/native/sqrt_unit_exhaustive.hip); and the sky
 UV clamp (one v_med3_f32: NaN -> 0, [0, 1]) against its rule on the bit
 pattern (tests/native/clamp_exhaustive.hip)."""
 import os
@@ -79,19 +80,19 @@ def test_cvt_flr_and_sincos_shifter_exhaustive(tmp_path):
     assert r.returncode == 0 and "mismatches 0" in r.stdout, r.stdout + r.stderr
 
 
-def test_fan_quotient_by_pi_exhaustive(tmp_path):
-    """geo::fan_lerp's device quotient by pi (RN(1/pi) product plus one fma
-    correction) equals the correctly rounded a / pi over its whole domain
-    (tests/native/divpi_exhaustive.hip)."""
+def test_sqrt_unit_exhaustive(tmp_path):
+    """geo::sqrt_unit_ (acos_pi_'s branch-free sqrt) equals the correctly
+    rounded sqrtf(fmaxf(x, 2^-96)) for every f32 x in [0, 1]
+    (tests/native/sqrt_unit_exhaustive.hip)."""
     import torch
 
     if not torch.cuda.is_available():
         pytest.skip("no HIP device")
     if not (os.path.exists(HIPCC) or shutil.which("hipcc")):
         pytest.skip("no hipcc")
-    exe = str(tmp_path / "divpi_exhaustive")
+    exe = str(tmp_path / "sqrt_unit_exhaustive")
     subprocess.run([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off",
                     "-fhip-fp32-correctly-rounded-divide-sqrt", "-fno-gpu-flush-denormals-to-zero",
-                    os.path.join(HERE, "native", "divpi_exhaustive.hip"), "-o", exe], check=True)
+                    os.path.join(HERE, "native", "sqrt_unit_exhaustive.hip"), "-o", exe], check=True)
     r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and "mismatches 0" in r.stdout, r.stdout + r.stderr

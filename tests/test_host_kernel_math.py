@@ -243,3 +243,34 @@ def test_host_transcendentals_equal_oracle(host):
         assert np.float32(oa).view(np.uint32) == a[i].view(np.uint32), (x, oa, a[i])
     assert O.asinf(-1.5) == np.float32(-math.pi / 2)
     assert abs(O.asinf(float("nan"))) == np.float32(math.pi / 2)
+
+
+def test_host_sky_transcendentals_equal_oracle(host):
+    """geo_math.h's per-pixel forms sincos_sky_ (rint by the shifter, parity
+    bit XOR), acos_pi_ (sqrt floor by fmaxf) and atan2_turns_ host-compiled
+    equal the oracle's restatement bit for bit: random and huge arguments,
+    x / pi at and next to half-integers (the shifter's ties), |x| > 1, signed
+    zeros, the axes and NaN."""
+    rng = np.random.default_rng(17)
+    inv_pi = np.float32(0.318309886183790671538)
+    ties = []
+    for k in range(-600, 600):
+        x0 = np.float32(np.float32(k + 0.5) / inv_pi)
+        ties += [x0, np.nextafter(x0, np.float32(np.inf)), np.nextafter(x0, np.float32(-np.inf))]
+    special = [0.0, -0.0, 1.0, -1.0, 1.5, -1.5, np.nan, -np.nan, 1 - 2**-24, -(1 - 2**-24)]
+    xs = np.concatenate([rng.uniform(-10, 10, 20000), rng.uniform(-1.2, 1.2, 20000), rng.uniform(-9000, 9000, 5000),
+                         np.array(ties, np.float64), special]).astype(np.float32)
+    ys = np.concatenate([rng.standard_normal(xs.size - 2 * len(special)), special, special[::-1]]).astype(np.float32)
+    n = xs.size
+    s, c, a, u = (np.empty(n, np.float32) for _ in range(4))
+    vp = ctypes.c_void_p
+    host.host_sky_math(vp(xs.ctypes.data), vp(ys.ctypes.data), ctypes.c_uint32(n), vp(s.ctypes.data),
+                       vp(c.ctypes.data), vp(a.ctypes.data), vp(u.ctypes.data))
+    bits = lambda v: np.float32(v).view(np.uint32)  # noqa: E731
+    for i in range(n):
+        x, y = float(xs[i]), float(ys[i])
+        os_, oc = O.sincos_sky(x)
+        assert (bits(os_), bits(oc)) == (s[i].view(np.uint32), c[i].view(np.uint32)) or math.isnan(x), (x, os_, s[i])
+        assert bits(O.acos_pi(x)) == a[i].view(np.uint32), (x, O.acos_pi(x), a[i])
+        ou = O.atan2_turns(y, x)
+        assert bits(ou) == u[i].view(np.uint32) or (math.isnan(ou) and math.isnan(u[i])), (y, x, ou, u[i])

@@ -55,7 +55,8 @@ def block_valu(path):
 def groups(bv):
     """Blocks in program order: set-up up to the loop, loop body (the blocks
     with the back edge and the two before it), Newton (until the epilogue's
-    sincos reduction, 0x3f22f983 = 2/pi), epilogue, step counter/cost tail."""
+    sincos reduction: 0x3ea2f983 = 1/pi since round 6, 0x3f22f983 = 2/pi
+    before), epilogue, step counter/cost tail."""
     names = [n for n, _ in bv]
     valu = dict(bv)
     lines = IB.kernel_lines(sys.argv[1] if len(sys.argv) > 1 else "/tmp/new.s", SYM)
@@ -63,7 +64,7 @@ def groups(bv):
     loop_end = next(i for i, n in enumerate(names) if any(x.startswith("s_cbranch_scc1") and names[i - 2] in x
                                                            for x in text[n]))
     loop = names[loop_end - 2:loop_end + 1]
-    epi0 = next(i for i, n in enumerate(names) if any("0x3f22f983" in x for x in text[n]))
+    epi0 = next(i for i, n in enumerate(names) if any("0x3ea2f983" in x or "0x3f22f983" in x for x in text[n]))
     tail0 = next(i for i, n in enumerate(names) if any("row_shr:1" in x for x in text[n]))
     setup = [n for n in names[:loop_end - 2] if n not in loop]
     newton = [n for n in names[loop_end + 1:epi0]]

@@ -6,7 +6,7 @@ stores, minus a pass-through kernel with the same loads and stores).
 The correctly rounded sqrt/reciprocal fallbacks (`v_sqrt_f32`,
 `v_div_scale_f32` sequences behind a wave-uniform branch that no frame pixel
 takes: denormal or huge operands, geo_math.h) are listed apart and not
-counted; asin's sqrt branch (|x| > 1/2) is counted, since frame pixels take it.
+counted.
 
     python tools/fan_blocks.py [--asm OUT.s]
 """
@@ -27,12 +27,12 @@ BLOCKS = ["kPass", "kRay", "kCentral", "kFanIndex", "kFanLerp", "kSkyUV", "kSinc
 LABEL = {
     "kRay": "camera ray + aberration (pixel_central_dir: 6 FMA, |d| sqrt, 1/(L - k dz))",
     "kCentral": "sin/cos of the central angle (med3 clamp, rho = sqrt, 1/rho)",
-    "kFanIndex": "fan index (asin of st, (pi/2 - theta)/pi, index and weight)",
+    "kFanIndex": "fan index (acos(st)/pi, index and weight)",
     "kFanLerp": "fan lerp (two loads, lerp)",
-    "kSkyUV": "sky UV (sincos of lambda', to_cart, M2, atan2, asin, clamps)",
-    "kSincos": "  of which sincos",
-    "kAtan2": "  of which atan2",
-    "kAsin": "  of which asin",
+    "kSkyUV": "sky UV (sincos of lambda', to_cart, M2, U in turns, V = acos/pi)",
+    "kSincos": "  of which sincos (sincos_sky_)",
+    "kAtan2": "  of which U (atan2_turns_ + clamp)",
+    "kAsin": "  of which V (acos_pi_)",
     "kSample": "bilinear sample (texel coordinates, quad loads, packed lerps)",
     "kBlend": "blend over the clear colour",
 }

@@ -60,11 +60,11 @@ __global__ __launch_bounds__(256) void blk(const float4* __restrict__ in, float4
     } else if constexpr (B == kSkyUV) {
         geo::sky_uv(a.m2, x.x, x.y, x.z, x.w, y.w, &y.x, &y.y);
     } else if constexpr (B == kSincos) {
-        geo::sincosf_(x.x, &y.x, &y.y);
+        geo::sincos_sky_(x.x, &y.x, &y.y);
     } else if constexpr (B == kAtan2) {
-        y.x = geo::atan2f_(x.x, x.y);
+        y.x = geo::med3_(geo::atan2_turns_(x.x, x.y), 0.0f, 1.0f);
     } else if constexpr (B == kAsin) {
-        y.x = geo::asinf_(x.x);
+        y.x = geo::acos_pi_(x.x);
     } else if constexpr (B == kSample) {
         const Quad q{a.sky, a.pitch_b};
         y.x = __uint_as_float(geo::sample_sky_quad_f(q, a.tw256, a.th256, x.x, x.y));

@@ -1180,7 +1180,7 @@ def ring_record(g, ctx, frame, scene, sky, W, H, args, flops_of, dev):
     same frame with the capture band's lanes integrated in f64 inside the
     render kernel, the mode that meets north_star's UV bar against the
     reference's own f64 arithmetic on every pixel.  Plain and ring frames are
-    timed interleaved (3 x K frames each, one launch per frame, one stream,
+    timed interleaved (3 runs each of max(K, ~25 ms) frames, one launch per frame, one stream,
     the learned dispatch order of each), each launch's kernel by an event
     pair on its dispatch; then the GPU's rows through the band against the
     CPU path's (geo_render_cpu: geo_band.h on the host)."""
@@ -1210,9 +1210,6 @@ def ring_record(g, ctx, frame, scene, sky, W, H, args, flops_of, dev):
     ring_steps = int(total.item())
     flops = flops_of(ring_steps, hits)
     del mask, steps
-    K = args.steps
-    ev = {i: (HipEvent(), HipEvent()) for i in range(0, K, max(1, args.event_every))}
-
     def run(sc, n, events=None):
         for i in range(n):
             if events is not None and i in events:
@@ -1220,7 +1217,15 @@ def ring_record(g, ctx, frame, scene, sky, W, H, args, flops_of, dev):
             ctx.render_rows(frame, sc, W, H, 0, H, out)
 
     run(ring_d, 100)  # its order learned, the clock settled
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
     run(plain_d, 100)
+    torch.cuda.synchronize()
+    # frames per timed run: at least the line's K and about 25 ms of plain
+    # frames (at K = 20 a 1080p run is 1.2 ms, short enough for the clock's
+    # transitions between runs to read as several per cent either way)
+    K = max(args.steps, min(2000, int(math.ceil(0.025 / max((time.perf_counter() - t0) / 100, 1e-6)))))
+    ev = {i: (HipEvent(), HipEvent()) for i in range(0, K, max(1, K // 10))}
     res = {"plain": [], "ring": [], "plain_k": [], "ring_k": []}
     for rep in range(3):
         for name, sc in (("plain", plain_d), ("ring", ring_d)):
@@ -1289,7 +1294,9 @@ def ring_record(g, ctx, frame, scene, sky, W, H, args, flops_of, dev):
                                 "mask, UV bits, steps"},
         "what": "GEO_FLAG_RING_F64: the capture band's lanes (|b/b_c - 1| < 8e-3 by the f32 ray) integrate in f64 "
                 "inside the render kernel; ms_per_step and plain_ms_per_step are the best of 3 interleaved "
-                "runs of K frames each (one launch per frame, one stream)",
+                "runs of `frames` frames each (one launch per frame, one stream; at least the line's K and "
+                "about 25 ms of plain frames)",
+        "frames": K,
     }
 
 

@@ -381,3 +381,60 @@ def test_timed_step_of_a_rank_without_rows():
         sf.drain()
         torch.cuda.synchronize()
         assert 0.0 <= ev[0].elapsed_time(ev[1]) < 1.0
+
+
+@pytest.mark.parametrize("world,K,lead", [(2, 4, 1), (4, 3, (3, 2)), (8, 2, 2)])
+def test_rank0_pipeline_ring_f64_per_frame(world, K, lead):
+    """GEO_FLAG_RING_F64 through the multi-GPU pipeline (bench.py --ring-f64
+    --batch-launch off at N > 1): each frame's bands render in their own launch
+    with the capture band in f64, and rank 0's assembled frames equal the
+    single-launch ring frame byte for byte (the band's pixels are per pixel,
+    whatever the band layout or dispatch order); a batched band-set launch
+    refuses the flag (geo.h: one frame per launch)."""
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    import schwarzschild_raytracer_wgpu_amd as g
+    from schwarzschild_raytracer_wgpu_amd.dist import BandLayout, ShardedFrame
+    from schwarzschild_raytracer_wgpu_amd.scenes import make_sky
+
+    W, H, B = 320, 180, 8
+    dev = torch.device("cuda:0")
+    ctx = g.Context(0)
+    ctx.set_sky(make_sky("equirect", (256, 128)))
+    frame, scene = default_frame(W, H), default_scene(512)
+    scene.flags |= g._lib.GEO_FLAG_RING_F64
+    plain = g.GeoScene.from_buffer_copy(bytes(scene))
+    plain.flags &= ~g._lib.GEO_FLAG_RING_F64
+    # the ring frame differs from the plain one (the band is in the frame:
+    # its lanes' lambda', so their UV bits)
+    uv_ring = torch.empty(H * W * 2, dtype=torch.float32, device=dev)
+    uv_plain = torch.empty(H * W * 2, dtype=torch.float32, device=dev)
+    ref = torch.empty(H * W * 4, dtype=torch.uint8, device=dev)
+    tmp = torch.empty(H * W * 4, dtype=torch.uint8, device=dev)
+    ctx.render_rows(frame, scene, W, H, 0, H, ref, out_uv=uv_ring)
+    ctx.render_rows(frame, plain, W, H, 0, H, tmp, out_uv=uv_plain)
+    torch.cuda.synchronize()
+    assert int((uv_ring != uv_plain).sum().item()) > 0
+    fake = FakeRcclGather(torch, [])
+    lead, pb = lead if isinstance(lead, tuple) else (lead, 1)
+    sf = ShardedFrame(ctx, frame, scene, W, H, B, 0, world, dev, dist=fake, frames_per_gather=K, render_streams=2,
+                      present_rgb=True, lead=lead, batch_launch=False, peer_bands=pb)
+    assert not sf.batch
+    for r in range(1, world):
+        fake.peer_bufs.append(_peer_bands(ctx, torch, frame, scene, W, H, B, r, world, lead, dev, sf.bpp,
+                                          pb).repeat(K))
+    nframes = 2 * K + 1
+    for i in range(nframes):
+        sf.step(i)
+    sf.drain()
+    torch.cuda.synchronize()
+    assert torch.equal(sf.frame_rgba(), ref)
+    # one launch for several frames: refused
+    L = BandLayout(H, B, world, 0, lead, pb)
+    out = torch.empty(2 * L.nbands() * L.band_height() * W * 4, dtype=torch.uint8, device=dev)
+    with pytest.raises(g.GeoError) as e:
+        ctx.render_band_set_frames([frame, frame], scene, W, H, L.band_height(), L.row0(), L.cycle_rows, L.nbands(),
+                                   out)
+    assert e.value.status == -1  # GEO_EINVAL

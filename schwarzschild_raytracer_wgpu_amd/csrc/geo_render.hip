@@ -459,6 +459,8 @@ __device__ __forceinline__ void fan_tile(const RenderArgs& a, const FrameK& f, s
 #if defined(GEO_FAN_PROBE) && (GEO_FAN_PROBE & 1)  // diagnostic: no texel loads
                 smp[k] = __float_as_uint(U[k]) ^ __float_as_uint(V[k]);
                 (void)quad;
+#elif defined(GEO_FAN_PROBE) && (GEO_FAN_PROBE & 8)  // diagnostic: every lane samples near one texel
+                smp[k] = geo::sample_sky_quad_f(quad, a.sky_w256, a.sky_h256, 0.5f + U[k] * 1e-6f, 0.5f);
 #else
                 smp[k] = geo::sample_sky_quad_f(quad, a.sky_w256, a.sky_h256, U[k], V[k]);
 #endif

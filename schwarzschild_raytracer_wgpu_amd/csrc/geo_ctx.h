@@ -19,6 +19,7 @@ struct geo_ctx {
     static constexpr int kSkyLevels = 4;
     uint32_t sky_lvl_w[kSkyLevels], sky_lvl_h[kSkyLevels], sky_lvl_off[kSkyLevels];
     uint32_t sky_total_bytes;
+    uint32_t sky_pairs_off;  // kSkyPairs: byte offset of level 0's row pairs in `sky` (geo_render.hip)
     // Ray fan, double-buffered so that a frame's fan can be solved on a side
     // stream while the previous frame's fan-mode draws still read the other
     // buffer.  fan[fan_cur] is the context's fan (fan_cur < 0: none).  Each

@@ -1129,6 +1129,19 @@ GEO_HD void pad_sky(const uint8_t* rgba8, uint32_t tw, uint32_t th, uint32_t* ds
     }
 }
 
+// Level 0 of the padded sky again as row pairs (the device's bilinear reads
+// this copy): padded texels (x, y) and (x, y + 1) side by side in 8 bytes,
+// rows y = 0 .. th, so the quad at padded (x, y) is the 16 bytes at
+// 2 ((y (tw + 2) + x)) texels: one 16-byte load, one 128-B line.  pad: the
+// padded level (pad_sky), dst: 2 (th + 1) (tw + 2) texels.
+GEO_HD void pair_sky_rows(const uint32_t* pad, uint32_t tw, uint32_t th, uint32_t* dst) {
+    const uint32_t pw = tw + 2u;
+    for (uint32_t y = 0; y <= th; ++y)
+        for (uint32_t x = 0; x < pw; ++x) {
+            dst[2u * ((size_t)y * pw + x)] = pad[(size_t)y * pw + x];
+            dst[2u * ((size_t)y * pw + x) + 1u] = pad[(size_t)(y + 1u) * pw + x];
+        }
+}
 
 // The G|A channels of a texel into the two 16-bit halves (bytes 1 and 3 to
 // bytes 0 and 2): one v_perm_b32 on the device.

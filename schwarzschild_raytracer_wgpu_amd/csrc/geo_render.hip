@@ -119,6 +119,7 @@ struct RenderArgs {
     float mip_w256[geo::kSkyMipLevels], mip_h256[geo::kSkyMipLevels];
     float sky_wf, sky_hf;
     uint32_t sky_total_bytes;
+    uint32_t sky_pairs_off, sky_pairs_pitch;  // kSkyPairs: level 0's row pairs (PairSkyQuad)
     const float* fan;
     uint32_t n_fan;
     uint32_t* out_rgba;
@@ -179,6 +180,42 @@ struct PaddedSkyQuad {
         t[3] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rsrc, off + 4u, (int)pitch_b, 0);
     }
 };
+
+// A/B variant (GEO_SKY_PAIRS=1): level 0 also stored as row pairs
+// (geo::pair_sky_rows), so a bilinear quad is 16 contiguous bytes, one
+// buffer_load_dwordx4 and one 128-B line, where the row-major quad spans two
+// rows, two lines.  Measured against PaddedSkyQuad: the fan draw -0.5 to
+// -1 % (one box read the 1080p draw -8 %), config 3 +0.2 to +0.8 %, the ring
+// overhead up by half a point (profiles/r06zk_sky_pairs_ab.txt,
+// profiles/r06zl_sky_pairs_ab.txt), for a second copy of level 0 in device
+// memory: not kept.
+#if defined(GEO_SKY_PAIRS)
+constexpr bool kSkyPairs = GEO_SKY_PAIRS != 0;
+#else
+constexpr bool kSkyPairs = false;
+#endif
+struct PairSkyQuad {
+    __amdgpu_buffer_rsrc_t rsrc;
+    uint32_t base, pitch_b;  // the pairs' byte offset in the sky buffer; bytes per pair row, (sky_w + 2) * 8
+    __device__ __forceinline__ void operator()(int ix0, int iy0, uint32_t (&t)[4]) const {
+        const uint32_t off = base + __umul24((uint32_t)(iy0 + 1), pitch_b) + ((uint32_t)(ix0 + 1) << 3);
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, off, 0, 0);
+        t[0] = v[0];  // (x, y)
+        t[2] = v[1];  // (x, y + 1)
+        t[1] = v[2];  // (x + 1, y)
+        t[3] = v[3];  // (x + 1, y + 1)
+    }
+};
+__device__ __forceinline__ auto level0_quad(const RenderArgs& a) {
+    if constexpr (kSkyPairs)
+        return PairSkyQuad{__builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(a.sky), 0, (int)a.sky_total_bytes,
+                                                             kBufferRsrcWord3),
+                           a.sky_pairs_off, a.sky_pairs_pitch};
+    else
+        return PaddedSkyQuad{__builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(a.sky), 0, (int)a.sky_bytes,
+                                                               kBufferRsrcWord3),
+                             a.sky_pitch_b};
+}
 
 // The texel quad of one mip level of the padded chain (geo_ctx::sky): like
 // PaddedSkyQuad at a per-lane level, so base and pitch are vector values.
@@ -246,9 +283,7 @@ __device__ __forceinline__ void shade_pixel_bh(const RenderArgs& a, const float*
     float U = 0.0f, V = 0.0f;
     if (!bh || a.out_uv)
         geo::sky_uv(central_to_uv, c2x, c2y, ct, rct, lam, &U, &V);
-    const PaddedSkyQuad quad{__builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(a.sky), 0,
-                                                               (int)a.sky_bytes, kBufferRsrcWord3),
-                             a.sky_pitch_b};
+    const auto quad = level0_quad(a);
     if (a.composite) {
         // over the previous spheres; a discarded pixel keeps the target
         if (!bh) {
@@ -450,9 +485,7 @@ __device__ __forceinline__ void fan_tile(const RenderArgs& a, const FrameK& f, s
 #pragma unroll
             for (uint32_t k = 0; k < LR; ++k)
                 geo::sky_uv(f.frame.central_to_uv, c2x[k], c2y[k], ct[k], rct[k], lam[k], &U[k], &V[k]);
-            const PaddedSkyQuad quad{__builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(a.sky), 0,
-                                                                       (int)a.sky_bytes, kBufferRsrcWord3),
-                                     a.sky_pitch_b};
+            const auto quad = level0_quad(a);
             uint32_t smp[LR];
 #pragma unroll
             for (uint32_t k = 0; k < LR; ++k) {
@@ -1200,6 +1233,11 @@ int geo_set_sky(geo_ctx* c, const uint8_t* rgba8, uint32_t w, uint32_t h) {
         total += ((uint64_t)lw[l] + 2u) * ((uint64_t)lh[l] + 2u) * 4u;
         if (total >= (1ull << 31)) return GEO_EINVAL;
     }
+    const uint64_t pairs_off = total;  // kSkyPairs: level 0's row pairs after the chain
+    if (kSkyPairs) {
+        total += ((uint64_t)w + 2u) * ((uint64_t)h + 1u) * 8u;
+        if (total >= (1ull << 31)) return GEO_EINVAL;
+    }
     DeviceGuard g(c->device);
     if (!g.ok) return GEO_EHIP;
     // the chain on the host: level 0 = the texture, level l + 1 = the 2 x 2
@@ -1215,6 +1253,7 @@ int geo_set_sky(geo_ctx* c, const uint8_t* rgba8, uint32_t w, uint32_t h) {
         }
         geo::pad_sky(reinterpret_cast<const uint8_t*>(lvl.data()), lw[l], lh[l], pad.data() + loff[l] / 4u);
     }
+    if (kSkyPairs) geo::pair_sky_rows(pad.data(), w, h, pad.data() + pairs_off / 4u);
     // Renders of this context still running on any of the caller's streams
     // (non-blocking ones do not order against a blocking copy) may be reading
     // the current sky: let them finish before it is overwritten or freed.  A
@@ -1241,6 +1280,7 @@ int geo_set_sky(geo_ctx* c, const uint8_t* rgba8, uint32_t w, uint32_t h) {
     c->sky_w = w;
     c->sky_h = h;
     c->sky_total_bytes = (uint32_t)total;
+    c->sky_pairs_off = (uint32_t)pairs_off;
     for (int l = 0; l < geo_ctx::kSkyLevels; ++l) {
         c->sky_lvl_w[l] = lw[l];
         c->sky_lvl_h[l] = lh[l];
@@ -1576,6 +1616,8 @@ static int render_impl(geo_ctx* c, const geo_frame* frames, uint32_t nframes, si
     a.sky_wf = (float)c->sky_w;
     a.sky_hf = (float)c->sky_h;
     a.sky_total_bytes = c->sky_total_bytes;
+    a.sky_pairs_off = c->sky_pairs_off;
+    a.sky_pairs_pitch = (c->sky_w + 2u) * 8u;
     a.tile_order = nullptr;
     a.tile_cost = nullptr;
     a.cost_overhead = adaptive ? kCostOverheadAdaptive : kCostOverheadDirect;

@@ -75,10 +75,21 @@ extern "C" int host_render(const geo_frame* f, const geo_scene* s, const float* 
 // against WrapClampQuad on the unpadded texture: the sampled RGBA of n (U, V)
 // pairs both ways.
 extern "C" int host_sample_padded(const uint32_t* sky, uint32_t sw, uint32_t sh, const float* U, const float* V,
-                                  uint32_t n, uint32_t* out_wrap, uint32_t* out_pad) {
+                                  uint32_t n, uint32_t* out_wrap, uint32_t* out_pad, uint32_t* out_pair) {
     uint32_t* pad = new uint32_t[((size_t)sw + 2) * ((size_t)sh + 2)];
     geo::pad_sky(reinterpret_cast<const uint8_t*>(sky), sw, sh, pad);
     const uint32_t pitch = sw + 2u;
+    // the row pairs the device reads (geo::pair_sky_rows, PairSkyQuad): the
+    // quad at padded (x, y) is the 4 texels from 2 (y pitch + x)
+    uint32_t* pairs = new uint32_t[2 * ((size_t)sw + 2) * ((size_t)sh + 1)];
+    geo::pair_sky_rows(pad, sw, sh, pairs);
+    auto paired = [pairs, pitch](int ix0, int iy0, uint32_t (&t)[4]) {
+        const size_t i = 2 * ((size_t)(iy0 + 1) * pitch + (size_t)(ix0 + 1));
+        t[0] = pairs[i];
+        t[2] = pairs[i + 1];
+        t[1] = pairs[i + 2];
+        t[3] = pairs[i + 3];
+    };
     auto padded = [pad, pitch](int ix0, int iy0, uint32_t (&t)[4]) {
         const size_t i = (size_t)(iy0 + 1) * pitch + (size_t)(ix0 + 1);
         t[0] = pad[i];
@@ -90,8 +101,10 @@ extern "C" int host_sample_padded(const uint32_t* sky, uint32_t sw, uint32_t sh,
     for (uint32_t i = 0; i < n; ++i) {
         out_wrap[i] = geo::sample_sky_raw(fetch, sw, sh, U[i], V[i]);
         out_pad[i] = geo::sample_sky_quad(padded, sw, sh, U[i], V[i]);
+        out_pair[i] = geo::sample_sky_quad(paired, sw, sh, U[i], V[i]);
     }
     delete[] pad;
+    delete[] pairs;
     return 0;
 }
 

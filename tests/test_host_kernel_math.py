@@ -194,7 +194,8 @@ def test_composite_over_clear_equals_plain_draw():
 @pytest.mark.parametrize("sw,sh", [(1, 1), (2, 1), (7, 5), (64, 32), (513, 257)])
 def test_padded_sky_quad_equals_wrap_clamp(host, sw, sh):
     """The device's sky sampling reads a padded copy (geo::pad_sky, 2 x 2 block
-    at (ix0 + 1, iy0 + 1)); it must sample exactly what the wrap/clamp quad on
+    at (ix0 + 1, iy0 + 1); level 0 as its row pairs, geo::pair_sky_rows, one
+    16-byte quad); it must sample exactly what the wrap/clamp quad on
     the unpadded texture does: random (U, V), the edges and corners, and the
     texel centres next to them."""
     rng = np.random.default_rng(sw * 1000 + sh)
@@ -204,10 +205,13 @@ def test_padded_sky_quad_equals_wrap_clamp(host, sw, sh):
     V = np.concatenate([rng.random(4000, dtype=np.float32), np.tile(edge, edge.size)]).astype(np.float32)
     a = np.empty(U.size, np.uint32)
     b = np.empty(U.size, np.uint32)
+    c = np.empty(U.size, np.uint32)
     vp = ctypes.c_void_p
     host.host_sample_padded(vp(sky.ctypes.data), ctypes.c_uint32(sw), ctypes.c_uint32(sh), vp(U.ctypes.data),
-                            vp(V.ctypes.data), ctypes.c_uint32(U.size), vp(a.ctypes.data), vp(b.ctypes.data))
+                            vp(V.ctypes.data), ctypes.c_uint32(U.size), vp(a.ctypes.data), vp(b.ctypes.data),
+                            vp(c.ctypes.data))
     assert np.array_equal(a, b)
+    assert np.array_equal(a, c)  # the row-pair copy the device reads (geo::pair_sky_rows)
 
 
 def test_host_transcendentals_equal_oracle(host):

@@ -1298,7 +1298,7 @@ def ring_record(g, ctx, frame, scene, sky, W, H, args, flops_of, dev):
         "matches_cpu": {"ok": bool(same), "rows": [rows[0], rows[-1]],
                         "what": "GPU rows vs geo_render_cpu's (geo_band.h on the host) through the band: RGBA, "
                                 "mask, UV bits, steps"},
-        "what": "GEO_FLAG_RING_F64: the capture band's lanes (|b/b_c - 1| < 8e-3 by the f32 ray) integrate in f64 "
+        "what": "GEO_FLAG_RING_F64: the capture band's lanes (|b/b_c - 1| < 5e-3 by the f32 ray) integrate in f64 "
                 "inside the render kernel; ms_per_step and plain_ms_per_step are the best of 3 interleaved "
                 "runs of `frames` frames each (one launch per frame, one stream; at least the line's K and "
                 "about 25 ms of plain frames)",

@@ -43,12 +43,13 @@
 extern "C" {
 #endif
 
-#define GEO_ABI_VERSION 7  /* 4: geo_render_band_set_frames, geo_assemble_shares;
+#define GEO_ABI_VERSION 8  /* 4: geo_render_band_set_frames, geo_assemble_shares;
                                 5: geo_render_band_set_batch, geo_dispatch_stats;
                                 6: GEO_FLAG_RING_F64;
                                 7: GEO_FLAG_RING_F64 inside the render kernel (any stream,
                                    no context memory), in GEO_MODE_ADAPTIVE too; steps_total
-                                   counts the band's f64 steps */
+                                   counts the band's f64 steps;
+                                8: GEO_RING_X 5e-3 (was 8e-3) */
 
 typedef enum geo_status {
     GEO_OK = 0,
@@ -105,7 +106,7 @@ typedef enum geo_status {
                                    no state in the context.  Not with GEO_MODE_FAN,
                                    GEO_FLAG_COMPOSITE, GEO_FLAG_MIPS or more than one frame
                                    (GEO_EINVAL). */
-#define GEO_RING_X 8e-3f
+#define GEO_RING_X 5e-3f  /* (8e-3 before ABI 8; tools/ring_width_margin.py) */
 
 /* Observer motion states, ObserverState (SR/simulation/observer.rs:12-16). */
 #define GEO_OBSERVER_UNMOVING 0

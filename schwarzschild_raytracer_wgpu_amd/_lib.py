@@ -30,7 +30,7 @@ GEO_FLAG_DEFER_STEPS = 1
 GEO_FLAG_COMPOSITE = 2
 GEO_FLAG_MIPS = 4
 GEO_FLAG_RING_F64 = 8
-GEO_RING_X = 8e-3
+GEO_RING_X = 5e-3
 GEO_MAX_BATCH_FRAMES = 8
 
 GEO_RAYS_NEAR = 1

@@ -37,7 +37,7 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_abi_and_status():
-    assert _lib.lib.geo_abi_version() == 7
+    assert _lib.lib.geo_abi_version() == 8
     assert _lib.status_str(0) == "ok"
     assert "invalid" in _lib.status_str(-1)
 

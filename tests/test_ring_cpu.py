@@ -39,7 +39,7 @@ def test_ring_band_follows_the_orbit_and_only_applies_outside_the_horizon():
     for s in (make_scene(0.0, 50.0, 2.5, math.pi / 100, 64, GEO_MODE_DIRECT),
               make_scene(1.0, 50.0, 0.7, math.pi / 100, 64, GEO_MODE_DIRECT)):
         assert O.ring_band(frame, _ring(s), w, h).sum() == 0
-    assert GEO_RING_X == 8e-3
+    assert GEO_RING_X == 5e-3
 
 
 def test_ring_render_is_f32_outside_and_f64_inside():

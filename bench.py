@@ -102,8 +102,7 @@ def parse():
                         "the metric's line is the level-0 path")
     p.add_argument("--ring-f64", action="store_true",
                    help="GEO_FLAG_RING_F64 on every frame: the capture band's lanes integrate in f64 inside the "
-                        "render kernel (direct or adaptive mode, one frame per launch: at N > 1 or with --share "
-                        "add --batch-launch off).  Without it an N = 1 "
+                        "render kernel (direct or adaptive mode; batched launches too).  Without it an N = 1 "
                         "direct/adaptive line still measures the mode beside the metric, as its `ring_f64` record")
     p.add_argument("--no-ring-record", action="store_true", help="skip the `ring_f64` record")
     p.add_argument("--no-frame-check", action="store_true",
@@ -337,14 +336,8 @@ def main():
     tol = cfg.tol if mode == g.GEO_MODE_ADAPTIVE else 0.0
     sampler_flags = g._lib.GEO_FLAG_MIPS if args.mips else 0
     if args.ring_f64:
-        # one frame per launch (geo.h): at N = 1 no --frames-per-launch; a
-        # band-set layout (N > 1 or --share) renders each frame's bands in
-        # its own launch only with --batch-launch off
-        batched = (args.frames_per_launch > 1 if lay_world == 1
-                   else args.batch_launch != "off" and args.frames_per_gather > 1)
-        if mode == g.GEO_MODE_FAN or args.mips or batched:
-            raise SystemExit("--ring-f64: direct or adaptive mode, level-0 sampler, one frame per launch "
-                             "(--frames-per-launch 1; at N > 1 or with --share, --batch-launch off) (geo.h)")
+        if mode == g.GEO_MODE_FAN or args.mips:
+            raise SystemExit("--ring-f64: direct or adaptive mode, level-0 sampler (geo.h)")
         sampler_flags |= g._lib.GEO_FLAG_RING_F64
     scene = g.make_scene(cfg.rs, cfg.sphere_r, obs.get_radial_position(), cfg.step, cfg.max_steps, mode,
                          flags=sampler_flags, tol=tol)

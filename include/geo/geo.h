@@ -49,7 +49,8 @@ extern "C" {
                                 7: GEO_FLAG_RING_F64 inside the render kernel (any stream,
                                    no context memory), in GEO_MODE_ADAPTIVE too; steps_total
                                    counts the band's f64 steps;
-                                8: GEO_RING_X 5e-3 (was 8e-3) */
+                                8: GEO_RING_X 5e-3 (was 8e-3); GEO_FLAG_RING_F64 in batched
+                                   launches (geo_render_band_set_frames / _batch) */
 
 typedef enum geo_status {
     GEO_OK = 0,
@@ -102,9 +103,11 @@ typedef enum geo_status {
                                    the f32 roundings (and, in the adaptive mode, its
                                    tolerance) past the 1e-4 UV bar.  The
                                    band's out_steps and steps_total are its f64 steps.  A
-                                   ring render launches one wave per workgroup and keeps
-                                   no state in the context.  Not with GEO_MODE_FAN,
-                                   GEO_FLAG_COMPOSITE, GEO_FLAG_MIPS or more than one frame
+                                   one-frame ring render launches one wave per workgroup; a
+                                   batch (geo_render_band_set_frames / _batch) carries each
+                                   frame's band factor and derives its constants on the
+                                   device; no state is kept in the context.  Not with
+                                   GEO_MODE_FAN, GEO_FLAG_COMPOSITE or GEO_FLAG_MIPS
                                    (GEO_EINVAL). */
 #define GEO_RING_X 5e-3f  /* (8e-3 before ABI 8; tools/ring_width_margin.py) */
 

@@ -59,9 +59,27 @@ struct BandConsts {
 #endif
 GEO_HD bool in_band(float kx, float ct) { return __builtin_fabsf(kx * ct - 1.0f) < GEO_BAND_X; }
 
-// Host: the constants for a frame and scene with rs > 0 and r_obs > rs.
-inline BandConsts band_consts(const geo_frame& f, const geo_scene& s, uint32_t width, uint32_t height) {
-    BandConsts k;
+// kx = r / (E b_c) rounded once: the band test's factor (rs > 0, r_obs > rs).
+GEO_HD float band_kx(float rs, float r_obs) {
+    const double r = (double)r_obs, rsd = (double)rs;
+    return (float)(r / (__builtin_sqrt(1.0 - rsd / r) * (1.5 * __builtin_sqrt(3.0) * rsd)));
+}
+
+// The next double above a positive finite x (nextafter(x, +inf)).
+GEO_HD double next_up_pos_(double x) {
+    uint64_t b;
+    __builtin_memcpy(&b, &x, 8);
+    ++b;
+    __builtin_memcpy(&x, &b, 8);
+    return x;
+}
+
+// The constants for a frame and scene with rs > 0 and r_obs > rs, written
+// field by field into k (on the device: a wave's LDS slot, so that a batched
+// launch derives each frame's constants where it needs them; the same IEEE
+// f64 operations on the host and the device).
+GEO_HD void band_consts_into(BandConsts& k, const geo_frame& f, float rs_f, float sphere_r_f, float r_obs_f,
+                             float step_f, uint32_t max_steps, uint32_t width, uint32_t height) {
     const float* m0 = f.display_to_movement;
     const double w = (double)width, hgt = (double)height;
     const double sx = 2.0 / w, ox = (1.0 - w) / w, sy = -2.0 / hgt, oy = (hgt - 1.0) / hgt;
@@ -80,9 +98,10 @@ inline BandConsts band_consts(const geo_frame& f, const geo_scene& s, uint32_t w
                      m1[6] == 0.0f && m1[8] == 0.0f && m1[9] == 0.0f && m1[10] == 1.0f)
                         ? 1u
                         : 0u;
-    k.k = (double)f.psi_factor_and_position[0];
-    k.kt = __builtin_sqrt(1.0 - k.k * k.k);
-    const double rs = (double)s.rs, sr = (double)s.sphere_r, r = (double)s.r_obs, step = (double)s.step;
+    const double psi = (double)f.psi_factor_and_position[0];
+    k.k = psi;
+    k.kt = __builtin_sqrt(1.0 - psi * psi);
+    const double rs = (double)rs_f, sr = (double)sphere_r_f, r = (double)r_obs_f, step = (double)step_f;
     k.r = r;
     k.energy = __builtin_sqrt(1.0 - rs / r);
     k.hor = (1.0 - rs / r) / (r * r);
@@ -98,17 +117,18 @@ inline BandConsts band_consts(const geo_frame& f, const geo_scene& s, uint32_t w
     const double c = r3_2;
     k.scale = c;
     const double u0 = 1.0 / r;
-    k.U0 = c * u0;
-    k.SU = c / sr;
+    const double U0 = c * u0, SU = c / sr, HU = c / rs;
+    k.U0 = U0;
+    k.SU = SU;
     k.BD = c * (0.9 * __builtin_fmin(u0, 1.0 / __builtin_fmax(sr, r3_2)));
-    k.HU = c / rs;
-    k.above0 = k.U0 > k.SU ? 1u : 0u;
-    if (k.above0) {  // inside the sphere: stops below SU (crossing, escape) or above HU (horizon)
-        k.lo = __builtin_nextafter(k.SU, __builtin_inf());
-        k.hi = k.HU;
+    k.HU = HU;
+    k.above0 = U0 > SU ? 1u : 0u;
+    if (U0 > SU) {  // inside the sphere: stops below SU (crossing, escape) or above HU (horizon)
+        k.lo = next_up_pos_(SU);
+        k.hi = HU;
     } else {  // outside it: stops above SU (crossing, horizon) or below BD (escape)
         k.lo = k.BD;
-        k.hi = __builtin_fmin(k.SU, k.HU);
+        k.hi = __builtin_fmin(SU, HU);
     }
     k.h = step;
     k.hh = step / 2.0;
@@ -116,8 +136,14 @@ inline BandConsts band_consts(const geo_frame& f, const geo_scene& s, uint32_t w
     k.hhh = step * step / 2.0;
     k.h6 = step / 6.0;
     k.h2_6 = step * step / 6.0;
-    k.kx = (float)(r / (__builtin_sqrt(1.0 - rs / r) * (1.5 * __builtin_sqrt(3.0) * rs)));
-    k.max_steps = s.max_steps;
+    k.kx = band_kx(rs_f, r_obs_f);
+    k.max_steps = max_steps;
+}
+
+// Host: the constants for a frame and scene with rs > 0 and r_obs > rs.
+inline BandConsts band_consts(const geo_frame& f, const geo_scene& s, uint32_t width, uint32_t height) {
+    BandConsts k;
+    band_consts_into(k, f, s.rs, s.sphere_r, s.r_obs, s.step, s.max_steps, width, height);
     return k;
 }
 

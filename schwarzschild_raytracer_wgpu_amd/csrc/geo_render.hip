@@ -85,6 +85,7 @@ template <uint32_t NF>
 struct FrameBatch {
     FrameK f[NF];
     geo::PixelConsts k[NF];
+    float ring_kx[NF];  // GEO_FLAG_RING_F64: frame z's band factor (geo::band_kx; 0: no band)
 };
 template <>
 struct FrameBatch<1> {
@@ -342,7 +343,7 @@ constexpr bool kAdaptiveWaveBlocks = true;
 constexpr bool kAdaptiveWaveBlocks = false;
 #endif
 __host__ __device__ constexpr bool wave_blocks(int mode, bool mips, uint32_t nf, bool ring) {
-    return (ring && kRingWaveBlocks) ||
+    return (ring && kRingWaveBlocks && nf == 1) ||
            (!mips && nf == 1 &&
             ((kDirectWaveBlocks && mode == GEO_MODE_DIRECT) || (kAdaptiveWaveBlocks && mode == GEO_MODE_ADAPTIVE)));
 }
@@ -520,7 +521,7 @@ __device__ __forceinline__ void fan_tile(const RenderArgs& a, const FrameK& f, s
 // take their traveled angle from the f64 path instead of the f32 one.
 template <int MODE, int KIND, bool MIPS, uint32_t NF, bool RING>
 __global__ __launch_bounds__(kBlock) void geo_render_kernel(const RenderArgs a, const FrameBatch<NF> fb,
-                                                            const BandArg<RING> bk) {
+                                                            const BandArg<RING && NF == 1> bk) {
 #if defined(GEO_WAVE_LOG)
     const unsigned long long t_wave0 = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -557,9 +558,12 @@ __global__ __launch_bounds__(kBlock) void geo_render_kernel(const RenderArgs a, 
         tile = make_uint2(blockIdx.x, a.tile_y0 + blockIdx.y);
     }
     const uint32_t lane = threadIdx.x & 63u;
-    // RING: the band's constants in LDS (kBandDwords)
-    __shared__ double band_lds[RING ? kBandDwords / 2u : 1u];
-    if constexpr (RING) {
+    // RING: the band's constants in LDS (kBandDwords): a one-frame launch
+    // copies them from its kernel arguments; a batched launch (RB) derives
+    // frame z's in a wave's own slot when the wave has band lanes
+    constexpr bool RB = RING && NF > 1;
+    __shared__ double band_lds[RING ? (RB ? kBlock / 64u : 1u) * (kBandDwords / 2u) : 1u];
+    if constexpr (RING && NF == 1) {
         // one 8-byte word per thread (kBandDwords / 2 <= 64)
         if (threadIdx.x < kBandDwords / 2u)
             reinterpret_cast<uint2*>(band_lds)[threadIdx.x] = reinterpret_cast<const uint2*>(&bk.k)[threadIdx.x];
@@ -599,8 +603,14 @@ __global__ __launch_bounds__(kBlock) void geo_render_kernel(const RenderArgs a, 
                 // the band's lanes skip the f32 integration (its loop runs on
                 // the other lanes) and take lambda' and the mask from the f64
                 // path; both then draw the sky from the f32 ray
-                const geo::BandConsts& bkl = *reinterpret_cast<const geo::BandConsts*>(band_lds);
-                const bool band = geo::in_band(bkl.kx, ct);
+                double* const bslot = band_lds + (RB ? wave * (kBandDwords / 2u) : 0u);
+                const geo::BandConsts& bkl = *reinterpret_cast<const geo::BandConsts*>(bslot);
+                float kx;
+                if constexpr (RB)
+                    kx = fb.ring_kx[z];
+                else
+                    kx = bkl.kx;
+                const bool band = geo::in_band(kx, ct);
 #if defined(GEO_RING_PRIO)  // A/B variant: a wave with band lanes issues first
                 if (geo::ballot_(band) != 0) __builtin_amdgcn_s_setprio(GEO_RING_PRIO);
 #endif
@@ -611,6 +621,20 @@ __global__ __launch_bounds__(kBlock) void geo_render_kernel(const RenderArgs a, 
                     bh = lam < geo::kBlackHoleLambda;
                 }
                 if (geo::ballot_(band) != 0) {
+                    if constexpr (RB) {
+                        // frame z's constants, written by the wave's first
+                        // active lane (lanes outside the frame are off here)
+                        // into the wave's slot (the same f64 operations as the
+                        // host's geo::band_consts), then read by the band's lanes
+                        if (lane == (uint32_t)__builtin_amdgcn_readfirstlane((int)lane)) {
+                            const geo::PixelConsts& kz = fb.k[z];
+                            geo::band_consts_into(*reinterpret_cast<geo::BandConsts*>(bslot), f.frame, kz.rs,
+                                                  kz.sphere_r, kz.r, kz.step, kz.max_steps, a.width, a.height);
+                        }
+                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                        __builtin_amdgcn_wave_barrier();
+                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                    }
                     if (band) {
                         GEO_COLD_ARM();
                         const double l = geo::band_lambda(bkl, px, py, &steps);
@@ -1442,8 +1466,17 @@ static int launch_tiles(RenderArgs a, const FrameBatch<NF>& fb, uint32_t nframes
                 hipExtLaunchKernelGGL((geo_render_kernel<MODE, KIND, false, 1, false>), grid, dim3(kBlock), 0, s,
                                       start, stop, 0, a, fb, BandArg<false>{});
         } else {
-            hipExtLaunchKernelGGL((geo_render_kernel<MODE, KIND, false, NF, false>), grid, dim3(kBlock), 0, s, start,
-                                  stop, 0, a, fb, BandArg<false>{});
+            bool done_ring = false;
+            if constexpr (MODE != GEO_MODE_FAN && KIND != geo::kFlat) {
+                if (band) {  // GEO_FLAG_RING_F64 in a batch: fb.ring_kx, the constants derived per wave
+                    hipExtLaunchKernelGGL((geo_render_kernel<MODE, KIND, false, NF, true>), grid, dim3(kBlock), 0, s,
+                                          start, stop, 0, a, fb, BandArg<false>{});
+                    done_ring = true;
+                }
+            }
+            if (!done_ring)
+                hipExtLaunchKernelGGL((geo_render_kernel<MODE, KIND, false, NF, false>), grid, dim3(kBlock), 0, s,
+                                      start, stop, 0, a, fb, BandArg<false>{});
         }
         if (hipGetLastError() != hipSuccess) return GEO_EHIP;
     }
@@ -1454,7 +1487,9 @@ static int launch_tiles(RenderArgs a, const FrameBatch<NF>& fb, uint32_t nframes
 // One frame (FrameBatch<1>, the kernel arguments as before batching), or a
 // batch of 2 .. kMaxBatchFrames in one launch (FrameBatch<kMaxBatchFrames>,
 // the frame in blockIdx.z; no mip-mapped sampler).  band: GEO_FLAG_RING_F64's
-// constants (one frame), or null.
+// constants (frame 0), or null; a batch carries each frame's band factor
+// (ring_kx, 0 where the frame has no capture orbit) and its kernel derives
+// the constants per wave from the frame and its scene constants.
 static_assert(sizeof(RenderArgs) + sizeof(FrameBatch<kMaxBatchFrames>) <= 4096, "kernel arguments fit 4 KiB");
 static_assert(sizeof(RenderArgs) + sizeof(FrameBatch<1>) + sizeof(BandArg<true>) <= 4096,
               "kernel arguments fit 4 KiB");
@@ -1472,9 +1507,10 @@ static int launch_frames(const RenderArgs& a, const FrameK* fk, const geo::Pixel
     for (uint32_t i = 0; i < nframes; ++i) {
         fb.f[i] = fk[i];
         fb.k[i] = pk[i];
+        fb.ring_kx[i] = (band && pk[i].rs > 0.0f && pk[i].r > pk[i].rs) ? geo::band_kx(pk[i].rs, pk[i].r) : 0.0f;
     }
     return launch_tiles<MODE, KIND, kMaxBatchFrames>(a, fb, nframes, false, tiles_x, tiles_y, s, done, t_start,
-                                                     t_stop, nullptr);
+                                                     t_stop, band);
 }
 }
 
@@ -1537,8 +1573,7 @@ static int render_impl(geo_ctx* c, const geo_frame* frames, uint32_t nframes, si
     if ((scene->flags & ~(GEO_FLAG_DEFER_STEPS | GEO_FLAG_COMPOSITE | GEO_FLAG_MIPS | GEO_FLAG_RING_F64)) != 0)
         return GEO_EINVAL;
     const bool ring_flag = (scene->flags & GEO_FLAG_RING_F64) != 0;
-    if (ring_flag && (scene->mode == GEO_MODE_FAN || nframes != 1 ||
-                      (scene->flags & (GEO_FLAG_COMPOSITE | GEO_FLAG_MIPS)) != 0))
+    if (ring_flag && (scene->mode == GEO_MODE_FAN || (scene->flags & (GEO_FLAG_COMPOSITE | GEO_FLAG_MIPS)) != 0))
         return GEO_EINVAL;
     // frame-aligned 2 x 2 quads: the rows a wave covers start on even frame rows
     const bool mips = (scene->flags & GEO_FLAG_MIPS) != 0;
@@ -1642,7 +1677,9 @@ static int render_impl(geo_ctx* c, const geo_frame* frames, uint32_t nframes, si
     }
     // GEO_FLAG_RING_F64 (geo_band.h): the band's lanes take the f64 path; no
     // capture orbit (rs = 0, or the observer inside the horizon): the plain draw
-    const bool ring = ring_flag && scene->rs > 0.0f && scene->r_obs > scene->rs;
+    bool ring = ring_flag && scene->rs > 0.0f && scene->r_obs > scene->rs;
+    if (ring_flag && scene_per_frame)  // a batch: any frame with a capture orbit (each gets its own factor)
+        for (uint32_t i = 1; i < nframes; ++i) ring = ring || (scene[i].rs > 0.0f && scene[i].r_obs > scene[i].rs);
     const int slot = render_slot(c, s);
     if (slot < 0) return GEO_EHIP;
     const hipEvent_t done = c->render_done[slot];
@@ -1696,8 +1733,8 @@ static int render_impl(geo_ctx* c, const geo_frame* frames, uint32_t nframes, si
             if (c->order_cur >= 0) a.tile_order = c->order[c->order_cur];
         }
     }
-    geo::BandConsts band_k;
-    if (ring) band_k = geo::band_consts(frames[0], *scene, width, height);
+    geo::BandConsts band_k;  // (one frame; a batch derives its frames' constants on the device)
+    if (ring && nframes == 1) band_k = geo::band_consts(frames[0], *scene, width, height);
     const geo::BandConsts* band = ring ? &band_k : nullptr;
     int st;
     if (scene->mode == GEO_MODE_FAN) {

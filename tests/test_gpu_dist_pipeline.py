@@ -384,13 +384,12 @@ def test_timed_step_of_a_rank_without_rows():
 
 
 @pytest.mark.parametrize("world,K,lead", [(2, 4, 1), (4, 3, (3, 2)), (8, 2, 2)])
-def test_rank0_pipeline_ring_f64_per_frame(world, K, lead):
+def test_rank0_pipeline_ring_f64(world, K, lead):
     """GEO_FLAG_RING_F64 through the multi-GPU pipeline (bench.py --ring-f64
-    --batch-launch off at N > 1): each frame's bands render in their own launch
-    with the capture band in f64, and rank 0's assembled frames equal the
-    single-launch ring frame byte for byte (the band's pixels are per pixel,
-    whatever the band layout or dispatch order); a batched band-set launch
-    refuses the flag (geo.h: one frame per launch)."""
+    at N > 1): each frame's bands in their own launch, and each batch's frames
+    in one launch, with the capture band in f64; rank 0's assembled frames
+    equal the single-launch ring frame byte for byte (the band's pixels are
+    per pixel, whatever the band layout, batch or dispatch order)."""
     import torch
 
     if not torch.cuda.is_available():
@@ -431,10 +430,16 @@ def test_rank0_pipeline_ring_f64_per_frame(world, K, lead):
     sf.drain()
     torch.cuda.synchronize()
     assert torch.equal(sf.frame_rgba(), ref)
-    # one launch for several frames: refused
-    L = BandLayout(H, B, world, 0, lead, pb)
-    out = torch.empty(2 * L.nbands() * L.band_height() * W * 4, dtype=torch.uint8, device=dev)
-    with pytest.raises(g.GeoError) as e:
-        ctx.render_band_set_frames([frame, frame], scene, W, H, L.band_height(), L.row0(), L.cycle_rows, L.nbands(),
-                                   out)
-    assert e.value.status == -1  # GEO_EINVAL
+    # batched: each batch's frames in one launch, the same frames
+    fake2 = FakeRcclGather(torch, fake.peer_bufs)
+    sf2 = ShardedFrame(ctx, frame, scene, W, H, B, 0, world, dev, dist=fake2, frames_per_gather=K, render_streams=2,
+                       present_rgb=True, lead=lead, batch_launch=True, peer_bands=pb)
+    assert sf2.batch == (K > 1)
+    for i in range(nframes):
+        sf2.step(i)
+    sf2.drain()
+    torch.cuda.synchronize()
+    assert torch.equal(sf2.frame_rgba(), ref)
+    last_n = nframes - (math.ceil(nframes / K) - 1) * K
+    for k in range(last_n):
+        assert torch.equal(sf2.frame_rgba(k), ref), k

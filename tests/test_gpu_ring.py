@@ -276,9 +276,9 @@ def test_ring_rejects_what_it_does_not_draw(geo, torch_mod):
         s = _ring(geo, default_scene(64))
         s.flags |= flag
         assert rows(s) == _lib.GEO_EINVAL, flag
-    fa = (geo.GeoFrame * 2)(frame, frame)
+    fa = (geo.GeoFrame * 2)(frame, frame)  # a batch draws the band too (test_ring_batched_launches_...)
     assert _lib.lib.geo_render_band_set_frames(ctx._h, fa, 2, ctypes.byref(ok), w, h, 8, 0, 8, 4, out.data_ptr(),
-                                               h * w * 4, None, stream) == _lib.GEO_EINVAL
+                                               h * w * 4, None, stream) == _lib.GEO_OK
     # no capture orbit (flat space, inside the horizon): the flag draws the f32 frame
     for s in (geo.make_scene(0.0, 50.0, 2.5, math.pi / 100, 64, geo.GEO_MODE_DIRECT),
               geo.make_scene(1.0, 50.0, 0.7, math.pi / 100, 64, geo.GEO_MODE_DIRECT)):
@@ -324,3 +324,73 @@ def test_ring_across_streams_and_sizes(geo, torch_mod):
         assert torch.equal(out, refs[k]), k
     ctx.close()
     ref_ctx.close()
+
+
+@pytest.mark.parametrize("mode", ["direct", "adaptive"])
+def test_ring_batched_launches_equal_one_frame_launches(geo, torch_mod, mode):
+    """GEO_FLAG_RING_F64 in batched launches (the multi-GPU pipeline's
+    geo_render_band_set_frames / _batch): each frame's band factor rides in
+    the batch and a wave with band lanes derives its frame's f64 constants
+    (geo::band_consts_into, the host's operations) in its LDS slot.  Every
+    frame of the batch equals its one-frame ring render byte for byte: three
+    cameras in one launch, and a moving observer's frames (one radius each,
+    one inside the photon sphere) through geo_render_band_set_batch; band
+    layouts with a partial last band."""
+    import ctypes
+
+    from schwarzschild_raytracer_wgpu_amd import _lib
+    from schwarzschild_raytracer_wgpu_amd.scenes import make_sky
+
+    torch = torch_mod
+    dev = torch.device("cuda:0")
+    W, H, BR = 320, 180, 8
+    ctx = geo.Context(0)
+    ctx.set_sky(make_sky("equirect", (256, 128)))
+    md = geo.GEO_MODE_ADAPTIVE if mode == "adaptive" else geo.GEO_MODE_DIRECT
+    stream = torch.cuda.current_stream().cuda_stream
+
+    def frame_at(pos, cam):
+        obs = geo.Observer(1.0, math.pi / 2, W, H)
+        obs.set_position(*pos)
+        obs.set_camera(*cam)
+        return obs.calc_transformation_pipeline(), obs.get_radial_position()
+
+    def one(frame, scene, row0, stride, nb):
+        o = torch.zeros(nb * BR * W * 4, dtype=torch.uint8, device=dev)
+        ctx.render_band_set(frame, scene, W, H, BR, row0, stride, nb, o)
+        return o
+
+    for row0, stride, nb in ((0, 8, 23), (8, 24, 8), (16, 32, 6)):
+        fb = nb * BR * W * 4
+        # three cameras, one scene, one launch
+        poses = [frame_at((2.5, 0.0, 0.1), (math.pi + d, 0.0)) for d in (0.0, 0.02, -0.03)]
+        scene = _ring(geo, geo.make_scene(1.0, 50.0, poses[0][1], math.pi / 100, 512, md,
+                                          tol=1e-6 if md == geo.GEO_MODE_ADAPTIVE else 0.0))
+        out = torch.zeros(3 * fb, dtype=torch.uint8, device=dev)
+        fa = (geo.GeoFrame * 3)(*[p[0] for p in poses])
+        assert _lib.lib.geo_render_band_set_frames(ctx._h, fa, 3, ctypes.byref(scene), W, H, BR, row0, stride, nb,
+                                                   out.data_ptr(), fb, None, stream) == _lib.GEO_OK
+        for i, (fr, _) in enumerate(poses):
+            assert torch.equal(out[i * fb:(i + 1) * fb], one(fr, scene, row0, stride, nb)), (row0, i)
+        # a moving observer: one radius per frame (outside and inside the photon sphere)
+        poses = [frame_at((r, 0.0, 0.1), (math.pi, 0.0)) for r in (2.5, 1.3, 4.0)]
+        scenes = [_ring(geo, geo.make_scene(1.0, 50.0, rr, math.pi / 100, 512, md,
+                                            tol=1e-6 if md == geo.GEO_MODE_ADAPTIVE else 0.0)) for _, rr in poses]
+        sa = (geo.GeoScene * 3)(*scenes)
+        fa = (geo.GeoFrame * 3)(*[p[0] for p in poses])
+        out = torch.zeros(3 * fb, dtype=torch.uint8, device=dev)
+        assert _lib.lib.geo_render_band_set_batch(ctx._h, fa, sa, 3, W, H, BR, row0, stride, nb, out.data_ptr(), fb,
+                                                  None, stream) == _lib.GEO_OK
+        for i, (fr, _) in enumerate(poses):
+            ref = one(fr, scenes[i], row0, stride, nb)
+            assert torch.equal(out[i * fb:(i + 1) * fb], ref), (row0, i)
+        # the band is in these frames: the ring frames differ from plain ones
+        plain = geo.GeoScene.from_buffer_copy(bytes(scenes[0]))
+        plain.flags &= ~_lib.GEO_FLAG_RING_F64
+        uv_r = torch.empty(nb * BR * W * 2, dtype=torch.float32, device=dev)
+        uv_p = torch.empty(nb * BR * W * 2, dtype=torch.float32, device=dev)
+        tmp = torch.empty(nb * BR * W * 4, dtype=torch.uint8, device=dev)
+        ctx.render_band_set(poses[0][0], scenes[0], W, H, BR, row0, stride, nb, tmp, out_uv=uv_r)
+        ctx.render_band_set(poses[0][0], plain, W, H, BR, row0, stride, nb, tmp, out_uv=uv_p)
+        torch.cuda.synchronize()
+        assert int((uv_r != uv_p).sum().item()) > 0

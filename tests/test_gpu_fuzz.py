@@ -140,8 +140,8 @@ def test_gpu_fuzz_batch_bitexact(geo, torch_mod):  # noqa: F811
     """geo_render_band_set_batch on seeded random batches: ragged frames,
     1..8 frames per launch, each frame's own uniform and observer radius
     (same side of the horizon; one radius in fan mode), random band layouts
-    (world 1..8, any rank, rank 0's taller bands), a gap between frames.
-    Every frame's packed bands == geo_render_band_set of that frame alone
+    (world 1..8, any rank, rank 0's taller bands), a gap between frames,
+    GEO_FLAG_RING_F64 on half the direct/adaptive batches.  Every frame's packed bands == geo_render_band_set of that frame alone
     (bytes, the gap untouched, step totals), and one frame per batch ==
     the oracle's f32 restatement on its rows."""
     from schwarzschild_raytracer_wgpu_amd import _lib
@@ -174,6 +174,13 @@ def test_gpu_fuzz_batch_bitexact(geo, torch_mod):  # noqa: F811
                     r = max(r, 1.005 * scene0.rs)
                 s.r_obs = r
             scenes.append(s)
+        # GEO_FLAG_RING_F64 on every frame of half the direct/adaptive batches
+        # (each frame's band factor in the batch, its constants derived on the device)
+        ring = (mode != _lib.GEO_MODE_FAN and rng.random() < 0.5
+                and (scene0.flags & (_lib.GEO_FLAG_COMPOSITE | _lib.GEO_FLAG_MIPS)) == 0)
+        if ring:
+            for s in scenes:
+                s.flags |= _lib.GEO_FLAG_RING_F64
         fan = None
         if mode == _lib.GEO_MODE_FAN:
             fan = ctx.solve_ray_fan(scene0.sphere_r, scene0.rs, 1000, scene0.step, 400, scene0.r_obs)
@@ -193,7 +200,8 @@ def test_gpu_fuzz_batch_bitexact(geo, torch_mod):  # noqa: F811
         fa, sa = (geo.GeoFrame * n)(*frames), (geo.GeoScene * n)(*scenes)
         st = _lib.lib.geo_render_band_set_batch(ctx._h, fa, sa, n, w, h, band_h, row0, row_stride, nbands,
                                                 out.data_ptr(), stride, tot.data_ptr(), stream)
-        layout = f"n={n} world={world} rank={rank} band={band_h} row0={row0} stride={row_stride} nbands={nbands}"
+        layout = (f"n={n} world={world} rank={rank} band={band_h} row0={row0} stride={row_stride} nbands={nbands}"
+                  f" ring={ring}")
         if st != _lib.GEO_OK:
             bad.append((desc, layout, f"status {st}"))
             continue
